@@ -1,0 +1,282 @@
+#!/usr/bin/env python3
+"""Benchmark: APSP node-pairs/s (routing build, C2) + packets relayed/s per round (relay, C5).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one routing build of BASELINE config 2 (1000-node complete GML graph, 1000 used
+nodes) from the device-resident arc CSR to the full 1000 x 1000 (latency u64, loss f32) table
+resident in HBM.  At N > 1 the source rows are sharded over the ranks (no collective inside the
+SSSP) and the table is all-gathered over RCCL so every rank ends with the full table; the timed
+region includes that all-gather.  The relay leg times one round of config 5 (100k hosts, 10M
+packets) per step: stamp + loss draw + bucket + per-destination sort, inputs resident in HBM.
+Rank 0 prints ONE JSON line.  Timing: barrier + device sync on both sides of exactly K steps,
+max over ranks.  The CPU baseline (rank 0, N = 1) times the C restatement of the reference
+(oracle/c) on the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "APSP node-pairs/s + packets relayed/s per round, 1/2/4/8 MI355X"
+# integer VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md chip table)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+HBM_PEAK_GBS = 8000.0
+RELAY_BYTES_PER_PACKET = 84   # 24 rec + 12 path + 24 event + 24 sort r/w
+RELAY_BYTES_PER_HOST = 80     # RNG state + event id, read + write
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup(n_gpus):
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier_sync(world):
+    import torch
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def load_pmc(name):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(p):
+        return json.load(open(p)).get(name)
+    return None
+
+
+def routing_leg(eng, world, rank, steps, warmup):
+    import torch
+    from shadow_amd import _native as N
+    from shadow_amd import synth
+    from shadow_amd.routing import NetworkGraph
+    el = synth.complete_graph(1000, 1)
+    g = NetworkGraph(el.node_ids, el.src, el.dst, el.latency_ns, el.packet_loss, el.directed)
+    n = g.n_nodes
+    used = np.arange(n, dtype=np.uint32)
+    cg = g._cgraph()
+    err = N.Error()
+    N.check(eng.lib.shd_routing_prepare(eng.ctx, C.byref(cg), N.ptr(used), n, N.ROUTE_SHORTEST,
+                                        C.byref(err)), "prepare", err)
+    per = (n + world - 1) // world
+    rb, re = min(rank * per, n), min((rank + 1) * per, n)
+    full_lat = torch.empty((world * per, n), dtype=torch.int64, device="cuda")
+    full_loss = torch.empty((world * per, n), dtype=torch.float32, device="cuda")
+    shard_lat = full_lat[rank * per:(rank + 1) * per]
+    shard_loss = full_loss[rank * per:(rank + 1) * per]
+
+    def step():
+        if re > rb:
+            st = eng.lib.shd_routing_run(eng.ctx, N.ALGO_AUTO, rb, re, N.ptr(shard_lat), N.ptr(shard_loss),
+                                         C.byref(err))
+            N.check(st, "shd_routing_run", err)
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_gather_into_tensor(full_lat, shard_lat)
+            dist.all_gather_into_tensor(full_loss, shard_loss)
+
+    for _ in range(warmup):
+        step()
+    barrier_sync(world)
+    main_ms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+        main_ms.append(eng.last_info()["ms_main"])
+    barrier_sync(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    info = eng.last_info()
+    arcs = info["arcs"]
+    kernel_ms = float(np.mean(main_ms)) if main_ms else 0.0
+    kernel_ms = max_over_ranks(kernel_ms, world)
+    ops_per_launch = 2.0 * (re - rb) * arcs          # one add + one min per arc per source row
+    achieved = ops_per_launch / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+    return dict(n=n, arcs=arcs, dt=dt, ms_per_step=dt / steps * 1e3, kernel_ms=kernel_ms,
+                achieved=achieved, algo=info["algo_used"], arcs_kept=info["arcs_kept"],
+                lat=full_lat[:n].cpu().numpy().view(np.uint64), loss=full_loss[:n].cpu().numpy(), el=el)
+
+
+def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table):
+    import torch
+    from shadow_amd import _native as N
+    from shadow_amd import synth
+    H, P = 100_000, 10_000_000
+    start, runahead = synth.SIM_START + 10**9, 10**6
+    b = synth.packet_batch(H, P, start, start + runahead, seed=4)
+    host_node = synth.c5_host_nodes(H, 1000)
+    rng0 = synth.host_rng_states(H, 1)
+    nid0 = np.zeros(H, np.uint64)
+    N.check(eng.lib.shd_relay_setup(eng.ctx, H, N.ptr(host_node), 1000, N.ptr(lat_table),
+                                    N.ptr(loss_table), N.ptr(rng0), N.ptr(nid0)), "relay_setup")
+    dev = lambda a, dt: torch.from_numpy(a.view(dt)).cuda()  # noqa: E731
+    d_off = dev(b.src_off, np.int32)
+    d_time = dev(b.send_time, np.int64)
+    d_dst = dev(b.dst_host, np.int32)
+    d_pay = dev(b.payload, np.int32)
+    st = torch.empty(P, dtype=torch.uint8, device="cuda")
+    ev_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    ev_deliver = torch.empty(P, dtype=torch.int64, device="cuda")
+    ev_src = torch.empty(P, dtype=torch.int32, device="cuda")
+    ev_seq = torch.empty(P, dtype=torch.int64, device="cuda")
+    ev_pkt = torch.empty(P, dtype=torch.int32, device="cuda")
+    batch = N.Batch(P, N.ptr(d_off).value, N.ptr(d_time).value, N.ptr(d_dst).value,
+                    N.ptr(d_pay).value, None)
+    out = N.RelayOut(N.ptr(st).value, N.ptr(ev_off).value, N.ptr(ev_deliver).value,
+                     N.ptr(ev_src).value, N.ptr(ev_seq).value, N.ptr(ev_pkt).value, 0, 0, 0)
+    rd = N.Round(start + runahead, start + 10**12, 0)
+
+    def step():
+        N.check(eng.lib.shd_relay_round_device(eng.ctx, C.byref(batch), C.byref(rd), C.byref(out)),
+                "relay_round_device")
+
+    for _ in range(warmup):
+        step()
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier_sync(world)
+    dt = max_over_ranks(time.perf_counter() - t0, world)
+    return dict(H=H, P=P, dt=dt, ms_per_step=dt / steps * 1e3, n_sent=out.n_sent, batch=b,
+                host_node=host_node, rng0=rng0)
+
+
+def cpu_baseline_routing(el, budget_s=8.0):
+    from oracle import corc
+    used = np.arange(el.n_nodes, dtype=np.uint32)
+    threads = corc.max_threads()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        code, lat, loss, _ = corc.routing(el.n_nodes, el.src, el.dst, el.latency_ns, el.packet_loss,
+                                          el.directed, used, variant=corc.FAITHFUL, threads=threads)
+        reps += 1
+        if time.perf_counter() - t0 > budget_s or reps >= 20:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    return dict(value=el.n_nodes ** 2 / dt, unit="node-pairs/s", cores=threads, kind="port",
+                sample=f"{reps} full C2 builds (faithful variant: per-source heap Dijkstra + "
+                       f"Vec::contains filter + HashMap materialisation, OpenMP over sources)"), lat
+
+
+def cpu_baseline_relay(rl, lat_table, loss_table, budget_s=8.0):
+    from oracle import corc
+    from shadow_amd import synth
+    b = rl["batch"]
+    threads = corc.max_threads()
+    start = synth.SIM_START + 10**9
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        rng = rl["rng0"].copy()
+        nid = np.zeros(rl["H"], np.uint64)
+        corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, rl["host_node"], lat_table,
+                         loss_table, rng, nid, start + 10**6, start + 10**12, 0, threads=threads,
+                         want_events=False)
+        reps += 1
+        if time.perf_counter() - t0 > budget_s or reps >= 5:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    return dict(value=rl["P"] / dt, unit="packets/s", cores=threads, kind="port",
+                sample=f"{reps} full C5 rounds (per-packet send_packet restatement, per-destination "
+                       f"mutex + binary-heap push, OpenMP over source hosts)")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--relay-steps", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-relay", action="store_true")
+    args = ap.parse_args()
+    world, rank, local = dist_setup(args.gpus)
+    from shadow_amd.routing import Engine
+    eng = Engine(local)
+
+    r = routing_leg(eng, world, rank, args.steps, args.warmup)
+    value = args.steps * r["n"] ** 2 / r["dt"]
+    res = {
+        "metric": METRIC, "value": value, "unit": "node-pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": r["ms_per_step"],
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u32 latency (u64 out) + f32 loss", "data": "synthetic",
+        "config": {"workload": "C2: APSP routing-table build, 1000-node complete undirected GML "
+                               "graph + self-loops, 1000 used nodes",
+                   "nodes": r["n"], "arcs": int(r["arcs"]), "arcs_after_prune": int(r["arcs_kept"]),
+                   "algo": int(r["algo"]),
+                   "parallelism": f"source-row shards x{world} + RCCL all-gather" if world > 1 else "1 GPU"},
+        "roofline": {"bound": "valu", "achieved": r["achieved"], "peak": VALU_PEAK_TOPS,
+                     "unit": "Tops/s", "frac": r["achieved"] / VALU_PEAK_TOPS,
+                     "traffic": load_pmc("routing"),
+                     "kernel_ms": r["kernel_ms"],
+                     "work": "2 int ops (add, min) per arc relaxation per source row = 2*n*A"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb, lat_cpu = cpu_baseline_routing(r["el"])
+        cb["bit_exact_vs_gpu"] = bool(np.array_equal(lat_cpu, r["lat"]))
+        res["cpu_baseline"] = cb
+    if not args.no_relay:
+        ks = args.relay_steps or max(3, args.steps // 2)
+        rl = relay_leg(eng, world, rank, ks, min(args.warmup, 2), r["lat"], r["loss"])
+        pv = ks * rl["P"] / rl["dt"]
+        ms = rl["ms_per_step"]
+        bytes_round = RELAY_BYTES_PER_PACKET * rl["P"] + RELAY_BYTES_PER_HOST * rl["H"]
+        ach = bytes_round / (ms * 1e-3) / 1e9
+        rel = {"metric": "packets relayed/s per round", "value": pv, "unit": "packets/s",
+               "steps": ks, "ms_per_round": ms, "n_sent_last_round": int(rl["n_sent"]),
+               "config": {"workload": "C5: 100k hosts on the C2 table, 10M packets per round "
+                                      "(src uniform, dst != src, 20% ACK / 60% 1448 B / 20% U[1,1448])",
+                          "hosts": rl["H"], "packets": rl["P"],
+                          "parallelism": "replica per GPU" if world > 1 else "1 GPU"},
+               "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": ach / HBM_PEAK_GBS, "traffic": load_pmc("relay"),
+                            "work": "84 B/packet + 80 B/host algorithmic (SURVEY 8(d)), whole round"}}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            rel["cpu_baseline"] = cpu_baseline_relay(rl, r["lat"], r["loss"])
+        res["relay"] = rel
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    eng.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,223 @@
+/*
+ * shd_accel.h -- C ABI of the MI355X (gfx950) engine for Shadow's two data-parallel paths:
+ *
+ *   1. the routing build: lexicographic (latency, then packet loss) shortest paths over the
+ *      GML network graph into the dense used-node RoutingInfo table, and the direct-path mode;
+ *   2. the per-round inter-host packet relay: path latency/loss lookup, seeded per-host loss
+ *      draw, delivery-time stamping, and the sort-merge of packet events into destination
+ *      hosts' event queues.
+ *
+ * Plain C types only (no torch / HIP types); caller-owned host buffers unless a function says
+ * "device".  No panic or C++ exception crosses this boundary: every entry point returns a
+ * shd_status.  One shd_ctx per GPU; a context is not thread-safe (the reference calls the
+ * routing build once from the setup thread and flushes the relay once per round from the
+ * manager thread).
+ *
+ * Reference interfaces replaced (FlyearthR/shadow, Shadow 3.0.0):
+ *   shd_routing_build      <- NetworkGraph::compute_shortest_paths / get_direct_paths
+ *                             (src/main/network/graph/mod.rs:185-254), called from
+ *                             generate_routing_info (src/main/core/sim_config.rs:424-461)
+ *   shd_routing_lookup     <- RoutingInfo::path (graph/mod.rs:446-448),
+ *                             WorkerShared::{latency,reliability} (src/main/core/worker.rs:529-543)
+ *   shd_routing_smallest_latency <- RoutingInfo::get_smallest_latency_ns (graph/mod.rs:476-478)
+ *   shd_relay_setup        <- WorkerShared tables built in Manager::run (core/manager.rs:309-332)
+ *                             + per-host RNG / event-id counter (src/main/host/host.rs:218,580-584)
+ *   shd_relay_round        <- the body of Worker::send_packet (src/main/core/worker.rs:328-413)
+ *                             for every send of one scheduling round, flushed at the round
+ *                             barrier (core/manager.rs:455-464), plus push_packet_to_host /
+ *                             EventQueue::push (worker.rs:619-629, core/work/event_queue.rs:28-48)
+ *   shd_path_packet_counts <- RoutingInfo::increment_packet_count / log_packet_counts
+ *                             (graph/mod.rs:451-474)
+ */
+#ifndef SHD_ACCEL_H
+#define SHD_ACCEL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHD_ABI_VERSION 1
+
+typedef enum shd_status {
+    SHD_OK = 0,
+    SHD_ERR_NO_EDGE = 1,          /* "No edge connecting node {a} to {b}"      graph/mod.rs:267-270 */
+    SHD_ERR_MULTI_EDGE = 2,       /* "More than one edge connecting node .."   graph/mod.rs:271-276 */
+    SHD_ERR_UNREACHABLE = 3,      /* reference panics: assert paths.len()==n^2 graph/mod.rs:221 */
+    SHD_ERR_LATENCY_OVERFLOW = 4, /* a path latency does not fit u64 ns (reference: overflow panic) */
+    SHD_ERR_INVALID = 5,          /* bad argument (null pointer, index out of range, ...)          */
+    SHD_ERR_HIP = 6,              /* HIP runtime failure                                           */
+    SHD_ERR_NOMEM = 7,            /* host or device allocation failed                              */
+    SHD_ERR_NO_HOST = 8,          /* "No host ID for dest address"              worker.rs:350-355 */
+    SHD_ERR_STATE = 9             /* call order violated (e.g. relay before setup)                 */
+} shd_status;
+
+typedef struct shd_ctx shd_ctx;
+
+/* Error detail; node ids are GML ids (graph/mod.rs:263-264 reports GML ids). */
+typedef struct shd_error {
+    int32_t code;      /* shd_status */
+    uint32_t node_a;
+    uint32_t node_b;
+} shd_error;
+
+/*
+ * Network graph after GML parsing (NetworkGraph, graph/mod.rs:115-183).  Node indices are the
+ * petgraph NodeIndex values (= GML node order); edges are in GML order.  edge_latency_ns is
+ * ShadowEdge.latency converted to ns (units.rs:377-388), edge_packet_loss the raw f32.
+ */
+typedef struct shd_graph {
+    uint32_t n_nodes;
+    uint32_t n_edges;
+    const uint32_t* edge_src;        /* node index, [n_edges] */
+    const uint32_t* edge_dst;        /* node index, [n_edges] */
+    const uint64_t* edge_latency_ns; /* [n_edges], > 0 */
+    const float* edge_packet_loss;   /* [n_edges], in [0,1] */
+    const uint32_t* node_ids;        /* GML id per node index [n_nodes]; NULL => id == index */
+    int32_t directed;                /* GML 'directed' (default 0) */
+} shd_graph;
+
+/* Routing modes (network.use_shortest_path, configuration.rs:276; sim_config.rs:442-458). */
+#define SHD_ROUTE_SHORTEST 0u
+#define SHD_ROUTE_DIRECT 1u
+
+/* Algorithm selection for SHD_ROUTE_SHORTEST (all produce identical bits). */
+#define SHD_ALGO_AUTO 0u     /* dense graphs: 2-hop prune + SSSP; sparse: SSSP           */
+#define SHD_ALGO_SSSP 1u     /* batched per-source label-correcting SSSP, labels in LDS   */
+#define SHD_ALGO_PRUNED 2u   /* dense k-nearest 2-hop edge prune, then SSSP               */
+#define SHD_ALGO_DELTA 3u    /* delta-stepping buckets inside the per-source SSSP         */
+#define SHD_ALGO_BLOCKED 4u  /* blocked min-plus (Floyd-Warshall) latency + tight-DAG loss */
+
+typedef struct shd_routing_info {
+    uint32_t algo_used;        /* SHD_ALGO_* that ran */
+    uint32_t wide_latency;     /* 1 if the u64-latency kernels ran (a path >= 2^32-1 ns) */
+    uint64_t arcs;             /* arcs after parallel-edge reduction */
+    uint64_t arcs_kept;        /* arcs after pruning (== arcs when no prune ran) */
+    double ms_total;           /* device time of the last build (HIP events) */
+    double ms_main;            /* device time of the dominant kernel */
+} shd_routing_info;
+
+/* ---------------------------------------------------------------- context */
+const char* shd_version(void);
+const char* shd_status_str(shd_status st);
+shd_ctx* shd_open(int device_ordinal, shd_status* st);
+void shd_close(shd_ctx* ctx);
+/* Stream for all device work of this context (a hipStream_t passed as void*; NULL => the
+ * context's own stream).  Lets a caller order the engine behind its own stream. */
+shd_status shd_set_stream(shd_ctx* ctx, void* hip_stream);
+
+/* ---------------------------------------------------------------- routing build */
+/*
+ * Build rows [row_begin, row_end) of the n_used x n_used table (row-major in `used` order;
+ * row_end == 0 means n_used).  lat_out/loss_out receive (row_end-row_begin) * n_used entries;
+ * either may be NULL, in which case the table stays only device-resident in the context.
+ * Diagonal = the node's single self-loop edge (graph/mod.rs:212-219).  Errors are reported
+ * for the whole used set exactly as the reference: missing/multiple self-loop -> NO_EDGE /
+ * MULTI_EDGE on the first such node in `used` order; unreachable pair -> UNREACHABLE.
+ */
+shd_status shd_routing_build(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
+                             uint32_t n_used, uint32_t mode, uint32_t algo,
+                             uint32_t row_begin, uint32_t row_end,
+                             uint64_t* lat_out, float* loss_out, shd_error* err);
+
+/*
+ * Two-phase form of the same build (what a caller that rebuilds, shards or benchmarks uses):
+ * shd_routing_prepare validates the graph and the used set, applies the self-loop rule and
+ * uploads the arc CSR (device-resident in the context); shd_routing_run then computes rows
+ * [row_begin, row_end) from the resident graph into device buffers on the context's stream
+ * (NULL outputs => the context's resident table).  Errors as for shd_routing_build.
+ */
+shd_status shd_routing_prepare(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
+                               uint32_t n_used, uint32_t mode, shd_error* err);
+shd_status shd_routing_run(shd_ctx* ctx, uint32_t algo, uint32_t row_begin, uint32_t row_end,
+                           uint64_t* d_lat_out, float* d_loss_out, shd_error* err);
+
+/* As shd_routing_build, writing the rows straight into device buffers (hipMalloc'd or torch
+ * tensors) on the context's stream; the call returns when the rows are complete. */
+shd_status shd_routing_build_device(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
+                                    uint32_t n_used, uint32_t mode, uint32_t algo,
+                                    uint32_t row_begin, uint32_t row_end,
+                                    uint64_t* d_lat_out, float* d_loss_out, shd_error* err);
+
+shd_status shd_routing_last_info(const shd_ctx* ctx, shd_routing_info* info);
+
+/* Look up one pair of the resident table (row index relative to row_begin of the last build). */
+shd_status shd_routing_lookup(shd_ctx* ctx, uint32_t src_row, uint32_t dst_col,
+                              uint64_t* latency_ns, float* packet_loss);
+shd_status shd_routing_smallest_latency(shd_ctx* ctx, uint64_t* latency_ns);
+
+/* ---------------------------------------------------------------- relay */
+/*
+ * Host tables for the relay: host -> used-node index (IpAssignment + RoutingInfo keys,
+ * worker.rs:529-543), the n_nodes x n_nodes table (NULL => the context's resident table from
+ * the last full routing build), each host's Xoshiro256++ state (4 x u64, host.rs:218) and next
+ * event id (host.rs:580-584).
+ */
+shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_node,
+                           uint32_t n_nodes, const uint64_t* lat, const float* loss,
+                           const uint64_t* rng_state, const uint64_t* next_event_id);
+
+typedef struct shd_round {
+    uint64_t round_end;      /* Worker::round_end_time */
+    uint64_t sim_end;        /* WorkerShared::sim_end_time */
+    uint64_t bootstrap_end;  /* WorkerShared::bootstrap_end_time */
+} shd_round;
+
+/*
+ * One round's staged sends, grouped by source host: host h's sends are packets
+ * [src_off[h], src_off[h+1]) in send order (src_off has n_hosts+1 entries).  chance may be
+ * NULL: the engine then draws from the device-resident per-host streams; otherwise chance[i]
+ * is the f64 the CPU drew from the host RNG at send time (worker.rs:365).
+ */
+typedef struct shd_batch {
+    uint64_t n_packets;
+    const uint32_t* src_off;
+    const uint64_t* send_time;   /* emulated ns */
+    const uint32_t* dst_host;    /* HostId after DNS resolution (worker.rs:350-355) */
+    const uint32_t* payload;     /* packet_getPayloadSize */
+    const double* chance;        /* optional */
+} shd_batch;
+
+#define SHD_PKT_SKIPPED 0u  /* now >= sim_end: returned before any effect (worker.rs:339-341) */
+#define SHD_PKT_DROPPED 1u  /* PDS_INET_DROPPED (worker.rs:370-378) */
+#define SHD_PKT_SENT 2u     /* PDS_INET_SENT + event pushed */
+
+/*
+ * Outputs (caller-owned host buffers, any may be NULL): status[n_packets]; the round's packet
+ * events grouped by destination host in EventQueue pop order (event.rs:84-155):
+ * ev_off[n_hosts+1], ev_deliver / ev_src / ev_seq / ev_pkt[n_sent] (ev_pkt = index of the
+ * packet in the batch); min_deliver = min over sent deliver times (u64 max if none,
+ * worker.rs:406); min_latency = min latency used (runahead.rs:60-115); n_sent.
+ */
+typedef struct shd_relay_out {
+    uint8_t* status;
+    uint32_t* ev_off;
+    uint64_t* ev_deliver;
+    uint32_t* ev_src;
+    uint64_t* ev_seq;
+    uint32_t* ev_pkt;
+    uint64_t min_deliver;
+    uint64_t min_latency;
+    uint64_t n_sent;
+} shd_relay_out;
+
+shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round* round,
+                           shd_relay_out* out);
+
+/* Device-buffer form (all pointers in shd_batch / shd_relay_out are device pointers; status,
+ * ev_* must hold n_packets entries).  Used by the multi-GPU driver and the benchmark. */
+shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const shd_round* round,
+                                  shd_relay_out* d_out);
+
+/* Read back the per-host RNG states / next event ids (e.g. to hand RNG use back to the CPU). */
+shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t* next_event_id);
+
+/* Per-path packet counters accumulated over all rounds (n_nodes x n_nodes u64, saturating). */
+shd_status shd_path_packet_counts(shd_ctx* ctx, uint64_t* counts);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHD_ACCEL_H */

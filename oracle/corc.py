@@ -1,0 +1,96 @@
+"""ctypes front end of the C restatement (oracle/c/oracle.c) -- test infrastructure only."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+TIDY, FAITHFUL = 0, 1
+CODES = {0: "OK", 1: "NO_EDGE", 2: "MULTI_EDGE", 3: "UNREACHABLE", 4: "NOMEM"}
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", os.path.join(_HERE, "c")])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        _lib.orc_shortest_paths.restype = C.c_int
+        _lib.orc_shortest_paths.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P,
+                                            C.c_uint32, C.c_int, C.c_int, P, P, P, P]
+        _lib.orc_direct_paths.restype = C.c_int
+        _lib.orc_direct_paths.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P,
+                                          C.c_uint32, P, P, P, P]
+        _lib.orc_relay_round.restype = C.c_int64
+        _lib.orc_relay_round.argtypes = [C.c_uint32, P, P, P, P, P, P, C.c_uint32, P, P, P, P,
+                                         C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, P, P, P,
+                                         P, P, P, P, P, P, P]
+        _lib.orc_max_threads.restype = C.c_int
+        _lib.orc_xoshiro_seed.argtypes = [C.c_uint64, P]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def routing(n_nodes, es, ed, el, ep, directed, used, shortest=True, variant=TIDY, threads=0):
+    """Returns (code, lat[n,n] u64, loss[n,n] f32, (err_a, err_b))."""
+    es = np.ascontiguousarray(es, np.uint32); ed = np.ascontiguousarray(ed, np.uint32)
+    el = np.ascontiguousarray(el, np.uint64); ep = np.ascontiguousarray(ep, np.float32)
+    used = np.ascontiguousarray(used, np.uint32)
+    n = len(used)
+    lat = np.zeros((n, n), np.uint64); loss = np.zeros((n, n), np.float32)
+    ea = np.zeros(1, np.uint32); eb = np.zeros(1, np.uint32)
+    if shortest:
+        rc = lib().orc_shortest_paths(n_nodes, len(es), _p(es), _p(ed), _p(el), _p(ep),
+                                      int(directed), _p(used), n, variant, threads, _p(lat),
+                                      _p(loss), _p(ea), _p(eb))
+    else:
+        rc = lib().orc_direct_paths(n_nodes, len(es), _p(es), _p(ed), _p(el), _p(ep),
+                                    int(directed), _p(used), n, _p(lat), _p(loss), _p(ea), _p(eb))
+    return CODES[rc], lat, loss, (int(ea[0]), int(eb[0]))
+
+
+def relay_round(src_off, send_time, dst_host, payload, host_node, lat, loss, rng, next_id,
+                round_end, sim_end, bootstrap_end, chance=None, threads=0, want_events=True):
+    """C restatement of one relay round.  rng [H,4] and next_id [H] are updated in place."""
+    n = len(send_time)
+    H = len(src_off) - 1
+    status = np.zeros(n, np.uint8); deliver = np.zeros(n, np.uint64); seq = np.zeros(n, np.uint64)
+    mind = np.zeros(1, np.uint64); minl = np.zeros(1, np.uint64)
+    out = None
+    if want_events:
+        out = dict(off=np.zeros(H + 1, np.uint32), deliver=np.zeros(n, np.uint64),
+                   src=np.zeros(n, np.uint32), seq=np.zeros(n, np.uint64), pkt=np.zeros(n, np.uint32))
+    nn = lat.shape[0]
+    n_sent = lib().orc_relay_round(
+        H, _p(np.ascontiguousarray(src_off, np.uint32)), _p(np.ascontiguousarray(send_time, np.uint64)),
+        _p(np.ascontiguousarray(dst_host, np.uint32)), _p(np.ascontiguousarray(payload, np.uint32)),
+        _p(None if chance is None else np.ascontiguousarray(chance, np.float64)),
+        _p(np.ascontiguousarray(host_node, np.uint32)), nn, _p(np.ascontiguousarray(lat, np.uint64)),
+        _p(np.ascontiguousarray(loss, np.float32)), _p(rng), _p(next_id), round_end, sim_end,
+        bootstrap_end, threads, _p(status), _p(deliver), _p(seq), _p(mind), _p(minl),
+        _p(out["off"]) if out else None, _p(out["deliver"]) if out else None,
+        _p(out["src"]) if out else None, _p(out["seq"]) if out else None,
+        _p(out["pkt"]) if out else None)
+    if out:
+        for k in ("deliver", "src", "seq", "pkt"):
+            out[k] = out[k][:n_sent]
+    return dict(status=status, deliver=deliver, seq=seq, min_deliver=int(mind[0]),
+                min_latency=int(minl[0]), n_sent=int(n_sent), events=out)
+
+
+def max_threads():
+    return lib().orc_max_threads()

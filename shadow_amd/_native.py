@@ -1,0 +1,125 @@
+"""ctypes binding of include/shd_accel.h (the in-tree libshd_accel.so).
+
+This is the reference-side binding a Python host would use; the Rust equivalent is shown in
+INTEGRATION.md.  There is no fallback: if the library is missing or no gfx950 GPU is present,
+every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libshd_accel.so")
+
+SHD_OK = 0
+STATUS_NAMES = {0: "OK", 1: "NO_EDGE", 2: "MULTI_EDGE", 3: "UNREACHABLE", 4: "LATENCY_OVERFLOW",
+                5: "INVALID", 6: "HIP", 7: "NOMEM", 8: "NO_HOST", 9: "STATE"}
+
+ROUTE_SHORTEST, ROUTE_DIRECT = 0, 1
+ALGO_AUTO, ALGO_SSSP, ALGO_PRUNED, ALGO_DELTA, ALGO_BLOCKED = 0, 1, 2, 3, 4
+PKT_SKIPPED, PKT_DROPPED, PKT_SENT = 0, 1, 2
+
+EXPORTED = [
+    "shd_version", "shd_status_str", "shd_open", "shd_close", "shd_set_stream",
+    "shd_routing_build", "shd_routing_prepare", "shd_routing_run", "shd_routing_build_device",
+    "shd_routing_last_info",
+    "shd_routing_lookup", "shd_routing_smallest_latency", "shd_relay_setup", "shd_relay_round",
+    "shd_relay_round_device", "shd_relay_get_host_state", "shd_path_packet_counts",
+]
+
+
+class ShdError(RuntimeError):
+    def __init__(self, status: int, where: str, node_a=None, node_b=None):
+        self.status = status
+        self.code = STATUS_NAMES.get(status, str(status))
+        self.node_a, self.node_b = node_a, node_b
+        super().__init__(f"{where}: {self.code}" +
+                         (f" (nodes {node_a}, {node_b})" if node_a is not None else ""))
+
+
+class Graph(C.Structure):
+    _fields_ = [("n_nodes", C.c_uint32), ("n_edges", C.c_uint32),
+                ("edge_src", C.c_void_p), ("edge_dst", C.c_void_p),
+                ("edge_latency_ns", C.c_void_p), ("edge_packet_loss", C.c_void_p),
+                ("node_ids", C.c_void_p), ("directed", C.c_int32)]
+
+
+class Error(C.Structure):
+    _fields_ = [("code", C.c_int32), ("node_a", C.c_uint32), ("node_b", C.c_uint32)]
+
+
+class RoutingInfo(C.Structure):
+    _fields_ = [("algo_used", C.c_uint32), ("wide_latency", C.c_uint32), ("arcs", C.c_uint64),
+                ("arcs_kept", C.c_uint64), ("ms_total", C.c_double), ("ms_main", C.c_double)]
+
+
+class Round(C.Structure):
+    _fields_ = [("round_end", C.c_uint64), ("sim_end", C.c_uint64), ("bootstrap_end", C.c_uint64)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("n_packets", C.c_uint64), ("src_off", C.c_void_p), ("send_time", C.c_void_p),
+                ("dst_host", C.c_void_p), ("payload", C.c_void_p), ("chance", C.c_void_p)]
+
+
+class RelayOut(C.Structure):
+    _fields_ = [("status", C.c_void_p), ("ev_off", C.c_void_p), ("ev_deliver", C.c_void_p),
+                ("ev_src", C.c_void_p), ("ev_seq", C.c_void_p), ("ev_pkt", C.c_void_p),
+                ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64)]
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load the native library; raises if it is absent (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"shd_accel native library missing at {path}: run "
+                           "`python -m shadow_amd.build` (or __graft_entry__.build())")
+    lib = C.CDLL(path)
+    P, U32, U64, I32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
+    sig = {
+        "shd_version": (C.c_char_p, []),
+        "shd_status_str": (C.c_char_p, [I32]),
+        "shd_open": (P, [C.c_int, P]),
+        "shd_close": (None, [P]),
+        "shd_set_stream": (I32, [P, P]),
+        "shd_routing_build": (I32, [P, P, P, U32, U32, U32, U32, U32, P, P, P]),
+        "shd_routing_build_device": (I32, [P, P, P, U32, U32, U32, U32, U32, P, P, P]),
+        "shd_routing_prepare": (I32, [P, P, P, U32, U32, P]),
+        "shd_routing_run": (I32, [P, U32, U32, U32, P, P, P]),
+        "shd_routing_last_info": (I32, [P, P]),
+        "shd_routing_lookup": (I32, [P, U32, U32, P, P]),
+        "shd_routing_smallest_latency": (I32, [P, P]),
+        "shd_relay_setup": (I32, [P, U32, P, U32, P, P, P, P]),
+        "shd_relay_round": (I32, [P, P, P, P]),
+        "shd_relay_round_device": (I32, [P, P, P, P]),
+        "shd_relay_get_host_state": (I32, [P, P, P]),
+        "shd_path_packet_counts": (I32, [P, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, where: str, err: Error | None = None):
+    if status != SHD_OK:
+        if err is not None and err.code != 0:
+            raise ShdError(status, where, err.node_a, err.node_b)
+        raise ShdError(status, where)
+
+
+def ptr(a):
+    """Host numpy array -> void*, or device torch tensor -> void* (data_ptr)."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return C.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(C.c_void_p)

@@ -1,0 +1,198 @@
+// C ABI entry points (include/shd_accel.h): context lifetime, routing build front ends,
+// resident-table lookups.  The relay entry points live in relay.hip.
+#include <new>
+
+#include "ctx.h"
+
+namespace shd {
+shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
+                                uint32_t n_used, uint32_t mode, shd_error* err);
+shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t re,
+                            uint64_t* d_lat, float* d_loss, shd_error* err);
+shd_status min_u64_device(shd_ctx* ctx, const uint64_t* d, uint64_t n, uint64_t* out);
+}  // namespace shd
+
+using namespace shd;
+
+extern "C" {
+
+const char* shd_version(void) { return "shd_accel 0.1 (gfx950)"; }
+
+const char* shd_status_str(shd_status st) {
+    switch (st) {
+        case SHD_OK: return "ok";
+        case SHD_ERR_NO_EDGE: return "no edge connecting nodes";
+        case SHD_ERR_MULTI_EDGE: return "more than one edge connecting nodes";
+        case SHD_ERR_UNREACHABLE: return "node pair unreachable";
+        case SHD_ERR_LATENCY_OVERFLOW: return "path latency overflows u64 ns";
+        case SHD_ERR_INVALID: return "invalid argument";
+        case SHD_ERR_HIP: return "HIP runtime error";
+        case SHD_ERR_NOMEM: return "out of memory";
+        case SHD_ERR_NO_HOST: return "no host ID for dest address";
+        case SHD_ERR_STATE: return "invalid call order";
+    }
+    return "unknown";
+}
+
+shd_ctx* shd_open(int device_ordinal, shd_status* st) {
+    auto fail = [&](shd_status s) -> shd_ctx* {
+        if (st) *st = s;
+        return nullptr;
+    };
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(SHD_ERR_HIP);
+    if (device_ordinal < 0 || device_ordinal >= n) return fail(SHD_ERR_INVALID);
+    if (hipSetDevice(device_ordinal) != hipSuccess) return fail(SHD_ERR_HIP);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device_ordinal) != hipSuccess) return fail(SHD_ERR_HIP);
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0) {
+        std::fprintf(stderr, "shd_accel: device %d is %s, this build targets gfx950 only\n",
+                     device_ordinal, prop.gcnArchName);
+        return fail(SHD_ERR_HIP);
+    }
+    shd_ctx* ctx = new (std::nothrow) shd_ctx();
+    if (!ctx) return fail(SHD_ERR_NOMEM);
+    ctx->device = device_ordinal;
+    ctx->n_cu = prop.multiProcessorCount;
+    ctx->max_lds = prop.sharedMemPerBlock;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return fail(SHD_ERR_HIP);
+    }
+    ctx->own_stream = true;
+    for (auto& e : ctx->ev)
+        if (hipEventCreate(&e) != hipSuccess) {
+            shd_close(ctx);
+            return fail(SHD_ERR_HIP);
+        }
+    if (st) *st = SHD_OK;
+    return ctx;
+}
+
+void shd_close(shd_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (auto& e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;  // DevBuf destructors free device memory
+}
+
+shd_status shd_set_stream(shd_ctx* ctx, void* hip_stream) {
+    if (!ctx) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    if (ctx->own_stream && ctx->stream) {
+        SHD_HIP(hipStreamSynchronize(ctx->stream));
+        SHD_HIP(hipStreamDestroy(ctx->stream));
+    }
+    if (hip_stream) {
+        ctx->stream = static_cast<hipStream_t>(hip_stream);
+        ctx->own_stream = false;
+    } else {
+        SHD_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->own_stream = true;
+    }
+    return SHD_OK;
+}
+
+shd_status shd_routing_build_device(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
+                                    uint32_t n_used, uint32_t mode, uint32_t algo,
+                                    uint32_t row_begin, uint32_t row_end, uint64_t* d_lat_out,
+                                    float* d_loss_out, shd_error* err) {
+    if (!ctx || !d_lat_out || !d_loss_out) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    SHD_TRY(routing_prepare_impl(ctx, g, used, n_used, mode, err));
+    return routing_run_impl(ctx, algo, row_begin, row_end, d_lat_out, d_loss_out, err);
+}
+
+shd_status shd_routing_prepare(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
+                               uint32_t n_used, uint32_t mode, shd_error* err) {
+    if (!ctx) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    ctx->t_rows = 0;
+    return routing_prepare_impl(ctx, g, used, n_used, mode, err);
+}
+
+shd_status shd_routing_run(shd_ctx* ctx, uint32_t algo, uint32_t row_begin, uint32_t row_end,
+                           uint64_t* d_lat_out, float* d_loss_out, shd_error* err) {
+    if (!ctx) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    if (!ctx->prep.ready) return SHD_ERR_STATE;
+    const uint32_t n = ctx->prep.n_used;
+    const uint32_t re = row_end ? row_end : n;
+    if (row_begin >= re || re > n) return SHD_ERR_INVALID;
+    if ((d_lat_out == nullptr) != (d_loss_out == nullptr)) return SHD_ERR_INVALID;
+    if (!d_lat_out) {  // into the context's resident table
+        const size_t cells = (size_t)(re - row_begin) * n;
+        SHD_TRY(ctx->t_lat.ensure(cells * 8));
+        SHD_TRY(ctx->t_loss.ensure(cells * 4));
+        ctx->t_rows = 0;
+        SHD_TRY(routing_run_impl(ctx, algo, row_begin, re, ctx->t_lat.as<uint64_t>(),
+                                 ctx->t_loss.as<float>(), err));
+        ctx->t_rows = re - row_begin;
+        ctx->t_cols = n;
+        ctx->t_row_begin = row_begin;
+        ctx->t_full = (row_begin == 0 && re == n);
+        return SHD_OK;
+    }
+    return routing_run_impl(ctx, algo, row_begin, re, d_lat_out, d_loss_out, err);
+}
+
+shd_status shd_routing_build(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
+                             uint32_t n_used, uint32_t mode, uint32_t algo, uint32_t row_begin,
+                             uint32_t row_end, uint64_t* lat_out, float* loss_out,
+                             shd_error* err) {
+    if (!ctx || !used || n_used == 0) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    const uint32_t re = row_end ? row_end : n_used;
+    if (row_begin >= re || re > n_used) return SHD_ERR_INVALID;
+    const size_t cells = (size_t)(re - row_begin) * n_used;
+    SHD_TRY(ctx->t_lat.ensure(cells * 8));
+    SHD_TRY(ctx->t_loss.ensure(cells * 4));
+    ctx->t_rows = 0;
+    SHD_TRY(routing_prepare_impl(ctx, g, used, n_used, mode, err));
+    SHD_TRY(routing_run_impl(ctx, algo, row_begin, re, ctx->t_lat.as<uint64_t>(),
+                             ctx->t_loss.as<float>(), err));
+    ctx->t_rows = re - row_begin;
+    ctx->t_cols = n_used;
+    ctx->t_row_begin = row_begin;
+    ctx->t_full = (row_begin == 0 && re == n_used);
+    if (lat_out)
+        SHD_HIP(hipMemcpyAsync(lat_out, ctx->t_lat.p, cells * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (loss_out)
+        SHD_HIP(hipMemcpyAsync(loss_out, ctx->t_loss.p, cells * 4, hipMemcpyDeviceToHost, ctx->stream));
+    SHD_HIP(hipStreamSynchronize(ctx->stream));
+    return SHD_OK;
+}
+
+shd_status shd_routing_last_info(const shd_ctx* ctx, shd_routing_info* info) {
+    if (!ctx || !info) return SHD_ERR_INVALID;
+    *info = ctx->info;
+    return SHD_OK;
+}
+
+shd_status shd_routing_lookup(shd_ctx* ctx, uint32_t src_row, uint32_t dst_col,
+                              uint64_t* latency_ns, float* packet_loss) {
+    if (!ctx) return SHD_ERR_INVALID;
+    if (ctx->t_rows == 0) return SHD_ERR_STATE;
+    if (src_row >= ctx->t_rows || dst_col >= ctx->t_cols) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    const size_t i = (size_t)src_row * ctx->t_cols + dst_col;
+    if (latency_ns)
+        SHD_HIP(hipMemcpyAsync(latency_ns, ctx->t_lat.as<uint64_t>() + i, 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (packet_loss)
+        SHD_HIP(hipMemcpyAsync(packet_loss, ctx->t_loss.as<float>() + i, 4, hipMemcpyDeviceToHost, ctx->stream));
+    SHD_HIP(hipStreamSynchronize(ctx->stream));
+    return SHD_OK;
+}
+
+shd_status shd_routing_smallest_latency(shd_ctx* ctx, uint64_t* latency_ns) {
+    if (!ctx || !latency_ns) return SHD_ERR_INVALID;
+    if (ctx->t_rows == 0) return SHD_ERR_STATE;
+    SHD_HIP(hipSetDevice(ctx->device));
+    return min_u64_device(ctx, ctx->t_lat.as<uint64_t>(), (uint64_t)ctx->t_rows * ctx->t_cols,
+                          latency_ns);
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+// Engine context (one per GPU) and grow-only device scratch.
+#pragma once
+#include <vector>
+
+#include "common.h"
+
+namespace shd {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) {
+            release();
+            p = o.p; bytes = o.bytes;
+            o.p = nullptr; o.bytes = 0;
+        }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    shd_status ensure(size_t need) {
+        if (need <= bytes) return SHD_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t want = need + need / 8 + 256;
+        if (hipMalloc(&p, want) != hipSuccess) return SHD_ERR_NOMEM;
+        bytes = want;
+        return SHD_OK;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+struct RelayState {
+    bool ready = false;
+    uint32_t n_hosts = 0;
+    uint32_t n_nodes = 0;
+    bool own_table = false;   // table copied by shd_relay_setup (else: routing resident table)
+    DevBuf host_node, lat, loss, rng, next_id, counts;
+    // per-round scratch
+    DevBuf pk_off, pk_time, pk_dst, pk_pay, pk_chance, st, ev_key, ev_key2, ev_val, ev_val2,
+        ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, scan_tmp, red;
+};
+
+struct PreparedGraph {
+    bool ready = false;
+    uint32_t mode = 0, V = 0, n_used = 0;
+    bool directed = false, narrow_arcs = false;
+    uint64_t arcs = 0, max_arc_lat = 0;
+    std::vector<uint32_t> used, node_ids, es, ed;
+    std::vector<uint64_t> el;
+    std::vector<float> ep;
+    shd_graph view() const {
+        shd_graph g{};
+        g.n_nodes = V;
+        g.n_edges = (uint32_t)es.size();
+        g.edge_src = es.data();
+        g.edge_dst = ed.data();
+        g.edge_latency_ns = el.data();
+        g.edge_packet_loss = ep.data();
+        g.node_ids = node_ids.data();
+        g.directed = directed;
+        return g;
+    }
+};
+
+}  // namespace shd
+
+struct shd_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int n_cu = 0;
+    size_t max_lds = 0;
+
+    // resident routing table of the last build: rows [row_begin, row_begin+rows) x cols
+    shd::DevBuf t_lat, t_loss;
+    uint32_t t_rows = 0, t_cols = 0, t_row_begin = 0;
+    bool t_full = false;
+    shd_routing_info info{};
+
+    shd::PreparedGraph prep;
+    shd::DevBuf d_es, d_ed, d_el, d_ep, d_col;   // direct mode edge arrays
+    // routing scratch
+    shd::DevBuf g_off, g_dst, g_lat, g_q, g_lat64, g_used, g_diag_lat, g_diag_loss, g_flags,
+        g_dense, g_prune_dst, g_prune_lat, g_prune_q, g_prune_cnt, g_labels, g_aux;
+
+    shd::RelayState relay;
+};

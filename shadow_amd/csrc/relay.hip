@@ -1,0 +1,521 @@
+// Per-round inter-host packet relay on gfx950.
+//
+// Reference semantics, per staged send (FlyearthR/shadow src/main/core/worker.rs:328-413):
+//   now >= sim_end -> nothing happens (no RNG draw, no status)                      :334-341
+//   reliability = (1.0f32 - loss) as f64                                 WorkerShared :538-543
+//   chance = src_host.rng.gen::<f64>() = (xoshiro256++ >> 11) * 2^-53                  :365
+//   drop iff !bootstrapping && chance >= reliability && payload_size > 0              :370-378
+//   deliver = max(now + latency, round_end); next-event-time min; lowest-used-latency  :380-406
+//   event (deliver, Packet, src_host_id, src_host_event_id) into the dst queue  :408-411, 619-629
+// Destination order = EventQueue pop order (core/work/event.rs:84-155): time, then src host id,
+// then src event id.  Every event of round r has deliver >= round_end, so batching the whole
+// round to the barrier (core/manager.rs:455-464) is exact.
+//
+// Pipeline (one stream, no host sync inside):
+//   K1 relay_stamp     one lane per source host walks its sends in order (the RNG stream and
+//                      the event-id counter are sequential per host); gathers the path, draws,
+//                      decides, stamps; claims a slot in the destination bucket (atomic count).
+//   K2 scan            exclusive scan of per-destination counts -> event offsets.
+//   K3 relay_scatter   one lane per packet scatters its event into the destination bucket.
+//   K4 segment_sort    one workgroup per destination sorts its bucket by the full event key
+//                      (unique), so the atomic slot order never shows in the output.
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include <vector>
+
+#include "ctx.h"
+
+namespace shd {
+
+constexpr uint32_t kStSkipped = 0, kStDropped = 1, kStSent = 2;
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+
+struct Xoshiro {
+    uint64_t s0, s1, s2, s3;
+    __device__ __forceinline__ uint64_t next() {
+        const uint64_t res = rotl64(s0 + s3, 23) + s0;
+        const uint64_t t = s1 << 17;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl64(s3, 45);
+        return res;
+    }
+    // rand 0.8.5 Standard for f64: 53 high bits, multiply-based, [0, 1)
+    __device__ __forceinline__ double gen_f64() {
+        return (double)(next() >> 11) * (1.0 / 9007199254740992.0);
+    }
+};
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = __shfl_xor(v, o);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+struct RelayArgs {
+    uint32_t n_hosts, n_nodes;
+    const uint32_t* src_off;
+    const uint64_t* send_time;
+    const uint32_t* dst_host;
+    const uint32_t* payload;
+    const double* chance;
+    const uint32_t* host_node;
+    const uint64_t* lat;
+    const float* loss;
+    uint64_t* rng;
+    uint64_t* next_id;
+    unsigned long long* counts;  // nullable
+    uint64_t round_end, sim_end, bootstrap_end;
+    uint8_t* status;
+    uint64_t* deliver;
+    uint64_t* seq;
+    uint32_t* slot;
+    uint32_t* dst_cnt;
+    unsigned long long* red;     // [0] min deliver, [1] min latency, [2] n_sent, [3] bad dst
+};
+
+__global__ __launch_bounds__(256) void relay_stamp(RelayArgs a) {
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    uint64_t my_min_d = ~0ull, my_min_l = ~0ull, my_sent = 0;
+    if (h < a.n_hosts) {
+        Xoshiro r{a.rng[4 * (size_t)h], a.rng[4 * (size_t)h + 1], a.rng[4 * (size_t)h + 2],
+                  a.rng[4 * (size_t)h + 3]};
+        uint64_t id = a.next_id[h];
+        const uint32_t sn = a.host_node[h];
+        const uint32_t i1 = a.src_off[h + 1];
+        for (uint32_t i = a.src_off[h]; i < i1; ++i) {
+            const uint64_t now = a.send_time[i];
+            uint8_t st = kStSkipped;
+            if (now < a.sim_end) {
+                const uint32_t d = a.dst_host[i];
+                if (d >= a.n_hosts) {  // "No host ID for dest address" (worker.rs:350-355)
+                    atomicMin(&a.red[3], (unsigned long long)i);
+                    a.status[i] = kStSkipped;
+                    continue;
+                }
+                const size_t pi = (size_t)sn * a.n_nodes + a.host_node[d];
+                const double reliability = (double)one_minus(a.loss[pi]);
+                const double chance = a.chance ? a.chance[i] : r.gen_f64();
+                const bool boot = now < a.bootstrap_end;
+                if (!boot && chance >= reliability && a.payload[i] > 0) {
+                    st = kStDropped;
+                } else {
+                    const uint64_t delay = a.lat[pi];
+                    uint64_t t = now + delay;
+                    if (t < a.round_end) t = a.round_end;
+                    st = kStSent;
+                    a.deliver[i] = t;
+                    a.seq[i] = id++;
+                    a.slot[i] = atomicAdd(&a.dst_cnt[d], 1u);
+                    if (a.counts) atomicAdd(&a.counts[pi], 1ull);
+                    my_min_d = t < my_min_d ? t : my_min_d;
+                    my_min_l = delay < my_min_l ? delay : my_min_l;
+                    ++my_sent;
+                }
+            }
+            a.status[i] = st;
+        }
+        a.rng[4 * (size_t)h] = r.s0;
+        a.rng[4 * (size_t)h + 1] = r.s1;
+        a.rng[4 * (size_t)h + 2] = r.s2;
+        a.rng[4 * (size_t)h + 3] = r.s3;
+        a.next_id[h] = id;
+    }
+    my_min_d = wave_min_u64(my_min_d);
+    my_min_l = wave_min_u64(my_min_l);
+    for (int o = 32; o > 0; o >>= 1) my_sent += __shfl_xor(my_sent, o);
+    if ((threadIdx.x & 63) == 0) {
+        if (my_min_d != ~0ull) atomicMin(&a.red[0], (unsigned long long)my_min_d);
+        if (my_min_l != ~0ull) atomicMin(&a.red[1], (unsigned long long)my_min_l);
+        if (my_sent) atomicAdd(&a.red[2], (unsigned long long)my_sent);
+    }
+}
+
+// Per-packet source host from the grouped offsets (binary search; hosts are few per packet).
+__device__ __forceinline__ uint32_t owner_of(const uint32_t* off, uint32_t n_hosts, uint32_t i) {
+    uint32_t lo = 0, hi = n_hosts;  // find h with off[h] <= i < off[h+1]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void relay_scatter(
+    uint64_t n, uint32_t n_hosts, const uint32_t* __restrict__ src_off,
+    const uint8_t* __restrict__ status, const uint32_t* __restrict__ dst_host,
+    const uint32_t* __restrict__ slot, const uint64_t* __restrict__ deliver,
+    const uint64_t* __restrict__ seq, const uint32_t* __restrict__ ev_off,
+    uint64_t* __restrict__ ev_deliver, uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq,
+    uint32_t* __restrict__ ev_pkt) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n || status[i] != kStSent) return;
+    const uint32_t pos = ev_off[dst_host[i]] + slot[i];
+    ev_deliver[pos] = deliver[i];
+    ev_src[pos] = owner_of(src_off, n_hosts, (uint32_t)i);
+    ev_seq[pos] = seq[i];
+    ev_pkt[pos] = (uint32_t)i;
+}
+
+// Sort one destination's bucket by (deliver, src, seq) -- bitonic network in LDS.
+constexpr uint32_t kSegCap = 1024;
+
+struct EvKey {
+    uint64_t t;
+    uint64_t sq;   // seq
+    uint32_t src;
+    uint32_t pkt;
+};
+__device__ __forceinline__ bool ev_less(const EvKey& a, const EvKey& b) {
+    if (a.t != b.t) return a.t < b.t;
+    if (a.src != b.src) return a.src < b.src;
+    return a.sq < b.sq;
+}
+
+__global__ __launch_bounds__(256) void segment_sort(
+    uint32_t n_hosts, const uint32_t* __restrict__ ev_off, uint64_t* __restrict__ ev_deliver,
+    uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq, uint32_t* __restrict__ ev_pkt,
+    uint32_t* __restrict__ big) {
+    __shared__ EvKey s[kSegCap];
+    const uint32_t d = blockIdx.x;
+    const uint32_t b = ev_off[d], n = ev_off[d + 1] - b;
+    if (n <= 1) return;
+    if (n > kSegCap) {
+        if (threadIdx.x == 0) big[atomicAdd(&big[0], 1u) + 1] = d;
+        return;
+    }
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+    for (uint32_t i = threadIdx.x; i < P; i += 256) {
+        if (i < n)
+            s[i] = EvKey{ev_deliver[b + i], ev_seq[b + i], ev_src[b + i], ev_pkt[b + i]};
+        else
+            s[i] = EvKey{~0ull, ~0ull, ~0u, ~0u};
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += 256) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    EvKey x = s[i], y = s[l];
+                    if (ev_less(y, x) == up) {
+                        s[i] = y;
+                        s[l] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += 256) {
+        const EvKey e = s[i];
+        ev_deliver[b + i] = e.t;
+        ev_src[b + i] = e.src;
+        ev_seq[b + i] = e.sq;
+        ev_pkt[b + i] = e.pkt;
+    }
+}
+
+// Oversized buckets (> kSegCap events for one destination in one round): bottom-up merge
+// sort of that bucket by one workgroup through a global scratch area.
+__global__ __launch_bounds__(256) void segment_sort_big(
+    const uint32_t* __restrict__ big, const uint32_t* __restrict__ ev_off,
+    uint64_t* __restrict__ ev_deliver, uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq,
+    uint32_t* __restrict__ ev_pkt, EvKey* __restrict__ tmp) {
+    const uint32_t d = big[1 + blockIdx.x];
+    const uint32_t b = ev_off[d], n = ev_off[d + 1] - b;
+    EvKey* A = tmp + b;  // this bucket's slice of the scratch (one EvKey per event)
+    for (uint32_t i = threadIdx.x; i < n; i += 256)
+        A[i] = EvKey{ev_deliver[b + i], ev_seq[b + i], ev_src[b + i], ev_pkt[b + i]};
+    __syncthreads();
+    // merge passes of run width w; each element finds its output rank by binary search in
+    // the sibling run (keys are unique, so ranks never collide)
+    for (uint32_t w = 1; w < n; w <<= 1) {
+        // merge runs [i, i+w) and [i+w, i+2w) into ev_* arrays, then copy back
+        for (uint32_t o = threadIdx.x; o < n; o += 256) {
+            const uint32_t run = o / (2 * w), lo = run * 2 * w;
+            const uint32_t mid = min(lo + w, n), hi = min(lo + 2 * w, n);
+            // rank of element o within the merged output: binary search in the other run
+            const EvKey x = A[o];
+            uint32_t rank;
+            if (o < mid) {
+                uint32_t l = mid, h = hi;  // count of elements in right run strictly less
+                while (l < h) {
+                    const uint32_t m = (l + h) >> 1;
+                    if (ev_less(A[m], x)) l = m + 1; else h = m;
+                }
+                rank = (o - lo) + (l - mid);
+            } else {
+                uint32_t l = lo, h = mid;  // count of elements in left run <= x (keys unique)
+                while (l < h) {
+                    const uint32_t m = (l + h) >> 1;
+                    if (ev_less(x, A[m])) h = m; else l = m + 1;
+                }
+                rank = (o - mid) + (l - lo);
+            }
+            const uint32_t dst = b + lo + rank;
+            ev_deliver[dst] = x.t;
+            ev_src[dst] = x.src;
+            ev_seq[dst] = x.sq;
+            ev_pkt[dst] = x.pkt;
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < n; i += 256)
+            A[i] = EvKey{ev_deliver[b + i], ev_seq[b + i], ev_src[b + i], ev_pkt[b + i]};
+        __syncthreads();
+    }
+}
+
+__global__ void min_u64_kernel(const uint64_t* __restrict__ d, uint64_t n,
+                               unsigned long long* __restrict__ out) {
+    uint64_t m = ~0ull;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        m = d[i] < m ? d[i] : m;
+    m = wave_min_u64(m);
+    if ((threadIdx.x & 63) == 0) atomicMin(out, (unsigned long long)m);
+}
+
+shd_status min_u64_device(shd_ctx* ctx, const uint64_t* d, uint64_t n, uint64_t* out) {
+    SHD_TRY(ctx->g_aux.ensure(8));
+    SHD_HIP(hipMemsetAsync(ctx->g_aux.p, 0xFF, 8, ctx->stream));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (n + 255) / 256);
+    min_u64_kernel<<<grid ? grid : 1, 256, 0, ctx->stream>>>(
+        d, n, reinterpret_cast<unsigned long long*>(ctx->g_aux.p));
+    SHD_HIP(hipMemcpyAsync(out, ctx->g_aux.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+    SHD_HIP(hipStreamSynchronize(ctx->stream));
+    return SHD_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------
+static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                               shd_relay_out* o, bool sync_scalars) {
+    RelayState& R = ctx->relay;
+    hipStream_t s = ctx->stream;
+    const uint64_t n = b->n_packets;
+    const uint32_t H = R.n_hosts;
+    SHD_TRY(R.red.ensure(64));
+    SHD_TRY(R.dst_cnt.ensure((size_t)(H + 1) * 4));
+    SHD_TRY(R.ev_key.ensure(std::max<uint64_t>(n, 1) * 8));   // deliver per packet
+    SHD_TRY(R.ev_key2.ensure(std::max<uint64_t>(n, 1) * 8));  // seq per packet
+    SHD_TRY(R.ev_val.ensure(std::max<uint64_t>(n, 1) * 4));   // slot per packet
+    SHD_TRY(R.scan_tmp.ensure(64));
+    unsigned long long init[4] = {~0ull, ~0ull, 0ull, ~0ull};
+    SHD_HIP(hipMemcpyAsync(R.red.p, init, sizeof(init), hipMemcpyHostToDevice, s));
+    SHD_HIP(hipMemsetAsync(R.dst_cnt.p, 0, (size_t)(H + 1) * 4, s));
+    RelayArgs a{};
+    a.n_hosts = H;
+    a.n_nodes = R.n_nodes;
+    a.src_off = b->src_off;
+    a.send_time = b->send_time;
+    a.dst_host = b->dst_host;
+    a.payload = b->payload;
+    a.chance = b->chance;
+    a.host_node = R.host_node.as<uint32_t>();
+    a.lat = R.own_table ? R.lat.as<uint64_t>() : ctx->t_lat.as<uint64_t>();
+    a.loss = R.own_table ? R.loss.as<float>() : ctx->t_loss.as<float>();
+    a.rng = R.rng.as<uint64_t>();
+    a.next_id = R.next_id.as<uint64_t>();
+    a.counts = R.counts.as<unsigned long long>();
+    a.round_end = rd->round_end;
+    a.sim_end = rd->sim_end;
+    a.bootstrap_end = rd->bootstrap_end;
+    a.status = o->status;
+    a.deliver = R.ev_key.as<uint64_t>();
+    a.seq = R.ev_key2.as<uint64_t>();
+    a.slot = R.ev_val.as<uint32_t>();
+    a.dst_cnt = R.dst_cnt.as<uint32_t>();
+    a.red = R.red.as<unsigned long long>();
+    relay_stamp<<<div_up(H, 256), 256, 0, s>>>(a);
+    SHD_HIP(hipGetLastError());
+    // exclusive scan of H+1 counts (last is 0) -> ev_off[0..H]
+    size_t tmp_bytes = 0;
+    SHD_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off, 0u,
+                                    (size_t)H + 1, rocprim::plus<uint32_t>(), s));
+    SHD_TRY(R.scan_tmp.ensure(tmp_bytes));
+    SHD_HIP(rocprim::exclusive_scan(R.scan_tmp.p, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off,
+                                    0u, (size_t)H + 1, rocprim::plus<uint32_t>(), s));
+    if (n)
+        relay_scatter<<<div_up(n, 256), 256, 0, s>>>(n, H, b->src_off, o->status, b->dst_host,
+                                                     R.ev_val.as<uint32_t>(), R.ev_key.as<uint64_t>(),
+                                                     R.ev_key2.as<uint64_t>(), o->ev_off, o->ev_deliver,
+                                                     o->ev_src, o->ev_seq, o->ev_pkt);
+    SHD_TRY(R.ev_val2.ensure((size_t)(H + 2) * 4));
+    SHD_HIP(hipMemsetAsync(R.ev_val2.p, 0, 4, s));
+    segment_sort<<<H, 256, 0, s>>>(H, o->ev_off, o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt,
+                                   R.ev_val2.as<uint32_t>());
+    SHD_HIP(hipGetLastError());
+    uint32_t n_big = 0;
+    SHD_HIP(hipMemcpyAsync(&n_big, R.ev_val2.p, 4, hipMemcpyDeviceToHost, s));
+    unsigned long long red[4];
+    SHD_HIP(hipMemcpyAsync(red, R.red.p, sizeof(red), hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    if (n_big) {
+        SHD_TRY(R.scan_tmp.ensure(std::max<uint64_t>(n, 1) * sizeof(EvKey)));
+        segment_sort_big<<<n_big, 256, 0, s>>>(R.ev_val2.as<uint32_t>(), o->ev_off, o->ev_deliver,
+                                               o->ev_src, o->ev_seq, o->ev_pkt,
+                                               R.scan_tmp.as<EvKey>());
+        SHD_HIP(hipGetLastError());
+        SHD_HIP(hipStreamSynchronize(s));
+    }
+    (void)sync_scalars;
+    if (red[3] != ~0ull) return SHD_ERR_NO_HOST;
+    o->min_deliver = red[0];
+    o->min_latency = red[1];
+    o->n_sent = red[2];
+    return SHD_OK;
+}
+
+}  // namespace shd
+
+using namespace shd;
+
+extern "C" {
+
+shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_node,
+                           uint32_t n_nodes, const uint64_t* lat, const float* loss,
+                           const uint64_t* rng_state, const uint64_t* next_event_id) {
+    if (!ctx || n_hosts == 0 || !host_node || !rng_state || !next_event_id || n_nodes == 0)
+        return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    RelayState& R = ctx->relay;
+    hipStream_t s = ctx->stream;
+    for (uint32_t h = 0; h < n_hosts; h++)
+        if (host_node[h] >= n_nodes) return SHD_ERR_INVALID;
+    if ((lat == nullptr) != (loss == nullptr)) return SHD_ERR_INVALID;
+    if (!lat) {
+        if (!ctx->t_full || ctx->t_cols != n_nodes) return SHD_ERR_STATE;
+        R.own_table = false;
+    } else {
+        const size_t nn = (size_t)n_nodes * n_nodes;
+        SHD_TRY(R.lat.ensure(nn * 8));
+        SHD_TRY(R.loss.ensure(nn * 4));
+        SHD_HIP(hipMemcpyAsync(R.lat.p, lat, nn * 8, hipMemcpyHostToDevice, s));
+        SHD_HIP(hipMemcpyAsync(R.loss.p, loss, nn * 4, hipMemcpyHostToDevice, s));
+        R.own_table = true;
+    }
+    SHD_TRY(R.host_node.ensure((size_t)n_hosts * 4));
+    SHD_TRY(R.rng.ensure((size_t)n_hosts * 32));
+    SHD_TRY(R.next_id.ensure((size_t)n_hosts * 8));
+    SHD_TRY(R.counts.ensure((size_t)n_nodes * n_nodes * 8));
+    SHD_HIP(hipMemcpyAsync(R.host_node.p, host_node, (size_t)n_hosts * 4, hipMemcpyHostToDevice, s));
+    SHD_HIP(hipMemcpyAsync(R.rng.p, rng_state, (size_t)n_hosts * 32, hipMemcpyHostToDevice, s));
+    SHD_HIP(hipMemcpyAsync(R.next_id.p, next_event_id, (size_t)n_hosts * 8, hipMemcpyHostToDevice, s));
+    SHD_HIP(hipMemsetAsync(R.counts.p, 0, (size_t)n_nodes * n_nodes * 8, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    R.n_hosts = n_hosts;
+    R.n_nodes = n_nodes;
+    R.ready = true;
+    return SHD_OK;
+}
+
+shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const shd_round* round,
+                                  shd_relay_out* d_out) {
+    if (!ctx || !d_batch || !round || !d_out) return SHD_ERR_INVALID;
+    if (!ctx->relay.ready) return SHD_ERR_STATE;
+    if (!d_batch->src_off || (d_batch->n_packets && (!d_batch->send_time || !d_batch->dst_host ||
+                                                     !d_batch->payload)))
+        return SHD_ERR_INVALID;
+    if (!d_out->status || !d_out->ev_off || !d_out->ev_deliver || !d_out->ev_src ||
+        !d_out->ev_seq || !d_out->ev_pkt)
+        return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    return relay_device(ctx, d_batch, round, d_out, true);
+}
+
+shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round* round,
+                           shd_relay_out* out) {
+    if (!ctx || !batch || !round || !out || !batch->src_off) return SHD_ERR_INVALID;
+    RelayState& R = ctx->relay;
+    if (!R.ready) return SHD_ERR_STATE;
+    SHD_HIP(hipSetDevice(ctx->device));
+    const uint64_t n = batch->n_packets;
+    const uint32_t H = R.n_hosts;
+    if (batch->src_off[0] != 0 || batch->src_off[H] != n) return SHD_ERR_INVALID;
+    for (uint32_t h = 0; h < H; h++)
+        if (batch->src_off[h + 1] < batch->src_off[h]) return SHD_ERR_INVALID;
+    hipStream_t s = ctx->stream;
+    const size_t nn = std::max<uint64_t>(n, 1);
+    SHD_TRY(R.pk_off.ensure((size_t)(H + 1) * 4));
+    SHD_TRY(R.pk_time.ensure(nn * 8));
+    SHD_TRY(R.pk_dst.ensure(nn * 4));
+    SHD_TRY(R.pk_pay.ensure(nn * 4));
+    SHD_TRY(R.st.ensure(nn));
+    SHD_TRY(R.ev_off.ensure((size_t)(H + 1) * 4));
+    SHD_TRY(R.ev_deliver.ensure(nn * 8));
+    SHD_TRY(R.ev_src.ensure(nn * 4));
+    SHD_TRY(R.ev_seq.ensure(nn * 8));
+    SHD_TRY(R.ev_pkt.ensure(nn * 4));
+    SHD_HIP(hipMemcpyAsync(R.pk_off.p, batch->src_off, (size_t)(H + 1) * 4, hipMemcpyHostToDevice, s));
+    if (n) {
+        SHD_HIP(hipMemcpyAsync(R.pk_time.p, batch->send_time, n * 8, hipMemcpyHostToDevice, s));
+        SHD_HIP(hipMemcpyAsync(R.pk_dst.p, batch->dst_host, n * 4, hipMemcpyHostToDevice, s));
+        SHD_HIP(hipMemcpyAsync(R.pk_pay.p, batch->payload, n * 4, hipMemcpyHostToDevice, s));
+    }
+    const double* d_chance = nullptr;
+    if (batch->chance && n) {
+        SHD_TRY(R.pk_chance.ensure(n * 8));
+        SHD_HIP(hipMemcpyAsync(R.pk_chance.p, batch->chance, n * 8, hipMemcpyHostToDevice, s));
+        d_chance = R.pk_chance.as<double>();
+    }
+    shd_batch db{n, R.pk_off.as<uint32_t>(), R.pk_time.as<uint64_t>(), R.pk_dst.as<uint32_t>(),
+                 R.pk_pay.as<uint32_t>(), d_chance};
+    shd_relay_out dout{};
+    dout.status = R.st.as<uint8_t>();
+    dout.ev_off = R.ev_off.as<uint32_t>();
+    dout.ev_deliver = R.ev_deliver.as<uint64_t>();
+    dout.ev_src = R.ev_src.as<uint32_t>();
+    dout.ev_seq = R.ev_seq.as<uint64_t>();
+    dout.ev_pkt = R.ev_pkt.as<uint32_t>();
+    SHD_TRY(relay_device(ctx, &db, round, &dout, true));
+    const uint64_t ns = dout.n_sent;
+    if (out->status && n) SHD_HIP(hipMemcpyAsync(out->status, dout.status, n, hipMemcpyDeviceToHost, s));
+    if (out->ev_off) SHD_HIP(hipMemcpyAsync(out->ev_off, dout.ev_off, (size_t)(H + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (ns) {
+        if (out->ev_deliver) SHD_HIP(hipMemcpyAsync(out->ev_deliver, dout.ev_deliver, ns * 8, hipMemcpyDeviceToHost, s));
+        if (out->ev_src) SHD_HIP(hipMemcpyAsync(out->ev_src, dout.ev_src, ns * 4, hipMemcpyDeviceToHost, s));
+        if (out->ev_seq) SHD_HIP(hipMemcpyAsync(out->ev_seq, dout.ev_seq, ns * 8, hipMemcpyDeviceToHost, s));
+        if (out->ev_pkt) SHD_HIP(hipMemcpyAsync(out->ev_pkt, dout.ev_pkt, ns * 4, hipMemcpyDeviceToHost, s));
+    }
+    SHD_HIP(hipStreamSynchronize(s));
+    out->min_deliver = dout.min_deliver;
+    out->min_latency = dout.min_latency;
+    out->n_sent = ns;
+    return SHD_OK;
+}
+
+shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t* next_event_id) {
+    if (!ctx) return SHD_ERR_INVALID;
+    RelayState& R = ctx->relay;
+    if (!R.ready) return SHD_ERR_STATE;
+    SHD_HIP(hipSetDevice(ctx->device));
+    if (rng_state)
+        SHD_HIP(hipMemcpyAsync(rng_state, R.rng.p, (size_t)R.n_hosts * 32, hipMemcpyDeviceToHost, ctx->stream));
+    if (next_event_id)
+        SHD_HIP(hipMemcpyAsync(next_event_id, R.next_id.p, (size_t)R.n_hosts * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SHD_HIP(hipStreamSynchronize(ctx->stream));
+    return SHD_OK;
+}
+
+shd_status shd_path_packet_counts(shd_ctx* ctx, uint64_t* counts) {
+    if (!ctx || !counts) return SHD_ERR_INVALID;
+    RelayState& R = ctx->relay;
+    if (!R.ready) return SHD_ERR_STATE;
+    SHD_HIP(hipSetDevice(ctx->device));
+    SHD_HIP(hipMemcpyAsync(counts, R.counts.p, (size_t)R.n_nodes * R.n_nodes * 8, hipMemcpyDeviceToHost, ctx->stream));
+    SHD_HIP(hipStreamSynchronize(ctx->stream));
+    return SHD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,573 @@
+// Routing build on gfx950: lexicographic (latency, loss) shortest paths into the dense
+// used-node table, and the direct-path mode.
+//
+// Reference semantics (FlyearthR/shadow src/main/network/graph/mod.rs):
+//   compute_shortest_paths :185-230 -- one petgraph Dijkstra per used source; the result of
+//     each is the lexicographic minimum over walks of the LEFT-FOLDED path cost (latency u64
+//     add; loss 1f32-(1f32-p)*(1f32-e), edge on the right).  Every non-loop edge strictly
+//     increases latency and the fold is monotone, so the minimum is a unique fixed point: any
+//     label-correcting relaxation that always appends one edge on the right converges to the
+//     same bits as Dijkstra.  That is what the kernels below do (never segment composition,
+//     which is not associative in f32 -- SURVEY F2).
+//   diagonal := the node's single self-loop edge, raw loss (:212-219); unreachable -> panic
+//     (:221); get_direct_paths :232-254 with get_edge_weight :258-295.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "ctx.h"
+
+namespace shd {
+
+// ------------------------------------------------------------------------------------------
+// Kernel 1: batched per-source SSSP, one workgroup per source row, labels in LDS.
+// Label = packed u64 key (lat32 << 32 | f32 loss bits); ds_min_rtn_u64 keeps the lexicographic
+// minimum exactly.  Active set = LDS bitmap; sweeps until a sweep improves nothing.
+// ------------------------------------------------------------------------------------------
+constexpr int kSsspBlock = 256;
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void sssp_lds_narrow(
+    const uint32_t* __restrict__ off, const uint32_t* __restrict__ adst,
+    const uint32_t* __restrict__ alat, const float* __restrict__ aq, uint32_t V,
+    const uint32_t* __restrict__ used, uint32_t n_used, uint32_t row_begin,
+    const uint64_t* __restrict__ diag_lat, const float* __restrict__ diag_loss,
+    uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, uint32_t* __restrict__ flags,
+    unsigned long long* __restrict__ unreach) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t* lab = reinterpret_cast<uint64_t*>(smem);
+    const uint32_t W = (V + 31) >> 5;
+    uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V);
+    uint32_t* ctl = bits + W;  // [0] dirty
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr uint32_t NW = BLOCK / 64;
+    const uint32_t row = row_begin + blockIdx.x;
+    const uint32_t src = used[row];
+
+    for (uint32_t v = tid; v < V; v += BLOCK) lab[v] = kKeyInf;
+    for (uint32_t w = tid; w < W; w += BLOCK) bits[w] = 0;
+    __syncthreads();
+    if (tid == 0) {
+        lab[src] = 0;  // PathProperties::default() = (0 ns, 0.0)
+        bits[src >> 5] = 1u << (src & 31);
+    }
+    bool ovf = false;
+    for (;;) {
+        if (tid == 0) ctl[0] = 0;
+        __syncthreads();
+        bool dirty = false;
+        // each wave takes word pairs (lane l <-> node 32*word + (l & 31))
+        for (uint32_t base = 2 * wave; base < W; base += 2 * NW) {
+            const uint32_t widx = base + (lane >> 5);
+            uint32_t peek = widx < W ? __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP)
+                                     : 0u;
+            if (__ballot(peek != 0) == 0) continue;  // wave-uniform skip of empty pairs
+            uint32_t word = 0;
+            if ((lane & 31) == 0 && peek) word = atomicExch(&bits[widx], 0u);
+            word = __shfl(word, lane & 32);
+            if ((word >> (lane & 31)) & 1u) {
+                const uint32_t u = widx * 32 + (lane & 31);
+                const uint64_t ku = __hip_atomic_load(&lab[u], __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t lu = key_lat(ku);
+                const float qu = one_minus(key_loss(ku));
+                const uint32_t k1 = off[u + 1];
+                for (uint32_t k = off[u]; k < k1; ++k) {
+                    const uint32_t v = adst[k];
+                    const uint32_t cl = lu + alat[k];
+                    if (cl < lu || cl == kLat32Inf) {  // path latency leaves u32: wide rerun
+                        ovf = true;
+                        continue;
+                    }
+                    const uint64_t cand = pack_key(cl, fold_q(qu, aq[k]));
+                    const uint64_t old = atomicMin(reinterpret_cast<unsigned long long*>(&lab[v]),
+                                                   (unsigned long long)cand);
+                    if (cand < old) {
+                        atomicOr(&bits[v >> 5], 1u << (v & 31));
+                        dirty = true;
+                    }
+                }
+            }
+        }
+        if (dirty) ctl[0] = 1;
+        __syncthreads();
+        const bool again = ctl[0] != 0;
+        __syncthreads();
+        if (!again) break;
+    }
+    if (ovf) atomicOr(&flags[0], 1u);
+    // write the row in `used` order; diagonal = self-loop edge
+    const size_t orow = (size_t)blockIdx.x * n_used;
+    for (uint32_t j = tid; j < n_used; j += BLOCK) {
+        uint64_t l;
+        float p;
+        if (j == row) {
+            l = diag_lat[j];
+            p = diag_loss[j];
+        } else {
+            const uint64_t k = lab[used[j]];
+            if (k == kKeyInf) {
+                atomicMin(unreach, (unsigned long long)((uint64_t)row * n_used + j));
+                l = ~0ull;
+                p = 0.0f;
+            } else {
+                l = key_lat(k);
+                p = key_loss(k);
+            }
+        }
+        out_lat[orow + j] = l;
+        out_loss[orow + j] = p;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Kernel 2 (wide fallback): u64 latencies, labels in global memory, pull-form Jacobi rounds
+// over in-arcs.  Used only when some path latency reaches 2^32-1 ns (or V exceeds the LDS).
+// One launch = one round for a batch of sources; grid (ceil(V/256), n_src).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sssp_wide_round(
+    const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
+    const uint64_t* __restrict__ in_lat, const float* __restrict__ in_q, uint32_t V,
+    const uint64_t* __restrict__ a_lat, const float* __restrict__ a_loss,
+    uint64_t* __restrict__ b_lat, float* __restrict__ b_loss, uint32_t* __restrict__ changed,
+    uint32_t* __restrict__ flags) {
+    const uint32_t v = blockIdx.x * 256 + threadIdx.x;
+    const size_t s = blockIdx.y;
+    if (v >= V) return;
+    const uint64_t* al = a_lat + s * V;
+    const float* ap = a_loss + s * V;
+    uint64_t bl = al[v];
+    float bp = ap[v];
+    bool ch = false;
+    for (uint32_t k = in_off[v]; k < in_off[v + 1]; ++k) {
+        const uint32_t u = in_src[k];
+        const uint64_t lu = al[u];
+        if (lu == ~0ull) continue;
+        const uint64_t cl = lu + in_lat[k];
+        if (cl < lu || cl == ~0ull) {
+            atomicOr(&flags[1], 1u);  // exceeds u64: LATENCY_OVERFLOW
+            continue;
+        }
+        const float cp = fold_q(one_minus(ap[u]), in_q[k]);
+        if (cl < bl || (cl == bl && cp < bp)) {
+            bl = cl;
+            bp = cp;
+            ch = true;
+        }
+    }
+    b_lat[s * V + v] = bl;
+    b_loss[s * V + v] = bp;
+    if (ch) changed[0] = 1;
+}
+
+__global__ void wide_init(uint64_t* lat, float* loss, uint32_t V, const uint32_t* used,
+                          uint32_t row0) {
+    const uint32_t v = blockIdx.x * 256 + threadIdx.x;
+    const size_t s = blockIdx.y;
+    if (v >= V) return;
+    const bool is_src = used[row0 + s] == v;
+    lat[s * V + v] = is_src ? 0ull : ~0ull;
+    loss[s * V + v] = 0.0f;
+}
+
+__global__ void wide_emit(const uint64_t* __restrict__ lat, const float* __restrict__ loss,
+                          uint32_t V, const uint32_t* __restrict__ used, uint32_t n_used,
+                          uint32_t row0, uint32_t out_row0, const uint64_t* __restrict__ diag_lat,
+                          const float* __restrict__ diag_loss, uint64_t* __restrict__ out_lat,
+                          float* __restrict__ out_loss, unsigned long long* __restrict__ unreach) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    const size_t s = blockIdx.y;
+    if (j >= n_used) return;
+    const uint32_t row = row0 + (uint32_t)s;
+    uint64_t l;
+    float p;
+    if (j == row) {
+        l = diag_lat[j];
+        p = diag_loss[j];
+    } else {
+        l = lat[s * V + used[j]];
+        p = loss[s * V + used[j]];
+        if (l == ~0ull) atomicMin(unreach, (unsigned long long)((uint64_t)row * n_used + j));
+    }
+    const size_t o = (size_t)(out_row0 + s) * n_used + j;
+    out_lat[o] = l;
+    out_loss[o] = p;
+}
+
+__global__ void arcs_q(const float* __restrict__ loss, float* __restrict__ q, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) q[i] = one_minus(loss[i]);
+}
+
+// ------------------------------------------------------------------------------------------
+// Direct-path mode: count edges per ordered used pair, keep the edge's raw (lat, loss);
+// the first pair (src-major in `used` order) without exactly one edge is the error.
+// ------------------------------------------------------------------------------------------
+__global__ void direct_scatter(const uint32_t* __restrict__ es, const uint32_t* __restrict__ ed,
+                               const uint64_t* __restrict__ el, const float* __restrict__ ep,
+                               uint32_t E, int directed, const int32_t* __restrict__ col,
+                               uint32_t n_used, uint32_t* __restrict__ cnt,
+                               uint64_t* __restrict__ tl, float* __restrict__ tp) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= E) return;
+    const int32_t a = col[es[i]], b = col[ed[i]];
+    if (a < 0 || b < 0) return;
+    size_t c = (size_t)a * n_used + b;
+    atomicAdd(&cnt[c], 1u);
+    tl[c] = el[i];
+    tp[c] = ep[i];
+    if (!directed && a != b) {
+        c = (size_t)b * n_used + a;
+        atomicAdd(&cnt[c], 1u);
+        tl[c] = el[i];
+        tp[c] = ep[i];
+    }
+}
+
+__global__ void direct_check(const uint32_t* __restrict__ cnt, uint64_t nn,
+                             unsigned long long* __restrict__ first_bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nn && cnt[i] != 1u) atomicMin(first_bad, (unsigned long long)i);
+}
+
+// ------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------
+struct HostGraph {
+    uint32_t V = 0;
+    std::vector<uint32_t> off, dst;      // out-CSR without self-loops (petgraph edges(node))
+    std::vector<uint64_t> lat;
+    std::vector<float> loss;
+    std::vector<uint64_t> diag_lat;      // per used index
+    std::vector<float> diag_loss;
+    uint64_t max_arc_lat = 0;
+};
+
+static uint32_t gml_id(const shd_graph* g, uint32_t idx) {
+    return g->node_ids ? g->node_ids[idx] : idx;
+}
+
+static shd_status set_err(shd_error* err, shd_status st, uint32_t a, uint32_t b) {
+    if (err) {
+        err->code = st;
+        err->node_a = a;
+        err->node_b = b;
+    }
+    return st;
+}
+
+static shd_status validate(const shd_graph* g, const uint32_t* used, uint32_t n_used) {
+    if (!g || !used || n_used == 0) return SHD_ERR_INVALID;
+    if (g->n_edges && (!g->edge_src || !g->edge_dst || !g->edge_latency_ns || !g->edge_packet_loss))
+        return SHD_ERR_INVALID;
+    for (uint32_t i = 0; i < g->n_edges; i++) {
+        if (g->edge_src[i] >= g->n_nodes || g->edge_dst[i] >= g->n_nodes) return SHD_ERR_INVALID;
+        const float p = g->edge_packet_loss[i];
+        if (!(p >= 0.0f && p <= 1.0f)) return SHD_ERR_INVALID;  // ShadowEdge::try_from range
+    }
+    std::vector<uint8_t> seen(g->n_nodes, 0);
+    for (uint32_t i = 0; i < n_used; i++) {
+        if (used[i] >= g->n_nodes || seen[used[i]]) return SHD_ERR_INVALID;
+        seen[used[i]] = 1;
+    }
+    return SHD_OK;
+}
+
+// Self-loop rule (graph/mod.rs:212-219 via get_edge_weight): exactly one per used node, first
+// offender in `used` order.  Fills the diagonal values.
+static shd_status diag_from_self_loops(const shd_graph* g, const uint32_t* used, uint32_t n_used,
+                                       HostGraph& H, shd_error* err) {
+    std::vector<uint32_t> cnt(g->n_nodes, 0), first(g->n_nodes, 0);
+    for (uint32_t i = 0; i < g->n_edges; i++) {
+        if (g->edge_src[i] != g->edge_dst[i]) continue;
+        const uint32_t v = g->edge_src[i];
+        if (cnt[v]++ == 0) first[v] = i;
+    }
+    H.diag_lat.resize(n_used);
+    H.diag_loss.resize(n_used);
+    for (uint32_t j = 0; j < n_used; j++) {
+        const uint32_t v = used[j];
+        if (cnt[v] == 0) return set_err(err, SHD_ERR_NO_EDGE, gml_id(g, v), gml_id(g, v));
+        if (cnt[v] > 1) return set_err(err, SHD_ERR_MULTI_EDGE, gml_id(g, v), gml_id(g, v));
+        H.diag_lat[j] = g->edge_latency_ns[first[v]];
+        H.diag_loss[j] = g->edge_packet_loss[first[v]];
+    }
+    return SHD_OK;
+}
+
+static void build_csr(const shd_graph* g, bool reverse, HostGraph& H) {
+    const uint32_t V = g->n_nodes;
+    H.V = V;
+    H.off.assign(V + 1, 0);
+    for (uint32_t i = 0; i < g->n_edges; i++) {
+        const uint32_t a = g->edge_src[i], b = g->edge_dst[i];
+        if (a == b) continue;  // a self-loop never improves a label (latency > 0)
+        H.off[(reverse && g->directed ? b : a) + 1]++;
+        if (!g->directed) H.off[b + 1]++;
+    }
+    for (uint32_t v = 0; v < V; v++) H.off[v + 1] += H.off[v];
+    const size_t A = H.off[V];
+    H.dst.resize(A);
+    H.lat.resize(A);
+    H.loss.resize(A);
+    std::vector<uint32_t> fill(H.off.begin(), H.off.end() - 1);
+    H.max_arc_lat = 0;
+    for (uint32_t i = 0; i < g->n_edges; i++) {
+        const uint32_t a = g->edge_src[i], b = g->edge_dst[i];
+        if (a == b) continue;
+        const uint64_t l = g->edge_latency_ns[i];
+        const float p = g->edge_packet_loss[i];
+        H.max_arc_lat = std::max(H.max_arc_lat, l);
+        auto put = [&](uint32_t from, uint32_t to) {
+            const uint32_t k = fill[from]++;
+            H.dst[k] = to;
+            H.lat[k] = l;
+            H.loss[k] = p;
+        };
+        if (g->directed) {
+            if (reverse) put(b, a); else put(a, b);
+        } else {
+            put(a, b);
+            put(b, a);
+        }
+    }
+}
+
+template <class T>
+static shd_status upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
+    SHD_TRY(b.ensure(std::max<size_t>(v.size(), 1) * sizeof(T)));
+    if (!v.empty()) SHD_HIP(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+    return SHD_OK;
+}
+
+static shd_status check_unreach(shd_ctx* ctx, shd_error* err) {
+    PreparedGraph& P = ctx->prep;
+    unsigned long long bad = 0;
+    SHD_HIP(hipMemcpyAsync(&bad, ctx->g_flags.as<char>() + 16, 8, hipMemcpyDeviceToHost, ctx->stream));
+    SHD_HIP(hipStreamSynchronize(ctx->stream));
+    if (bad != ~0ull) {
+        const uint32_t r = (uint32_t)(bad / P.n_used), c = (uint32_t)(bad % P.n_used);
+        return set_err(err, SHD_ERR_UNREACHABLE, P.node_ids[P.used[r]], P.node_ids[P.used[c]]);
+    }
+    return SHD_OK;
+}
+
+static shd_status reset_flags(shd_ctx* ctx) {
+    SHD_TRY(ctx->g_flags.ensure(64));
+    SHD_HIP(hipMemsetAsync(ctx->g_flags.p, 0, 16, ctx->stream));
+    SHD_HIP(hipMemsetAsync(ctx->g_flags.as<char>() + 16, 0xFF, 8, ctx->stream));
+    return SHD_OK;
+}
+
+// Wide path: u64 latency, global labels, Jacobi rounds over in-arcs; batches of sources.
+static shd_status run_wide(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d_lat, float* d_loss,
+                           shd_error* err) {
+    PreparedGraph& P = ctx->prep;
+    shd_graph g = P.view();
+    HostGraph R;
+    build_csr(&g, /*reverse=*/true, R);
+    hipStream_t s = ctx->stream;
+    DevBuf w_off, w_src, w_lat, w_loss, w_q;
+    SHD_TRY(upload(w_off, R.off, s));
+    SHD_TRY(upload(w_src, R.dst, s));
+    SHD_TRY(upload(w_lat, R.lat, s));
+    SHD_TRY(upload(w_loss, R.loss, s));
+    SHD_TRY(w_q.ensure(std::max<size_t>(R.loss.size(), 1) * 4));
+    if (!R.loss.empty())
+        arcs_q<<<div_up(R.loss.size(), 256), 256, 0, s>>>(w_loss.as<float>(), w_q.as<float>(), R.loss.size());
+    const uint32_t V = R.V, n_used = P.n_used;
+    const uint32_t batch = std::max<uint32_t>(
+        1, std::min<uint32_t>(re - rb, (uint32_t)((1ull << 30) / (24ull * V))));
+    DevBuf la, pa, lb, pb, ch;
+    SHD_TRY(la.ensure((size_t)batch * V * 8));
+    SHD_TRY(lb.ensure((size_t)batch * V * 8));
+    SHD_TRY(pa.ensure((size_t)batch * V * 4));
+    SHD_TRY(pb.ensure((size_t)batch * V * 4));
+    SHD_TRY(ch.ensure(4));
+    for (uint32_t r0 = rb; r0 < re; r0 += batch) {
+        const uint32_t nb = std::min(batch, re - r0);
+        dim3 gv(div_up(V, 256), nb);
+        wide_init<<<gv, 256, 0, s>>>(la.as<uint64_t>(), pa.as<float>(), V, ctx->g_used.as<uint32_t>(), r0);
+        for (;;) {
+            SHD_HIP(hipMemsetAsync(ch.p, 0, 4, s));
+            sssp_wide_round<<<gv, 256, 0, s>>>(w_off.as<uint32_t>(), w_src.as<uint32_t>(),
+                                               w_lat.as<uint64_t>(), w_q.as<float>(), V,
+                                               la.as<uint64_t>(), pa.as<float>(), lb.as<uint64_t>(),
+                                               pb.as<float>(), ch.as<uint32_t>(), ctx->g_flags.as<uint32_t>());
+            uint32_t changed = 0;
+            SHD_HIP(hipMemcpyAsync(&changed, ch.p, 4, hipMemcpyDeviceToHost, s));
+            SHD_HIP(hipStreamSynchronize(s));
+            std::swap(la, lb);
+            std::swap(pa, pb);
+            if (!changed) break;
+        }
+        dim3 ge(div_up(n_used, 256), nb);
+        wide_emit<<<ge, 256, 0, s>>>(la.as<uint64_t>(), pa.as<float>(), V, ctx->g_used.as<uint32_t>(),
+                                     n_used, r0, r0 - rb, ctx->g_diag_lat.as<uint64_t>(),
+                                     ctx->g_diag_loss.as<float>(), d_lat, d_loss,
+                                     reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16));
+    }
+    uint32_t fl[2] = {0, 0};
+    SHD_HIP(hipMemcpyAsync(fl, ctx->g_flags.p, 8, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    if (fl[1]) return set_err(err, SHD_ERR_LATENCY_OVERFLOW, 0, 0);
+    ctx->info.wide_latency = 1;
+    return check_unreach(ctx, err);
+}
+
+shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
+                                uint32_t n_used, uint32_t mode, shd_error* err) {
+    if (err) *err = shd_error{SHD_OK, 0, 0};
+    PreparedGraph& P = ctx->prep;
+    P.ready = false;
+    SHD_TRY(validate(g, used, n_used));
+    if (mode != SHD_ROUTE_SHORTEST && mode != SHD_ROUTE_DIRECT) return SHD_ERR_INVALID;
+    hipStream_t s = ctx->stream;
+    P.mode = mode;
+    P.V = g->n_nodes;
+    P.n_used = n_used;
+    P.directed = g->directed != 0;
+    P.used.assign(used, used + n_used);
+    P.node_ids.resize(g->n_nodes);
+    for (uint32_t v = 0; v < g->n_nodes; v++) P.node_ids[v] = gml_id(g, v);
+    P.es.assign(g->edge_src, g->edge_src + g->n_edges);
+    P.ed.assign(g->edge_dst, g->edge_dst + g->n_edges);
+    P.el.assign(g->edge_latency_ns, g->edge_latency_ns + g->n_edges);
+    P.ep.assign(g->edge_packet_loss, g->edge_packet_loss + g->n_edges);
+    SHD_TRY(upload(ctx->g_used, P.used, s));
+    if (mode == SHD_ROUTE_DIRECT) {
+        std::vector<int32_t> col(g->n_nodes, -1);
+        for (uint32_t j = 0; j < n_used; j++) col[used[j]] = (int32_t)j;
+        SHD_TRY(upload(ctx->d_es, P.es, s));
+        SHD_TRY(upload(ctx->d_ed, P.ed, s));
+        SHD_TRY(upload(ctx->d_el, P.el, s));
+        SHD_TRY(upload(ctx->d_ep, P.ep, s));
+        SHD_TRY(upload(ctx->d_col, col, s));
+    } else {
+        HostGraph H;
+        SHD_TRY(diag_from_self_loops(g, used, n_used, H, err));
+        SHD_TRY(upload(ctx->g_diag_lat, H.diag_lat, s));
+        SHD_TRY(upload(ctx->g_diag_loss, H.diag_loss, s));
+        build_csr(g, /*reverse=*/false, H);
+        P.arcs = H.dst.size();
+        P.max_arc_lat = H.max_arc_lat;
+        P.narrow_arcs = H.max_arc_lat < kLat32Inf;
+        if (P.narrow_arcs) {
+            std::vector<uint32_t> l32(H.lat.begin(), H.lat.end());
+            SHD_TRY(upload(ctx->g_off, H.off, s));
+            SHD_TRY(upload(ctx->g_dst, H.dst, s));
+            SHD_TRY(upload(ctx->g_lat, l32, s));
+            SHD_TRY(upload(ctx->g_aux, H.loss, s));
+            SHD_TRY(ctx->g_q.ensure(std::max<size_t>(H.loss.size(), 1) * 4));
+            if (!H.loss.empty())
+                arcs_q<<<div_up(H.loss.size(), 256), 256, 0, s>>>(ctx->g_aux.as<float>(),
+                                                                 ctx->g_q.as<float>(), H.loss.size());
+        }
+    }
+    SHD_HIP(hipStreamSynchronize(s));
+    P.ready = true;
+    return SHD_OK;
+}
+
+static shd_status run_direct(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d_lat,
+                             float* d_loss, shd_error* err) {
+    PreparedGraph& P = ctx->prep;
+    hipStream_t s = ctx->stream;
+    const uint32_t n_used = P.n_used;
+    const uint64_t nn = (uint64_t)n_used * n_used;
+    const uint32_t E = (uint32_t)P.es.size();
+    DevBuf cnt, tl, tp;
+    SHD_TRY(cnt.ensure(nn * 4));
+    SHD_TRY(tl.ensure(nn * 8));
+    SHD_TRY(tp.ensure(nn * 4));
+    SHD_HIP(hipEventRecord(ctx->ev[2], s));
+    SHD_HIP(hipMemsetAsync(cnt.p, 0, nn * 4, s));
+    if (E)
+        direct_scatter<<<div_up(E, 256), 256, 0, s>>>(
+            ctx->d_es.as<uint32_t>(), ctx->d_ed.as<uint32_t>(), ctx->d_el.as<uint64_t>(),
+            ctx->d_ep.as<float>(), E, P.directed, ctx->d_col.as<int32_t>(), n_used,
+            cnt.as<uint32_t>(), tl.as<uint64_t>(), tp.as<float>());
+    auto* bad_d = reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16);
+    direct_check<<<div_up(nn, 256), 256, 0, s>>>(cnt.as<uint32_t>(), nn, bad_d);
+    const size_t rows = re - rb;
+    SHD_HIP(hipMemcpyAsync(d_lat, tl.as<uint64_t>() + (size_t)rb * n_used, rows * n_used * 8,
+                           hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipMemcpyAsync(d_loss, tp.as<float>() + (size_t)rb * n_used, rows * n_used * 4,
+                           hipMemcpyDeviceToDevice, s));
+    SHD_HIP(hipEventRecord(ctx->ev[1], s));
+    unsigned long long bad = 0;
+    SHD_HIP(hipMemcpyAsync(&bad, bad_d, 8, hipMemcpyDeviceToHost, s));
+    uint32_t c = 0;
+    SHD_HIP(hipStreamSynchronize(s));
+    if (bad != ~0ull) {
+        SHD_HIP(hipMemcpyAsync(&c, cnt.as<uint32_t>() + bad, 4, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipStreamSynchronize(s));
+        const uint32_t r = (uint32_t)(bad / n_used), q = (uint32_t)(bad % n_used);
+        return set_err(err, c == 0 ? SHD_ERR_NO_EDGE : SHD_ERR_MULTI_EDGE, P.node_ids[P.used[r]],
+                       P.node_ids[P.used[q]]);
+    }
+    return SHD_OK;
+}
+
+static shd_status run_sssp(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d_lat, float* d_loss,
+                           bool* ovf) {
+    PreparedGraph& P = ctx->prep;
+    hipStream_t s = ctx->stream;
+    const uint32_t V = P.V;
+    const size_t lds = (size_t)V * 8 + (size_t)((V + 31) / 32) * 4 + 16;
+    SHD_HIP(hipEventRecord(ctx->ev[2], s));
+    sssp_lds_narrow<kSsspBlock><<<re - rb, kSsspBlock, lds, s>>>(
+        ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(), ctx->g_lat.as<uint32_t>(),
+        ctx->g_q.as<float>(), V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
+        ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
+        ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16));
+    SHD_HIP(hipGetLastError());
+    SHD_HIP(hipEventRecord(ctx->ev[3], s));
+    ctx->info.algo_used = SHD_ALGO_SSSP;
+    uint32_t fl = 0;
+    SHD_HIP(hipMemcpyAsync(&fl, ctx->g_flags.p, 4, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    *ovf = fl != 0;
+    return SHD_OK;
+}
+
+shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t re,
+                            uint64_t* d_lat, float* d_loss, shd_error* err) {
+    if (err) *err = shd_error{SHD_OK, 0, 0};
+    PreparedGraph& P = ctx->prep;
+    if (!P.ready) return SHD_ERR_STATE;
+    if (re == 0) re = P.n_used;
+    if (rb >= re || re > P.n_used) return SHD_ERR_INVALID;
+    hipStream_t s = ctx->stream;
+    ctx->info = shd_routing_info{};
+    ctx->info.arcs = P.arcs;
+    ctx->info.arcs_kept = P.arcs;
+    SHD_TRY(reset_flags(ctx));
+    SHD_HIP(hipEventRecord(ctx->ev[0], s));
+    if (P.mode == SHD_ROUTE_DIRECT) {
+        shd_status st = run_direct(ctx, rb, re, d_lat, d_loss, err);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+        ctx->info.ms_total = ctx->info.ms_main = ms;
+        return st;
+    }
+    const size_t lds = (size_t)P.V * 8 + (size_t)((P.V + 31) / 32) * 4 + 16;
+    if (P.narrow_arcs && lds <= ctx->max_lds) {
+        bool ovf = false;
+        (void)algo;
+        SHD_TRY(run_sssp(ctx, rb, re, d_lat, d_loss, &ovf));
+        SHD_HIP(hipEventRecord(ctx->ev[1], s));
+        SHD_HIP(hipEventSynchronize(ctx->ev[1]));
+        float ms = 0, ms_main = 0;
+        (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+        (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);
+        ctx->info.ms_total = ms;
+        ctx->info.ms_main = ms_main;
+        if (!ovf) return check_unreach(ctx, err);
+        SHD_TRY(reset_flags(ctx));  // some path latency >= 2^32-1 ns: redo with u64 labels
+    }
+    return run_wide(ctx, rb, re, d_lat, d_loss, err);
+}
+
+}  // namespace shd

@@ -1,0 +1,109 @@
+"""Host-side mirror of the per-round packet relay (``Worker::send_packet`` batched per round).
+
+Mirrors ``src/main/core/worker.rs:328-413`` (send_packet), ``:497-629`` (WorkerShared tables,
+push_packet_to_host) and the destination ``EventQueue`` order (``core/work/event.rs:84-155``).
+A round's staged sends are flushed once at the round barrier (``core/manager.rs:455-464``);
+the result is, per destination host, its new packet events in the order its EventQueue would
+pop them, plus the round reductions (min deliver time, min latency used).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+from .routing import Engine, default_engine
+
+
+@dataclass
+class RoundResult:
+    status: np.ndarray        # u8 per packet: 0 skipped (now >= sim_end), 1 dropped, 2 sent
+    ev_off: np.ndarray        # u32 [n_hosts+1]: destination h's events are [ev_off[h], ev_off[h+1])
+    ev_deliver: np.ndarray    # u64 [n_sent]
+    ev_src: np.ndarray        # u32 [n_sent]
+    ev_seq: np.ndarray        # u64 [n_sent] (src_host_event_id)
+    ev_pkt: np.ndarray        # u32 [n_sent] index of the packet in the batch
+    min_deliver: int          # u64::MAX when nothing was sent
+    min_latency: int
+    n_sent: int
+
+    def events_for(self, dst: int):
+        a, b = int(self.ev_off[dst]), int(self.ev_off[dst + 1])
+        return list(zip(self.ev_deliver[a:b].tolist(), self.ev_src[a:b].tolist(),
+                        self.ev_seq[a:b].tolist(), self.ev_pkt[a:b].tolist()))
+
+
+def group_by_source(n_hosts: int, src_host: np.ndarray):
+    """Stable grouping of staged sends by source host -> (order, src_off).
+
+    Worker threads stage sends in per-thread buffers; each host runs on one thread per round,
+    so a stable sort by source keeps every host's send order.
+    """
+    src_host = np.asarray(src_host, np.uint32)
+    order = np.argsort(src_host, kind="stable")
+    counts = np.bincount(src_host, minlength=n_hosts)
+    off = np.zeros(n_hosts + 1, np.uint32)
+    np.cumsum(counts, out=off[1:])
+    return order, off
+
+
+class Relay:
+    """Device-resident relay tables of one GPU (``shd_relay_setup``)."""
+
+    def __init__(self, host_node, rng_state, next_event_id, lat=None, loss=None,
+                 engine: Engine | None = None):
+        self.eng = engine or default_engine()
+        self.host_node = np.ascontiguousarray(host_node, np.uint32)
+        self.n_hosts = len(self.host_node)
+        rng = np.ascontiguousarray(rng_state, np.uint64).reshape(self.n_hosts, 4)
+        nid = np.ascontiguousarray(next_event_id, np.uint64)
+        if lat is not None:
+            lat = np.ascontiguousarray(lat, np.uint64)
+            loss = np.ascontiguousarray(loss, np.float32)
+            n_nodes = lat.shape[0]
+        else:
+            n_nodes = int(self.host_node.max()) + 1
+        self.n_nodes = n_nodes
+        N.check(self.eng.lib.shd_relay_setup(self.eng.ctx, self.n_hosts, N.ptr(self.host_node),
+                                             n_nodes, N.ptr(lat), N.ptr(loss), N.ptr(rng),
+                                             N.ptr(nid)), "shd_relay_setup")
+
+    def round(self, src_off, send_time, dst_host, payload, round_end: int, sim_end: int,
+              bootstrap_end: int = 0, chance=None) -> RoundResult:
+        src_off = np.ascontiguousarray(src_off, np.uint32)
+        send_time = np.ascontiguousarray(send_time, np.uint64)
+        dst_host = np.ascontiguousarray(dst_host, np.uint32)
+        payload = np.ascontiguousarray(payload, np.uint32)
+        if chance is not None:
+            chance = np.ascontiguousarray(chance, np.float64)
+        n = len(send_time)
+        b = N.Batch(n, N.ptr(src_off).value, N.ptr(send_time).value, N.ptr(dst_host).value,
+                    N.ptr(payload).value, N.ptr(chance).value if chance is not None else None)
+        rd = N.Round(round_end, sim_end, bootstrap_end)
+        status = np.zeros(n, np.uint8)
+        ev_off = np.zeros(self.n_hosts + 1, np.uint32)
+        ev_deliver = np.zeros(n, np.uint64)
+        ev_src = np.zeros(n, np.uint32)
+        ev_seq = np.zeros(n, np.uint64)
+        ev_pkt = np.zeros(n, np.uint32)
+        out = N.RelayOut(N.ptr(status).value, N.ptr(ev_off).value, N.ptr(ev_deliver).value,
+                         N.ptr(ev_src).value, N.ptr(ev_seq).value, N.ptr(ev_pkt).value, 0, 0, 0)
+        N.check(self.eng.lib.shd_relay_round(self.eng.ctx, C.byref(b), C.byref(rd), C.byref(out)),
+                "shd_relay_round")
+        ns = out.n_sent
+        return RoundResult(status, ev_off, ev_deliver[:ns], ev_src[:ns], ev_seq[:ns], ev_pkt[:ns],
+                           out.min_deliver, out.min_latency, ns)
+
+    def host_state(self):
+        rng = np.zeros((self.n_hosts, 4), np.uint64)
+        nid = np.zeros(self.n_hosts, np.uint64)
+        N.check(self.eng.lib.shd_relay_get_host_state(self.eng.ctx, N.ptr(rng), N.ptr(nid)),
+                "shd_relay_get_host_state")
+        return rng, nid
+
+    def packet_counts(self):
+        c = np.zeros((self.n_nodes, self.n_nodes), np.uint64)
+        N.check(self.eng.lib.shd_path_packet_counts(self.eng.ctx, N.ptr(c)), "packet_counts")
+        return c

@@ -1,0 +1,129 @@
+"""GPU parity tests of the per-round relay: statuses, event order per destination, RNG streams,
+event ids and round reductions, bit-exact against the golden fixtures and the C restatement."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import corc
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _u64(xs):
+    return np.asarray([int(v) for v in xs], np.uint64)
+
+
+def test_golden_relay_cases(engine):
+    from shadow_amd.relay import Relay
+    for case in json.load(open(os.path.join(GOLD, "relay_cases.json"))):
+        rng = np.asarray([[int(v) for v in r] for r in case["rng"]], np.uint64).reshape(-1, 4)
+        rl = Relay(case["host_node"], rng, _u64(case["next_id"]), np.asarray(case["lat"], np.uint64),
+                   np.asarray(case["loss_bits"], np.uint32).view(np.float32), engine=engine)
+        r = rl.round(case["src_off"], _u64(case["send_time"]), case["dst_host"], case["payload"],
+                     int(case["round_end"]), int(case["sim_end"]), int(case["bootstrap_end"]))
+        e = case["expect"]
+        assert r.status.tolist() == e["status"], case["name"]
+        assert r.ev_off.tolist() == e["ev_off"], case["name"]
+        got = [[str(t), int(s), str(q), int(p)] for t, s, q, p in
+               zip(r.ev_deliver.tolist(), r.ev_src.tolist(), r.ev_seq.tolist(), r.ev_pkt.tolist())]
+        assert got == e["ev"], case["name"]
+        assert str(r.min_deliver) == e["min_deliver"] and str(r.min_latency) == e["min_latency"]
+        st, nid = rl.host_state()
+        assert [[str(v) for v in row] for row in st.tolist()] == e["rng"]
+        assert [str(v) for v in nid.tolist()] == e["next_id"]
+
+
+def _c5_like(n_hosts, n_nodes, n_packets, seed, start=10**9, runahead=10**6):
+    from shadow_amd import synth
+    el = synth.complete_graph(n_nodes, seed)
+    used = np.arange(n_nodes, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(n_nodes, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    b = synth.packet_batch(n_hosts, n_packets, start, start + runahead, seed=seed)
+    return lat, loss, synth.c5_host_nodes(n_hosts, n_nodes), synth.host_rng_states(n_hosts, 1), b
+
+
+@pytest.mark.parametrize("chance_mode", [False, True])
+def test_multi_round_vs_c_oracle(engine, chance_mode):
+    """Three consecutive rounds on 20k hosts / 1M packets: streams and ids carry across rounds."""
+    from shadow_amd.relay import Relay
+    H, NN = 20_000, 200
+    lat, loss, host_node, rng0, _ = _c5_like(H, NN, 1000, 11)
+    nid0 = np.zeros(H, np.uint64)
+    rl = Relay(host_node, rng0, nid0, lat, loss, engine=engine)
+    orng, onid = rng0.copy(), nid0.copy()
+    start, ra = 10**9, 10**6
+    for rnd in range(3):
+        from shadow_amd import synth
+        b = synth.packet_batch(H, 1_000_000, start, start + ra, seed=50 + rnd)
+        chance = np.random.default_rng(rnd).random(b.n) if chance_mode else None
+        o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss,
+                             orng, onid, start + ra, start + 100 * ra, start + ra // 2 if rnd == 0 else 0,
+                             chance=chance)
+        r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, start + ra, start + 100 * ra,
+                     start + ra // 2 if rnd == 0 else 0, chance=chance)
+        assert np.array_equal(r.status, o["status"])
+        ev = o["events"]
+        assert np.array_equal(r.ev_off, ev["off"])
+        assert np.array_equal(r.ev_deliver, ev["deliver"])
+        assert np.array_equal(r.ev_src, ev["src"])
+        assert np.array_equal(r.ev_seq, ev["seq"])
+        assert np.array_equal(r.ev_pkt, ev["pkt"])
+        assert (r.min_deliver, r.min_latency, r.n_sent) == (o["min_deliver"], o["min_latency"], o["n_sent"])
+        st, nid = rl.host_state()
+        assert np.array_equal(st, orng) and np.array_equal(nid, onid)
+        start += ra
+
+
+def test_hot_destination_bucket(engine):
+    """One destination receiving far more than one LDS bucket (oversized-segment sort path)."""
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    H, NN = 500, 20
+    lat, loss, host_node, rng0, b = _c5_like(H, NN, 200_000, 5)
+    dst = b.dst_host.copy()
+    dst[::3] = 7
+    src = np.repeat(np.arange(H), np.diff(b.src_off)).astype(np.uint32)
+    dst[(dst == src)] = (dst[(dst == src)] + 1) % H
+    nid0 = np.zeros(H, np.uint64)
+    o = corc.relay_round(b.src_off, b.send_time, dst, b.payload, host_node, lat, loss, rng0.copy(),
+                         nid0.copy(), 10**9 + 10**6, 10**12, 0)
+    rl = Relay(host_node, rng0, nid0, lat, loss, engine=engine)
+    r = rl.round(b.src_off, b.send_time, dst, b.payload, 10**9 + 10**6, 10**12, 0)
+    ev = o["events"]
+    assert int(ev["off"][8] - ev["off"][7]) > 1024
+    assert np.array_equal(r.ev_off, ev["off"])
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(r, "ev_" + k), ev[k]), k
+    del synth
+
+
+def test_packet_counts(engine):
+    from shadow_amd.relay import Relay
+    H, NN = 1000, 30
+    lat, loss, host_node, rng0, b = _c5_like(H, NN, 50_000, 3)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, 10**9 + 10**6, 10**12, 0)
+    src = np.repeat(np.arange(H), np.diff(b.src_off))
+    sent = r.status == 2
+    want = np.zeros((NN, NN), np.uint64)
+    np.add.at(want, (host_node[src[sent]], host_node[b.dst_host[sent]]), 1)
+    assert np.array_equal(rl.packet_counts(), want)
+
+
+def test_empty_and_all_skipped_rounds(engine):
+    from shadow_amd.relay import Relay
+    H = 10
+    rl = Relay(np.zeros(H, np.uint32), np.ones((H, 4), np.uint64), np.zeros(H, np.uint64),
+               np.full((1, 1), 10**6, np.uint64), np.zeros((1, 1), np.float32), engine=engine)
+    r = rl.round(np.zeros(H + 1, np.uint32), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
+                 np.zeros(0, np.uint32), 10, 100, 0)
+    assert r.n_sent == 0 and r.min_deliver == 2**64 - 1
+    off = np.arange(H + 1, dtype=np.uint32)
+    r = rl.round(off, np.full(H, 500, np.uint64), (np.arange(H) + 1) % H, np.ones(H, np.uint32), 10, 100, 0)
+    assert r.n_sent == 0 and (r.status == 0).all()
+    st, _ = rl.host_state()
+    assert (st == 1).all()   # no draw for completed sends

@@ -1,0 +1,147 @@
+"""GPU parity tests of the routing build: HIP engine vs golden fixtures and the CPU oracle.
+Bit-exact latencies and loss bits; error codes and the GML ids they name."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import corc
+from tests.graphs import KAT_SHORTEST_PATH, engine_graph_from_edges, engine_graph_from_gml, random_graph
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+ALGOS = [0, 1, 2, 3, 4]
+
+
+def _graph(case):
+    from shadow_amd.routing import NetworkGraph
+    return NetworkGraph(case["node_ids"], case["src"], case["dst"], case["lat"],
+                        np.asarray(case["loss_bits"], np.uint32).view(np.float32), case["directed"])
+
+
+def _assert_table(t, lat, loss_bits):
+    assert np.array_equal(t.lat, np.asarray(lat, np.uint64))
+    assert np.array_equal(t.loss.view(np.uint32), np.asarray(loss_bits, np.uint32))
+
+
+@pytest.mark.parametrize("directed", [True, False])
+def test_reference_kat_shortest_path(engine, directed):
+    """The reference's own test_shortest_path (graph/mod.rs:562-649) through the engine."""
+    g = engine_graph_from_gml(KAT_SHORTEST_PATH.format(directed=int(directed)))
+    n0, n1, n2 = (g.node_id_to_index(i) for i in (0, 1, 2))
+    sp = g.compute_shortest_paths([n0, n1, n2], engine)
+    lat = lambda a, b: sp[(a, b)][0]  # noqa: E731
+    assert lat(n0, n0) == 3333 and lat(n1, n1) == 5555 and lat(n2, n2) == 7777
+    assert lat(n0, n1) == 3 and lat(n0, n2) == 7
+    if directed:
+        assert (lat(n1, n0), lat(n1, n2), lat(n2, n0), lat(n2, n1)) == (5, 12, 16, 11)
+    else:
+        assert (lat(n1, n0), lat(n1, n2), lat(n2, n0), lat(n2, n1)) == (3, 10, 7, 10)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_golden_routing_cases(engine, algo):
+    from shadow_amd.routing import NetGraphError, RoutingPanic
+    for case in json.load(open(os.path.join(GOLD, "routing_cases.json"))):
+        g = _graph(case)
+        exp = case["expect"]
+        build = (lambda: g.compute_shortest_paths(case["used"], engine, algo=algo)) \
+            if case["mode"] == "shortest" else (lambda: g.get_direct_paths(case["used"], engine))
+        if exp["status"] == "OK":
+            _assert_table(build(), exp["lat"], exp["loss_bits"])
+        elif exp["status"] == "UNREACHABLE":
+            with pytest.raises(RoutingPanic, match=f"node {exp['a']} to {exp['b']}"):
+                build()
+        else:
+            word = "No edge" if exp["status"] == "NO_EDGE" else "More than one edge"
+            with pytest.raises(NetGraphError, match=f"{word} connecting node {exp['a']} to {exp['b']}"):
+                build()
+
+
+@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("algo", ALGOS)
+def test_random_graphs_vs_c_oracle(engine, seed, algo):
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(2, 300))
+    ids, s, d, l, p, directed = random_graph(rng, n, float(rng.uniform(0.005, 0.3)), bool(seed % 2),
+                                             max_ms=int(rng.integers(2, 50)))
+    n_used = int(rng.integers(1, n + 1))
+    used = rng.choice(n, size=n_used, replace=False).astype(np.uint32)
+    code, lat, loss, _ = corc.routing(n, s, d, l, p, directed, used)
+    assert code == "OK"
+    from shadow_amd.routing import NetworkGraph
+    t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=algo)
+    _assert_table(t, lat, loss.view(np.uint32))
+
+
+def test_wide_latency_fallback(engine):
+    """Path latencies >= 2^32 ns take the u64 kernels; still bit-exact."""
+    rng = np.random.default_rng(7)
+    ids, s, d, l, p, directed = random_graph(rng, 60, 0.05, False)
+    l = (l // np.uint64(1_000_000)) * np.uint64(900_000_000)   # up to 18 s per edge
+    used = np.arange(60, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(60, s, d, l, p, directed, used)
+    assert code == "OK" and lat.max() > 2**32
+    from shadow_amd.routing import NetworkGraph
+    t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine)
+    _assert_table(t, lat, loss.view(np.uint32))
+    assert engine.last_info()["wide_latency"] == 1
+
+
+@pytest.fixture(scope="module")
+def c2_case():
+    from shadow_amd import synth
+    el = synth.complete_graph(1000, 1)
+    used = np.arange(1000, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(1000, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    return el, used, lat, loss
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_c2_full_bit_exact(engine, c2_case, algo):
+    """BASELINE config 2 (1k-node complete graph) against the C restatement."""
+    el, used, lat, loss = c2_case
+    t = engine_graph_from_edges(el).compute_shortest_paths(used, engine, algo=algo)
+    _assert_table(t, lat, loss.view(np.uint32))
+    assert engine.smallest_latency_ns() == int(lat.min())
+
+
+def test_c3_rows_bit_exact(engine):
+    """BASELINE config 3 (10k-node BA graph): a row slice against the C restatement."""
+    from shadow_amd import synth
+    el = synth.barabasi_albert(10_000, 3, 2)
+    used = np.arange(10_000, dtype=np.uint32)
+    rows = used[:64]
+    code, lat, loss, _ = corc.routing(10_000, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    g = engine_graph_from_edges(el)
+    for algo in (1, 3):
+        t = g.compute_shortest_paths(used, engine, algo=algo, rows=(0, 64))
+        _assert_table(t, lat[:64], loss[:64].view(np.uint32))
+        t = g.compute_shortest_paths(used, engine, algo=algo, rows=(5000, 5100))
+        _assert_table(t, lat[5000:5100], loss[5000:5100].view(np.uint32))
+    del rows
+
+
+def test_direct_paths_c2(engine):
+    from shadow_amd import synth
+    el = synth.complete_graph(300, 9)
+    used = np.random.default_rng(1).permutation(300).astype(np.uint32)
+    code, lat, loss, _ = corc.routing(300, el.src, el.dst, el.latency_ns, el.packet_loss, False, used,
+                                      shortest=False)
+    assert code == "OK"
+    t = engine_graph_from_edges(el).get_direct_paths(used, engine)
+    _assert_table(t, lat, loss.view(np.uint32))
+
+
+def test_row_shards_concatenate(engine):
+    from shadow_amd import synth
+    el = synth.complete_graph(257, 3)
+    used = np.arange(257, dtype=np.uint32)
+    g = engine_graph_from_edges(el)
+    full = g.compute_shortest_paths(used, engine)
+    parts = [g.compute_shortest_paths(used, engine, rows=(a, min(a + 64, 257))) for a in range(0, 257, 64)]
+    assert np.array_equal(np.concatenate([p.lat for p in parts]), full.lat)
+    assert np.array_equal(np.concatenate([p.loss for p in parts]).view(np.uint32), full.loss.view(np.uint32))
