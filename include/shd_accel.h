@@ -214,7 +214,10 @@ shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const 
 /* Read back the per-host RNG states / next event ids (e.g. to hand RNG use back to the CPU). */
 shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t* next_event_id);
 
-/* Per-path packet counters accumulated over all rounds (n_nodes x n_nodes u64, saturating). */
+/* Per-path packet counters (RoutingInfo::increment_packet_count, graph/mod.rs:451-458): on by
+ * default; the reference only reads them in log_packet_counts (never called), so a caller may
+ * turn them off.  Counts accumulate over all rounds (n_nodes x n_nodes u64). */
+shd_status shd_relay_set_counters(shd_ctx* ctx, int32_t enabled);
 shd_status shd_path_packet_counts(shd_ctx* ctx, uint64_t* counts);
 
 #ifdef __cplusplus

@@ -25,7 +25,8 @@ EXPORTED = [
     "shd_routing_build", "shd_routing_prepare", "shd_routing_run", "shd_routing_build_device",
     "shd_routing_last_info",
     "shd_routing_lookup", "shd_routing_smallest_latency", "shd_relay_setup", "shd_relay_round",
-    "shd_relay_round_device", "shd_relay_get_host_state", "shd_path_packet_counts",
+    "shd_relay_round_device", "shd_relay_get_host_state", "shd_relay_set_counters",
+    "shd_path_packet_counts",
 ]
 
 
@@ -80,6 +81,12 @@ def load(path: str = LIB_PATH) -> C.CDLL:
     if not os.path.exists(path):
         raise RuntimeError(f"shd_accel native library missing at {path}: run "
                            "`python -m shadow_amd.build` (or __graft_entry__.build())")
+    # torch bundles its own libamdhip64 with the same soname: load it first so this library and
+    # torch share ONE HIP runtime in the process (device pointers and streams then interoperate)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     P, U32, U64, I32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
     sig = {
@@ -99,6 +106,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_relay_round": (I32, [P, P, P, P]),
         "shd_relay_round_device": (I32, [P, P, P, P]),
         "shd_relay_get_host_state": (I32, [P, P, P]),
+        "shd_relay_set_counters": (I32, [P, I32]),
         "shd_path_packet_counts": (I32, [P, P]),
     }
     for name, (res, args) in sig.items():

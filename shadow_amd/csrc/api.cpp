@@ -1,5 +1,6 @@
 // C ABI entry points (include/shd_accel.h): context lifetime, routing build front ends,
 // resident-table lookups.  The relay entry points live in relay.hip.
+#include <cstdlib>
 #include <new>
 
 #include "ctx.h"
@@ -55,6 +56,10 @@ shd_ctx* shd_open(int device_ordinal, shd_status* st) {
     ctx->device = device_ordinal;
     ctx->n_cu = prop.multiProcessorCount;
     ctx->max_lds = prop.sharedMemPerBlock;
+    {
+        const char* v = std::getenv("SHD_SSSP_STATS");
+        ctx->stats_on = v && *v == '1';
+    }
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return fail(SHD_ERR_HIP);

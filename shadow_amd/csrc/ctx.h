@@ -45,17 +45,23 @@ struct RelayState {
     uint32_t n_hosts = 0;
     uint32_t n_nodes = 0;
     bool own_table = false;   // table copied by shd_relay_setup (else: routing resident table)
-    DevBuf host_node, lat, loss, rng, next_id, counts;
+    bool table_narrow = false;  // every path latency < 2^32 ns -> 16-byte event records (v2)
+    bool force_v1 = false;      // SHD_RELAY_FORCE_V1=1 (testing)
+    bool count_on = true;       // per-path packet counters (RoutingInfo::increment_packet_count)
+    bool last_v2 = false;
+    unsigned long long red_host[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    DevBuf host_node, lat, loss, rng, next_id, rng2, next_id2, counts;
     // per-round scratch
     DevBuf pk_off, pk_time, pk_dst, pk_pay, pk_chance, st, ev_key, ev_key2, ev_val, ev_val2,
-        ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, scan_tmp, red;
+        ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, scan_tmp, red, rec, brec, tmp;
 };
 
 struct PreparedGraph {
     bool ready = false;
     uint32_t mode = 0, V = 0, n_used = 0;
     bool directed = false, narrow_arcs = false;
-    uint64_t arcs = 0, max_arc_lat = 0;
+    uint64_t arcs = 0, max_arc_lat = 0, pruned_arcs = 0;
+    uint32_t mean_arc_lat = 1;
     std::vector<uint32_t> used, node_ids, es, ed;
     std::vector<uint64_t> el;
     std::vector<float> ep;
@@ -88,12 +94,13 @@ struct shd_ctx {
     uint32_t t_rows = 0, t_cols = 0, t_row_begin = 0;
     bool t_full = false;
     shd_routing_info info{};
+    bool stats_on = false;   // SHD_SSSP_STATS=1: count expansions / sweeps (tuning only)
 
     shd::PreparedGraph prep;
     shd::DevBuf d_es, d_ed, d_el, d_ep, d_col;   // direct mode edge arrays
     // routing scratch
     shd::DevBuf g_off, g_dst, g_lat, g_q, g_lat64, g_used, g_diag_lat, g_diag_loss, g_flags,
-        g_dense, g_prune_dst, g_prune_lat, g_prune_q, g_prune_cnt, g_labels, g_aux;
+        g_dense, g_prune_dst, g_prune_cnt, g_labels, g_aux, g_arc16;
 
     shd::RelayState relay;
 };

@@ -19,6 +19,7 @@
 //   K3 relay_scatter   one lane per packet scatters its event into the destination bucket.
 //   K4 segment_sort    one workgroup per destination sorts its bucket by the full event key
 //                      (unique), so the atomic slot order never shows in the output.
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -70,8 +71,10 @@ struct RelayArgs {
     const uint32_t* host_node;
     const uint64_t* lat;
     const float* loss;
-    uint64_t* rng;
-    uint64_t* next_id;
+    const uint64_t* rng;       // host state at round start (read)
+    const uint64_t* next_id;
+    uint64_t* rng_out;         // host state after the round (written; committed on success)
+    uint64_t* next_id_out;
     unsigned long long* counts;  // nullable
     uint64_t round_end, sim_end, bootstrap_end;
     uint8_t* status;
@@ -123,11 +126,11 @@ __global__ __launch_bounds__(256) void relay_stamp(RelayArgs a) {
             }
             a.status[i] = st;
         }
-        a.rng[4 * (size_t)h] = r.s0;
-        a.rng[4 * (size_t)h + 1] = r.s1;
-        a.rng[4 * (size_t)h + 2] = r.s2;
-        a.rng[4 * (size_t)h + 3] = r.s3;
-        a.next_id[h] = id;
+        a.rng_out[4 * (size_t)h] = r.s0;
+        a.rng_out[4 * (size_t)h + 1] = r.s1;
+        a.rng_out[4 * (size_t)h + 2] = r.s2;
+        a.rng_out[4 * (size_t)h + 3] = r.s3;
+        a.next_id_out[h] = id;
     }
     my_min_d = wave_min_u64(my_min_d);
     my_min_l = wave_min_u64(my_min_l);
@@ -276,6 +279,298 @@ __global__ __launch_bounds__(256) void segment_sort_big(
     }
 }
 
+// ==========================================================================================
+// Relay v2 (every path latency < 2^32 ns and every deliver - round_end < 2^32): 16-byte event
+// records {deliver - round_end, src host, seq - seq_base[src], packet index}.
+//
+// K1 relay_stamp_v2: a workgroup owns BLOCK consecutive source hosts, i.e. one contiguous range
+// of the source-grouped batch, and walks it in chunks of C packets staged through LDS:
+//   (a) coalesced loads of the chunk's send times / destinations / payloads (/ chances);
+//   (b) each host marks its packets in the chunk (owner map in LDS);
+//   (c) lane-per-packet gather of the path entry (host_node[dst], lat, loss);
+//   (d) lane-per-host sequential pass: RNG draw, drop rule, deliver stamp, event id -- the only
+//       part that must follow each host's send order;
+//   (e) lane-per-packet: claim a destination-bucket slot, coalesced stores of status/record/slot.
+// ==========================================================================================
+constexpr uint32_t kStampHosts = 256;
+constexpr uint32_t kStampChunk = 1024;
+
+struct RelayArgs2 {
+    uint32_t n_hosts, n_nodes;
+    const uint32_t* src_off;
+    const uint64_t* send_time;
+    const uint32_t* dst_host;
+    const uint32_t* payload;
+    const double* chance;
+    const uint32_t* host_node;
+    const uint64_t* lat;
+    const float* loss;
+    const uint64_t* rng;
+    const uint64_t* next_id;
+    uint64_t* rng_out;
+    uint64_t* next_id_out;
+    unsigned long long* counts;
+    uint64_t round_end, sim_end, bootstrap_end;
+    uint8_t* status;
+    uint4* rec;          // per packet (valid when SENT)
+    uint32_t* slot;      // per packet
+    uint32_t* dst_cnt;
+    unsigned long long* red;   // [0] min deliver [1] min latency [2] n_sent [3] bad dst [4] wide
+};
+
+__global__ __launch_bounds__(kStampHosts) void relay_stamp_v2(RelayArgs2 a) {
+    constexpr uint32_t B = kStampHosts, C = kStampChunk;
+    __shared__ uint32_t s_off[B + 1];
+    __shared__ uint64_t t_time[C];
+    __shared__ uint32_t t_dst[C];
+    __shared__ uint32_t t_pay[C];
+    __shared__ uint32_t t_lat[C];
+    __shared__ float t_loss[C];
+    __shared__ uint32_t t_aux[C];    // owner lane, then the event record's deliver offset
+    __shared__ uint32_t t_seq[C];    // seq offset (SENT) | status in the top byte
+    const uint32_t tid = threadIdx.x;
+    const uint32_t h0 = blockIdx.x * B;
+    const uint32_t nh = min(B, a.n_hosts - h0);
+    for (uint32_t i = tid; i <= nh; i += B) s_off[i] = a.src_off[h0 + i];
+    __syncthreads();
+    const bool mine = tid < nh;
+    const uint32_t h = h0 + tid;
+    uint32_t my_b = 0, my_e = 0;
+    Xoshiro r{0, 0, 0, 0};
+    uint64_t id0 = 0;
+    uint32_t nsent = 0;
+    if (mine) {
+        my_b = s_off[tid];
+        my_e = s_off[tid + 1];
+        r = Xoshiro{a.rng[4 * (size_t)h], a.rng[4 * (size_t)h + 1], a.rng[4 * (size_t)h + 2],
+                    a.rng[4 * (size_t)h + 3]};
+        id0 = a.next_id[h];
+    }
+    uint64_t min_d = ~0ull, min_l = ~0ull;
+    bool wide = false;
+    const uint32_t P0 = s_off[0], P1 = s_off[nh];
+    for (uint32_t c0 = P0; c0 < P1; c0 += C) {
+        const uint32_t cn = min(C, P1 - c0);
+        for (uint32_t j = tid; j < cn; j += B) {   // (a)
+            t_time[j] = a.send_time[c0 + j];
+            t_dst[j] = a.dst_host[c0 + j];
+            t_pay[j] = a.payload[c0 + j];
+        }
+        if (mine)                                    // (b)
+            for (uint32_t i = max(my_b, c0); i < min(my_e, c0 + cn); ++i) t_aux[i - c0] = tid;
+        __syncthreads();
+        for (uint32_t j = tid; j < cn; j += B) {   // (c)
+            const uint32_t d = t_dst[j];
+            if (d >= a.n_hosts) {
+                atomicMin(&a.red[3], (unsigned long long)(c0 + j));
+                t_lat[j] = 0;
+                t_loss[j] = 0.0f;
+                continue;
+            }
+            const size_t pi = (size_t)a.host_node[h0 + t_aux[j]] * a.n_nodes + a.host_node[d];
+            const uint64_t l = a.lat[pi];
+            if (l >> 32) wide = true;
+            t_lat[j] = (uint32_t)l;
+            t_loss[j] = a.loss[pi];
+        }
+        __syncthreads();
+        if (mine) {                                  // (d) sequential per source host
+            for (uint32_t i = max(my_b, c0); i < min(my_e, c0 + cn); ++i) {
+                const uint32_t j = i - c0;
+                const uint64_t now = t_time[j];
+                uint32_t st = kStSkipped, off = 0;
+                if (now < a.sim_end && t_dst[j] < a.n_hosts) {
+                    const double reliability = (double)one_minus(t_loss[j]);
+                    const double ch = a.chance ? a.chance[i] : r.gen_f64();
+                    if (!(now < a.bootstrap_end) && ch >= reliability && t_pay[j] > 0) {
+                        st = kStDropped;
+                    } else {
+                        const uint64_t lat = t_lat[j];
+                        uint64_t t = now + lat;
+                        if (t < a.round_end) t = a.round_end;
+                        const uint64_t dd = t - a.round_end;
+                        if (dd >> 32) wide = true;
+                        off = (uint32_t)dd;
+                        min_d = t < min_d ? t : min_d;
+                        min_l = lat < min_l ? lat : min_l;
+                        st = kStSent;
+                        t_seq[j] = nsent++;
+                    }
+                }
+                t_aux[j] = off;
+                t_pay[j] = st;   // payload no longer needed: reuse as status
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = tid; j < cn; j += B) {   // (e)
+            const uint32_t st = t_pay[j];
+            a.status[c0 + j] = (uint8_t)st;
+            if (st == kStSent) {
+                const uint32_t d = t_dst[j];
+                a.slot[c0 + j] = atomicAdd(&a.dst_cnt[d], 1u);
+                // owner recomputed from the chunk range: binary search in s_off
+                uint32_t lo = 0, hi = nh;
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_off[mid] <= c0 + j) lo = mid; else hi = mid;
+                }
+                a.rec[c0 + j] = make_uint4(t_aux[j], h0 + lo, t_seq[j], c0 + j);
+                if (a.counts)
+                    atomicAdd(&a.counts[(size_t)a.host_node[h0 + lo] * a.n_nodes + a.host_node[d]], 1ull);
+            }
+        }
+        __syncthreads();
+    }
+    if (mine) {
+        a.rng_out[4 * (size_t)h] = r.s0;
+        a.rng_out[4 * (size_t)h + 1] = r.s1;
+        a.rng_out[4 * (size_t)h + 2] = r.s2;
+        a.rng_out[4 * (size_t)h + 3] = r.s3;
+        a.next_id_out[h] = id0 + nsent;
+    }
+    min_d = wave_min_u64(min_d);
+    min_l = wave_min_u64(min_l);
+    uint64_t ns = nsent;
+    for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
+    const bool any_wide = __ballot(wide) != 0;
+    if ((tid & 63) == 0) {
+        if (min_d != ~0ull) atomicMin(&a.red[0], (unsigned long long)min_d);
+        if (min_l != ~0ull) atomicMin(&a.red[1], (unsigned long long)min_l);
+        if (ns) atomicAdd(&a.red[2], (unsigned long long)ns);
+        if (any_wide) atomicOr(&a.red[4], 1ull);
+    }
+}
+
+__global__ __launch_bounds__(256) void relay_scatter_v2(
+    uint64_t n, const uint8_t* __restrict__ status, const uint32_t* __restrict__ dst_host,
+    const uint32_t* __restrict__ slot, const uint4* __restrict__ rec,
+    const uint32_t* __restrict__ ev_off, uint4* __restrict__ brec) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n || status[i] != kStSent) return;
+    brec[ev_off[dst_host[i]] + slot[i]] = rec[i];
+}
+
+__device__ __forceinline__ bool rec_less(const uint4& a, const uint4& b) {
+    if (a.x != b.x) return a.x < b.x;     // deliver offset
+    if (a.y != b.y) return a.y < b.y;     // src host
+    return a.z < b.z;                     // event id offset
+}
+
+// One wave per destination bucket (<= kWaveSeg events): bitonic network in the wave's LDS
+// slice, wave-synchronous (no workgroup barrier); then SoA output in EventQueue pop order.
+constexpr uint32_t kWaveSeg = 256;
+
+__global__ __launch_bounds__(256) void segment_sort_v2(
+    uint32_t n_hosts, const uint32_t* __restrict__ ev_off, const uint4* __restrict__ brec,
+    uint64_t round_end, const uint64_t* __restrict__ seq_base, uint64_t* __restrict__ ev_deliver,
+    uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq, uint32_t* __restrict__ ev_pkt,
+    uint32_t* __restrict__ big) {
+    __shared__ uint4 s[4][kWaveSeg];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t d = blockIdx.x * 4 + w;
+    if (d >= n_hosts) return;
+    const uint32_t b = ev_off[d], n = ev_off[d + 1] - b;
+    if (n == 0) return;
+    if (n > kWaveSeg) {
+        if (lane == 0) big[atomicAdd(&big[0], 1u) + 1] = d;
+        return;
+    }
+    uint4* x = s[w];
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+    for (uint32_t i = lane; i < P; i += 64)
+        x[i] = i < n ? brec[b + i] : make_uint4(~0u, ~0u, ~0u, ~0u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = lane; i < P; i += 64) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint4 p = x[i], q = x[l];
+                    if (rec_less(q, p) == ((i & k) == 0)) {
+                        x[i] = q;
+                        x[l] = p;
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+    for (uint32_t i = lane; i < n; i += 64) {
+        const uint4 e = x[i];
+        ev_deliver[b + i] = round_end + e.x;
+        ev_src[b + i] = e.y;
+        ev_seq[b + i] = seq_base[e.y] + e.z;
+        ev_pkt[b + i] = e.w;
+    }
+}
+
+// Buckets larger than one wave's LDS slice: bottom-up merge passes by one workgroup in a
+// global scratch copy of the bucket (rank by binary search in the sibling run; keys unique).
+__global__ __launch_bounds__(256) void segment_sort_v2_big(
+    const uint32_t* __restrict__ big, const uint32_t* __restrict__ ev_off, uint4* __restrict__ brec,
+    uint4* __restrict__ tmp, uint64_t round_end, const uint64_t* __restrict__ seq_base,
+    uint64_t* __restrict__ ev_deliver, uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq,
+    uint32_t* __restrict__ ev_pkt) {
+    for (uint32_t bi = blockIdx.x; bi < big[0]; bi += gridDim.x) {
+        const uint32_t d = big[1 + bi];
+        const uint32_t b = ev_off[d], n = ev_off[d + 1] - b;
+        uint4* A = brec + b;
+        uint4* T = tmp + b;
+        for (uint32_t w = 1; w < n; w <<= 1) {
+            for (uint32_t o = threadIdx.x; o < n; o += 256) {
+                const uint32_t lo = (o / (2 * w)) * 2 * w;
+                const uint32_t mid = min(lo + w, n), hi = min(lo + 2 * w, n);
+                const uint4 xv = A[o];
+                uint32_t rank;
+                if (o < mid) {
+                    uint32_t l = mid, h = hi;
+                    while (l < h) {
+                        const uint32_t m = (l + h) >> 1;
+                        if (rec_less(A[m], xv)) l = m + 1; else h = m;
+                    }
+                    rank = (o - lo) + (l - mid);
+                } else {
+                    uint32_t l = lo, h = mid;
+                    while (l < h) {
+                        const uint32_t m = (l + h) >> 1;
+                        if (rec_less(xv, A[m])) h = m; else l = m + 1;
+                    }
+                    rank = (o - mid) + (l - lo);
+                }
+                T[lo + rank] = xv;
+            }
+            __syncthreads();
+            for (uint32_t o = threadIdx.x; o < n; o += 256) A[o] = T[o];
+            __syncthreads();
+        }
+        for (uint32_t i = threadIdx.x; i < n; i += 256) {
+            const uint4 e = A[i];
+            ev_deliver[b + i] = round_end + e.x;
+            ev_src[b + i] = e.y;
+            ev_seq[b + i] = seq_base[e.y] + e.z;
+            ev_pkt[b + i] = e.w;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void max_u64_kernel(const uint64_t* __restrict__ d, uint64_t n,
+                               unsigned long long* __restrict__ out) {
+    uint64_t m = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        m = d[i] > m ? d[i] : m;
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t w = __shfl_xor(m, o);
+        m = w > m ? w : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)m);
+}
+
 __global__ void min_u64_kernel(const uint64_t* __restrict__ d, uint64_t n,
                                unsigned long long* __restrict__ out) {
     uint64_t m = ~0ull;
@@ -299,19 +594,17 @@ shd_status min_u64_device(shd_ctx* ctx, const uint64_t* d, uint64_t n, uint64_t*
 // ------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------
-static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
-                               shd_relay_out* o, bool sync_scalars) {
+// v1 pipeline: u64 deliver times (used when a path latency or deliver offset needs > 32 bits)
+static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                                  shd_relay_out* o) {
     RelayState& R = ctx->relay;
     hipStream_t s = ctx->stream;
     const uint64_t n = b->n_packets;
     const uint32_t H = R.n_hosts;
-    SHD_TRY(R.red.ensure(64));
-    SHD_TRY(R.dst_cnt.ensure((size_t)(H + 1) * 4));
     SHD_TRY(R.ev_key.ensure(std::max<uint64_t>(n, 1) * 8));   // deliver per packet
     SHD_TRY(R.ev_key2.ensure(std::max<uint64_t>(n, 1) * 8));  // seq per packet
     SHD_TRY(R.ev_val.ensure(std::max<uint64_t>(n, 1) * 4));   // slot per packet
-    SHD_TRY(R.scan_tmp.ensure(64));
-    unsigned long long init[4] = {~0ull, ~0ull, 0ull, ~0ull};
+    unsigned long long init[8] = {~0ull, ~0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
     SHD_HIP(hipMemcpyAsync(R.red.p, init, sizeof(init), hipMemcpyHostToDevice, s));
     SHD_HIP(hipMemsetAsync(R.dst_cnt.p, 0, (size_t)(H + 1) * 4, s));
     RelayArgs a{};
@@ -327,7 +620,9 @@ static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round
     a.loss = R.own_table ? R.loss.as<float>() : ctx->t_loss.as<float>();
     a.rng = R.rng.as<uint64_t>();
     a.next_id = R.next_id.as<uint64_t>();
-    a.counts = R.counts.as<unsigned long long>();
+    a.rng_out = R.rng2.as<uint64_t>();
+    a.next_id_out = R.next_id2.as<uint64_t>();
+    a.counts = R.count_on ? R.counts.as<unsigned long long>() : nullptr;
     a.round_end = rd->round_end;
     a.sim_end = rd->sim_end;
     a.bootstrap_end = rd->bootstrap_end;
@@ -339,7 +634,6 @@ static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round
     a.red = R.red.as<unsigned long long>();
     relay_stamp<<<div_up(H, 256), 256, 0, s>>>(a);
     SHD_HIP(hipGetLastError());
-    // exclusive scan of H+1 counts (last is 0) -> ev_off[0..H]
     size_t tmp_bytes = 0;
     SHD_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off, 0u,
                                     (size_t)H + 1, rocprim::plus<uint32_t>(), s));
@@ -358,22 +652,105 @@ static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round
     SHD_HIP(hipGetLastError());
     uint32_t n_big = 0;
     SHD_HIP(hipMemcpyAsync(&n_big, R.ev_val2.p, 4, hipMemcpyDeviceToHost, s));
-    unsigned long long red[4];
-    SHD_HIP(hipMemcpyAsync(red, R.red.p, sizeof(red), hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipMemcpyAsync(R.red_host, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     if (n_big) {
-        SHD_TRY(R.scan_tmp.ensure(std::max<uint64_t>(n, 1) * sizeof(EvKey)));
+        SHD_TRY(R.tmp.ensure(std::max<uint64_t>(n, 1) * sizeof(EvKey)));
         segment_sort_big<<<n_big, 256, 0, s>>>(R.ev_val2.as<uint32_t>(), o->ev_off, o->ev_deliver,
-                                               o->ev_src, o->ev_seq, o->ev_pkt,
-                                               R.scan_tmp.as<EvKey>());
+                                               o->ev_src, o->ev_seq, o->ev_pkt, R.tmp.as<EvKey>());
         SHD_HIP(hipGetLastError());
         SHD_HIP(hipStreamSynchronize(s));
     }
-    (void)sync_scalars;
-    if (red[3] != ~0ull) return SHD_ERR_NO_HOST;
-    o->min_deliver = red[0];
-    o->min_latency = red[1];
-    o->n_sent = red[2];
+    return SHD_OK;
+}
+
+// v2 pipeline: 16-byte records, chunked stamp, wave-per-destination sort; one host sync.
+static shd_status relay_device_v2(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                                  shd_relay_out* o) {
+    RelayState& R = ctx->relay;
+    hipStream_t s = ctx->stream;
+    const uint64_t n = b->n_packets;
+    const uint32_t H = R.n_hosts;
+    const size_t nn = std::max<uint64_t>(n, 1);
+    SHD_TRY(R.rec.ensure(nn * 16));
+    SHD_TRY(R.brec.ensure(nn * 16));
+    SHD_TRY(R.tmp.ensure(nn * 16));
+    SHD_TRY(R.ev_val.ensure(nn * 4));
+    SHD_TRY(R.ev_val2.ensure((size_t)(H + 2) * 4));
+    unsigned long long init[8] = {~0ull, ~0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
+    SHD_HIP(hipMemcpyAsync(R.red.p, init, sizeof(init), hipMemcpyHostToDevice, s));
+    SHD_HIP(hipMemsetAsync(R.dst_cnt.p, 0, (size_t)(H + 1) * 4, s));
+    SHD_HIP(hipMemsetAsync(R.ev_val2.p, 0, 4, s));
+    RelayArgs2 a{};
+    a.n_hosts = H;
+    a.n_nodes = R.n_nodes;
+    a.src_off = b->src_off;
+    a.send_time = b->send_time;
+    a.dst_host = b->dst_host;
+    a.payload = b->payload;
+    a.chance = b->chance;
+    a.host_node = R.host_node.as<uint32_t>();
+    a.lat = R.own_table ? R.lat.as<uint64_t>() : ctx->t_lat.as<uint64_t>();
+    a.loss = R.own_table ? R.loss.as<float>() : ctx->t_loss.as<float>();
+    a.rng = R.rng.as<uint64_t>();
+    a.next_id = R.next_id.as<uint64_t>();
+    a.rng_out = R.rng2.as<uint64_t>();
+    a.next_id_out = R.next_id2.as<uint64_t>();
+    a.counts = R.count_on ? R.counts.as<unsigned long long>() : nullptr;
+    a.round_end = rd->round_end;
+    a.sim_end = rd->sim_end;
+    a.bootstrap_end = rd->bootstrap_end;
+    a.status = o->status;
+    a.rec = R.rec.as<uint4>();
+    a.slot = R.ev_val.as<uint32_t>();
+    a.dst_cnt = R.dst_cnt.as<uint32_t>();
+    a.red = R.red.as<unsigned long long>();
+    relay_stamp_v2<<<div_up(H, kStampHosts), kStampHosts, 0, s>>>(a);
+    SHD_HIP(hipGetLastError());
+    size_t tmp_bytes = 0;
+    SHD_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off, 0u,
+                                    (size_t)H + 1, rocprim::plus<uint32_t>(), s));
+    SHD_TRY(R.scan_tmp.ensure(tmp_bytes));
+    SHD_HIP(rocprim::exclusive_scan(R.scan_tmp.p, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off,
+                                    0u, (size_t)H + 1, rocprim::plus<uint32_t>(), s));
+    if (n)
+        relay_scatter_v2<<<div_up(n, 256), 256, 0, s>>>(n, o->status, b->dst_host,
+                                                        R.ev_val.as<uint32_t>(), R.rec.as<uint4>(),
+                                                        o->ev_off, R.brec.as<uint4>());
+    segment_sort_v2<<<div_up(H, 4), 256, 0, s>>>(H, o->ev_off, R.brec.as<uint4>(), rd->round_end,
+                                                 R.next_id.as<uint64_t>(), o->ev_deliver, o->ev_src,
+                                                 o->ev_seq, o->ev_pkt, R.ev_val2.as<uint32_t>());
+    segment_sort_v2_big<<<64, 256, 0, s>>>(R.ev_val2.as<uint32_t>(), o->ev_off, R.brec.as<uint4>(),
+                                           R.tmp.as<uint4>(), rd->round_end, R.next_id.as<uint64_t>(),
+                                           o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt);
+    SHD_HIP(hipGetLastError());
+    SHD_HIP(hipMemcpyAsync(R.red_host, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    return SHD_OK;
+}
+
+// One round: the new host state (RNG streams, event ids) is written to the second buffer and
+// committed only when the round succeeds, so a failed round leaves the hosts untouched.
+static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                               shd_relay_out* o) {
+    RelayState& R = ctx->relay;
+    const uint32_t H = R.n_hosts;
+    SHD_TRY(R.red.ensure(64));
+    SHD_TRY(R.dst_cnt.ensure((size_t)(H + 1) * 4));
+    SHD_TRY(R.scan_tmp.ensure(64));
+    bool v2 = R.table_narrow && !R.force_v1;
+    if (v2) {
+        SHD_TRY(relay_device_v2(ctx, b, rd, o));
+        if (R.red_host[4]) v2 = false;   // a deliver offset needs 64 bits: redo with v1
+    }
+    if (!v2) SHD_TRY(relay_device_v1(ctx, b, rd, o));
+    if (R.red_host[3] != ~0ull) return SHD_ERR_NO_HOST;
+    std::swap(R.rng, R.rng2);
+    std::swap(R.next_id, R.next_id2);
+    o->min_deliver = R.red_host[0];
+    o->min_latency = R.red_host[1];
+    o->n_sent = R.red_host[2];
+    R.last_v2 = v2;
     return SHD_OK;
 }
 
@@ -408,6 +785,8 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
     SHD_TRY(R.host_node.ensure((size_t)n_hosts * 4));
     SHD_TRY(R.rng.ensure((size_t)n_hosts * 32));
     SHD_TRY(R.next_id.ensure((size_t)n_hosts * 8));
+    SHD_TRY(R.rng2.ensure((size_t)n_hosts * 32));
+    SHD_TRY(R.next_id2.ensure((size_t)n_hosts * 8));
     SHD_TRY(R.counts.ensure((size_t)n_nodes * n_nodes * 8));
     SHD_HIP(hipMemcpyAsync(R.host_node.p, host_node, (size_t)n_hosts * 4, hipMemcpyHostToDevice, s));
     SHD_HIP(hipMemcpyAsync(R.rng.p, rng_state, (size_t)n_hosts * 32, hipMemcpyHostToDevice, s));
@@ -416,6 +795,22 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
     SHD_HIP(hipStreamSynchronize(s));
     R.n_hosts = n_hosts;
     R.n_nodes = n_nodes;
+    {   // v2 needs every path latency < 2^32 ns (max over the table)
+        const uint64_t* tl = R.own_table ? R.lat.as<uint64_t>() : ctx->t_lat.as<uint64_t>();
+        SHD_TRY(ctx->g_aux.ensure(8));
+        SHD_HIP(hipMemsetAsync(ctx->g_aux.p, 0, 8, s));
+        const uint64_t nn = (uint64_t)n_nodes * n_nodes;
+        max_u64_kernel<<<(uint32_t)std::min<uint64_t>(2048, (nn + 255) / 256), 256, 0, s>>>(
+            tl, nn, reinterpret_cast<unsigned long long*>(ctx->g_aux.p));
+        uint64_t mx = 0;
+        SHD_HIP(hipMemcpyAsync(&mx, ctx->g_aux.p, 8, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipStreamSynchronize(s));
+        R.table_narrow = (mx >> 32) == 0;
+    }
+    {
+        const char* v = std::getenv("SHD_RELAY_FORCE_V1");
+        R.force_v1 = v && *v == '1';
+    }
     R.ready = true;
     return SHD_OK;
 }
@@ -431,7 +826,7 @@ shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const 
         !d_out->ev_seq || !d_out->ev_pkt)
         return SHD_ERR_INVALID;
     SHD_HIP(hipSetDevice(ctx->device));
-    return relay_device(ctx, d_batch, round, d_out, true);
+    return relay_device(ctx, d_batch, round, d_out);
 }
 
 shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round* round,
@@ -478,7 +873,7 @@ shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round
     dout.ev_src = R.ev_src.as<uint32_t>();
     dout.ev_seq = R.ev_seq.as<uint64_t>();
     dout.ev_pkt = R.ev_pkt.as<uint32_t>();
-    SHD_TRY(relay_device(ctx, &db, round, &dout, true));
+    SHD_TRY(relay_device(ctx, &db, round, &dout));
     const uint64_t ns = dout.n_sent;
     if (out->status && n) SHD_HIP(hipMemcpyAsync(out->status, dout.status, n, hipMemcpyDeviceToHost, s));
     if (out->ev_off) SHD_HIP(hipMemcpyAsync(out->ev_off, dout.ev_off, (size_t)(H + 1) * 4, hipMemcpyDeviceToHost, s));
@@ -505,6 +900,12 @@ shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t*
     if (next_event_id)
         SHD_HIP(hipMemcpyAsync(next_event_id, R.next_id.p, (size_t)R.n_hosts * 8, hipMemcpyDeviceToHost, ctx->stream));
     SHD_HIP(hipStreamSynchronize(ctx->stream));
+    return SHD_OK;
+}
+
+shd_status shd_relay_set_counters(shd_ctx* ctx, int32_t enabled) {
+    if (!ctx) return SHD_ERR_INVALID;
+    ctx->relay.count_on = enabled != 0;
     return SHD_OK;
 }
 

@@ -12,6 +12,7 @@
 //   diagonal := the node's single self-loop edge, raw loss (:212-219); unreachable -> panic
 //     (:221); get_direct_paths :232-254 with get_edge_weight :258-295.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -23,81 +24,133 @@ namespace shd {
 // Kernel 1: batched per-source SSSP, one workgroup per source row, labels in LDS.
 // Label = packed u64 key (lat32 << 32 | f32 loss bits); ds_min_rtn_u64 keeps the lexicographic
 // minimum exactly.  Active set = LDS bitmap; sweeps until a sweep improves nothing.
+// Arcs are 16-byte AoS records {dst, lat32,
+// q = 1f32 - loss bits, 0} so one dwordx4 load fetches an arc; a group of G lanes relaxes one
+// active node's arcs together (G ~ average degree), so a node costs one load latency instead
+// of `degree` dependent ones.  64/G nodes are in flight per wave, NW waves per source.
 // ------------------------------------------------------------------------------------------
-constexpr int kSsspBlock = 256;
-
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void sssp_lds_narrow(
-    const uint32_t* __restrict__ off, const uint32_t* __restrict__ adst,
-    const uint32_t* __restrict__ alat, const float* __restrict__ aq, uint32_t V,
-    const uint32_t* __restrict__ used, uint32_t n_used, uint32_t row_begin,
-    const uint64_t* __restrict__ diag_lat, const float* __restrict__ diag_loss,
-    uint64_t* __restrict__ out_lat, float* __restrict__ out_loss, uint32_t* __restrict__ flags,
-    unsigned long long* __restrict__ unreach) {
+// delta = bucket width in ns for delta-stepping (SHD_ALGO_DELTA): a sweep only expands active
+// nodes whose latency is <= (min active latency + delta), which keeps the expansion order close
+// to Dijkstra's and cuts re-expansions.  delta = 0xFFFFFFFF expands every active node (plain
+// chaotic Bellman-Ford).  Both converge to the same unique fixed point.
+template <int BLOCK, int G>
+__global__ __launch_bounds__(BLOCK) void sssp_lds_group(
+    const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
+    const uint4* __restrict__ arcs, uint32_t V, const uint32_t* __restrict__ used,
+    uint32_t n_used, uint32_t row_begin, const uint64_t* __restrict__ diag_lat,
+    const float* __restrict__ diag_loss, uint64_t* __restrict__ out_lat,
+    float* __restrict__ out_loss, uint32_t* __restrict__ flags,
+    unsigned long long* __restrict__ unreach, uint32_t delta,
+    unsigned long long* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
     uint64_t* lab = reinterpret_cast<uint64_t*>(smem);
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V);
-    uint32_t* ctl = bits + W;  // [0] dirty
+    uint32_t* ctl = bits + W;            // [0] dirty  [1] min active latency
+    uint32_t* wq = ctl + 4;              // per-wave queue of up to 32 node ids
+    // [V] arc range {beg, end}, 8-byte aligned after the queues
+    const uint32_t rng_off = (((uint32_t)((wq + NW * 32) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
+    uint2* rng = reinterpret_cast<uint2*>(smem + rng_off);
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    constexpr uint32_t NW = BLOCK / 64;
+    const uint32_t grp = lane / G, gl = lane % G;
+    uint32_t* q = wq + wave * 32;
     const uint32_t row = row_begin + blockIdx.x;
     const uint32_t src = used[row];
+    const bool use_delta = delta != kLat32Inf;
 
-    for (uint32_t v = tid; v < V; v += BLOCK) lab[v] = kKeyInf;
+    for (uint32_t v = tid; v < V; v += BLOCK) {
+        lab[v] = kKeyInf;
+        rng[v] = make_uint2(abeg[v], aend[v]);
+    }
     for (uint32_t w = tid; w < W; w += BLOCK) bits[w] = 0;
     __syncthreads();
     if (tid == 0) {
-        lab[src] = 0;  // PathProperties::default() = (0 ns, 0.0)
+        lab[src] = 0;
         bits[src >> 5] = 1u << (src & 31);
     }
     bool ovf = false;
+    uint32_t expanded = 0, sweeps = 0;
     for (;;) {
-        if (tid == 0) ctl[0] = 0;
+        if (tid == 0) {
+            ctl[0] = 0;
+            ctl[1] = kLat32Inf;
+        }
         __syncthreads();
+        uint32_t thr = kLat32Inf;
+        if (use_delta) {
+            uint32_t m = kLat32Inf;
+            for (uint32_t widx = wave; widx < W; widx += NW) {
+                const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (word == 0) continue;
+                if (lane < 32 && ((word >> lane) & 1u)) m = min(m, key_lat(lab[widx * 32 + lane]));
+            }
+            for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+            if (lane == 0 && m != kLat32Inf) atomicMin(&ctl[1], m);
+            __syncthreads();
+            const uint32_t lo = ctl[1];
+            if (lo == kLat32Inf) break;  // no active node anywhere
+            thr = lo + delta < lo ? kLat32Inf - 1 : lo + delta;
+        }
         bool dirty = false;
-        // each wave takes word pairs (lane l <-> node 32*word + (l & 31))
-        for (uint32_t base = 2 * wave; base < W; base += 2 * NW) {
-            const uint32_t widx = base + (lane >> 5);
-            uint32_t peek = widx < W ? __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP)
-                                     : 0u;
-            if (__ballot(peek != 0) == 0) continue;  // wave-uniform skip of empty pairs
-            uint32_t word = 0;
-            if ((lane & 31) == 0 && peek) word = atomicExch(&bits[widx], 0u);
-            word = __shfl(word, lane & 32);
-            if ((word >> (lane & 31)) & 1u) {
-                const uint32_t u = widx * 32 + (lane & 31);
-                const uint64_t ku = __hip_atomic_load(&lab[u], __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-                const uint32_t lu = key_lat(ku);
-                const float qu = one_minus(key_loss(ku));
-                const uint32_t k1 = off[u + 1];
-                for (uint32_t k = off[u]; k < k1; ++k) {
-                    const uint32_t v = adst[k];
-                    const uint32_t cl = lu + alat[k];
-                    if (cl < lu || cl == kLat32Inf) {  // path latency leaves u32: wide rerun
-                        ovf = true;
-                        continue;
-                    }
-                    const uint64_t cand = pack_key(cl, fold_q(qu, aq[k]));
-                    const uint64_t old = atomicMin(reinterpret_cast<unsigned long long*>(&lab[v]),
-                                                   (unsigned long long)cand);
-                    if (cand < old) {
-                        atomicOr(&bits[v >> 5], 1u << (v & 31));
-                        dirty = true;
+        for (uint32_t widx = wave; widx < W; widx += NW) {
+            const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (word == 0) continue;  // wave-uniform
+            bool sel = lane < 32 && ((word >> lane) & 1u);
+            if (use_delta && sel) sel = key_lat(lab[widx * 32 + lane]) <= thr;
+            const uint32_t mask = (uint32_t)__ballot(sel);
+            if (mask == 0) continue;
+            // words are owned by one wave; other waves only set bits, so clearing `mask` is exact
+            if (lane == 0) atomicAnd(&bits[widx], ~mask);
+            const uint32_t n = __popc(mask);
+            if (sel) q[__popc(mask & ((1u << lane) - 1u))] = widx * 32 + lane;
+            expanded += n;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t t = 0; t < n; t += NG) {
+                const uint32_t qi = t + grp;
+                if (qi < n) {
+                    const uint32_t u = q[qi];
+                    const uint64_t ku = __hip_atomic_load(&lab[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const uint32_t lu = key_lat(ku);
+                    const float qu = one_minus(key_loss(ku));
+                    const uint2 r = rng[u];
+                    for (uint32_t k = r.x + gl; k < r.y; k += G) {
+                        const uint4 a = arcs[k];
+                        const uint32_t cl = lu + a.y;
+                        if (cl < lu || cl == kLat32Inf) {
+                            ovf = true;
+                            continue;
+                        }
+                        const uint64_t cand = pack_key(cl, fold_q(qu, __uint_as_float(a.z)));
+                        const uint64_t old = atomicMin(reinterpret_cast<unsigned long long*>(&lab[a.x]),
+                                                       (unsigned long long)cand);
+                        if (cand < old) {
+                            atomicOr(&bits[a.x >> 5], 1u << (a.x & 31));
+                            dirty = true;
+                        }
                     }
                 }
             }
+            __builtin_amdgcn_wave_barrier();
         }
-        if (dirty) ctl[0] = 1;
-        __syncthreads();
-        const bool again = ctl[0] != 0;
-        __syncthreads();
-        if (!again) break;
+        ++sweeps;
+        if (!use_delta) {
+            if (dirty) ctl[0] = 1;
+            __syncthreads();
+            const bool again = ctl[0] != 0;
+            __syncthreads();
+            if (!again) break;
+        } else {
+            __syncthreads();
+        }
     }
     if (ovf) atomicOr(&flags[0], 1u);
-    // write the row in `used` order; diagonal = self-loop edge
+    if (stats && lane == 0) {
+        atomicAdd(&stats[0], (unsigned long long)expanded);
+        if (wave == 0) atomicAdd(&stats[1], (unsigned long long)sweeps);
+    }
     const size_t orow = (size_t)blockIdx.x * n_used;
     for (uint32_t j = tid; j < n_used; j += BLOCK) {
         uint64_t l;
@@ -118,6 +171,113 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_narrow(
         }
         out_lat[orow + j] = l;
         out_loss[orow + j] = p;
+    }
+}
+
+__global__ __launch_bounds__(256) void arcs_pack(const uint32_t* __restrict__ dst,
+                                                 const uint32_t* __restrict__ lat,
+                                                 const float* __restrict__ loss,
+                                                 uint4* __restrict__ out, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = make_uint4(dst[i], lat[i], __float_as_uint(one_minus(loss[i])), 0u);
+}
+
+// ------------------------------------------------------------------------------------------
+// Dense-graph arc pruning (SHD_ALGO_PRUNED).  An arc (u,v) lies on no shortest-latency path if
+// some 2-hop detour u->x->v is STRICTLY shorter; such arcs cannot change any lexicographic
+// label (the latency part is decided first and every tight path avoids them), so the SSSP
+// below runs on the surviving arcs only and still reproduces the reference's bits.  x ranges
+// over the K lowest-latency neighbours of u (any subset is sound; the nearest catch almost
+// all: C2 keeps ~49 of 999 arcs per node with K = 32).  Ties (detour == arc) are kept.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dense_init(uint64_t* __restrict__ Wk, uint64_t nn) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nn) Wk[i] = kKeyInf;
+}
+
+// one workgroup per row u: lexicographic min over parallel arcs into the dense key matrix
+__global__ __launch_bounds__(256) void dense_scatter(const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ adst,
+                                                     const uint32_t* __restrict__ alat,
+                                                     const float* __restrict__ aloss, uint32_t V,
+                                                     uint64_t* __restrict__ Wk) {
+    const uint32_t u = blockIdx.x;
+    for (uint32_t k = off[u] + threadIdx.x; k < off[u + 1]; k += 256)
+        atomicMin(reinterpret_cast<unsigned long long*>(&Wk[(size_t)u * V + adst[k]]),
+                  (unsigned long long)pack_key(alat[k], aloss[k]));
+}
+
+__global__ __launch_bounds__(256) void dense_lat(const uint64_t* __restrict__ Wk,
+                                                 uint32_t* __restrict__ Wl, uint64_t nn) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nn) Wl[i] = key_lat(Wk[i]);
+}
+
+template <int BLOCK, int K>
+__global__ __launch_bounds__(BLOCK) void prune_rows(
+    const uint32_t* __restrict__ Wl, const uint64_t* __restrict__ Wk, uint32_t V, uint32_t P,
+    uint32_t* __restrict__ pbeg, uint32_t* __restrict__ pend, uint4* __restrict__ parcs,
+    uint32_t* __restrict__ cursor) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t* s = reinterpret_cast<uint64_t*>(smem);  // P entries (lat << 32 | x)
+    uint4* kept = reinterpret_cast<uint4*>(s + P);     // V staged arcs
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(kept + V);
+    const uint32_t u = blockIdx.x, tid = threadIdx.x;
+    const uint32_t* row = Wl + (size_t)u * V;
+    for (uint32_t i = tid; i < P; i += BLOCK)
+        s[i] = i < V ? (((uint64_t)row[i] << 32) | i) : ~0ull;
+    if (tid == 0) cnt[0] = 0;
+    __syncthreads();
+    // bitonic sort ascending (only the first K entries are used)
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < P; i += BLOCK) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = s[i], b = s[l];
+                    if ((a > b) == ((i & k) == 0)) {
+                        s[i] = b;
+                        s[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    uint32_t xs[K], as[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const uint64_t e = j < (int)P ? s[j] : ~0ull;
+        as[j] = (uint32_t)(e >> 32);
+        xs[j] = (uint32_t)e;
+    }
+    const size_t base = (size_t)u * V;
+    for (uint32_t v = tid; v < V; v += BLOCK) {  // 2-hop test of every arc of u
+        const uint32_t w = row[v];
+        if (w == kLat32Inf) continue;
+        uint32_t z = kLat32Inf;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            if (as[j] == kLat32Inf) break;
+            const uint32_t b = Wl[(size_t)xs[j] * V + v];
+            const uint32_t t = as[j] + b;
+            if (b != kLat32Inf && t >= as[j]) z = min(z, t);
+        }
+        if (w <= z) {
+            const uint32_t slot = atomicAdd(&cnt[0], 1u);
+            const uint64_t key = Wk[base + v];
+            kept[slot] = make_uint4(v, w, __float_as_uint(one_minus(key_loss(key))), 0u);
+        }
+    }
+    __syncthreads();
+    // rows land contiguously (in any row order) so the kept arcs stay dense in L2
+    if (tid == 0) cnt[1] = atomicAdd(cursor, cnt[0]);
+    __syncthreads();
+    const uint32_t n = cnt[0], at = cnt[1];
+    for (uint32_t i = tid; i < n; i += BLOCK) parcs[at + i] = kept[i];
+    if (tid == 0) {
+        pbeg[u] = at;
+        pend[u] = at + n;
     }
 }
 
@@ -242,6 +402,7 @@ struct HostGraph {
     std::vector<uint64_t> diag_lat;      // per used index
     std::vector<float> diag_loss;
     uint64_t max_arc_lat = 0;
+    double sum_arc_lat = 0;
 };
 
 static uint32_t gml_id(const shd_graph* g, uint32_t idx) {
@@ -317,8 +478,9 @@ static void build_csr(const shd_graph* g, bool reverse, HostGraph& H) {
         const uint32_t a = g->edge_src[i], b = g->edge_dst[i];
         if (a == b) continue;
         const uint64_t l = g->edge_latency_ns[i];
-        const float p = g->edge_packet_loss[i];
+        const float p = g->edge_packet_loss[i] + 0.0f;  // -0.0 -> +0.0: same fold, ordered bits
         H.max_arc_lat = std::max(H.max_arc_lat, l);
+        H.sum_arc_lat += l;
         auto put = [&](uint32_t from, uint32_t to) {
             const uint32_t k = fill[from]++;
             H.dst[k] = to;
@@ -357,6 +519,7 @@ static shd_status reset_flags(shd_ctx* ctx) {
     SHD_TRY(ctx->g_flags.ensure(64));
     SHD_HIP(hipMemsetAsync(ctx->g_flags.p, 0, 16, ctx->stream));
     SHD_HIP(hipMemsetAsync(ctx->g_flags.as<char>() + 16, 0xFF, 8, ctx->stream));
+    SHD_HIP(hipMemsetAsync(ctx->g_flags.as<char>() + 32, 0, 16, ctx->stream));
     return SHD_OK;
 }
 
@@ -453,16 +616,20 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
         P.arcs = H.dst.size();
         P.max_arc_lat = H.max_arc_lat;
         P.narrow_arcs = H.max_arc_lat < kLat32Inf;
+        P.mean_arc_lat = H.dst.empty() ? 1u
+                         : (uint32_t)std::min<double>(kLat32Inf - 1, H.sum_arc_lat / H.dst.size());
         if (P.narrow_arcs) {
             std::vector<uint32_t> l32(H.lat.begin(), H.lat.end());
             SHD_TRY(upload(ctx->g_off, H.off, s));
             SHD_TRY(upload(ctx->g_dst, H.dst, s));
             SHD_TRY(upload(ctx->g_lat, l32, s));
             SHD_TRY(upload(ctx->g_aux, H.loss, s));
-            SHD_TRY(ctx->g_q.ensure(std::max<size_t>(H.loss.size(), 1) * 4));
+            SHD_TRY(ctx->g_arc16.ensure(std::max<size_t>(H.loss.size(), 1) * 16));
             if (!H.loss.empty())
-                arcs_q<<<div_up(H.loss.size(), 256), 256, 0, s>>>(ctx->g_aux.as<float>(),
-                                                                 ctx->g_q.as<float>(), H.loss.size());
+                arcs_pack<<<div_up(H.loss.size(), 256), 256, 0, s>>>(
+                    ctx->g_dst.as<uint32_t>(), ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(),
+                    ctx->g_arc16.as<uint4>(), H.loss.size());
+            P.pruned_arcs = 0;
         }
     }
     SHD_HIP(hipStreamSynchronize(s));
@@ -510,25 +677,118 @@ static shd_status run_direct(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d
     return SHD_OK;
 }
 
-static shd_status run_sssp(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d_lat, float* d_loss,
-                           bool* ovf) {
+struct ArcView {
+    const uint32_t *beg, *end;
+    const uint4* arcs;
+    uint64_t n_arcs;
+};
+
+template <int BLOCK, int G>
+static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, size_t lds,
+                         uint64_t* d_lat, float* d_loss, uint32_t delta) {
+    PreparedGraph& P = ctx->prep;
+    sssp_lds_group<BLOCK, G><<<re - rb, BLOCK, lds, ctx->stream>>>(
+        A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
+        ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
+        ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
+        delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr);
+}
+
+static size_t sssp_lds_bytes(uint32_t V, uint32_t block) {
+    // labels + bitmap + control + per-wave queues + arc ranges (8-byte aligned)
+    const size_t head = (size_t)V * 8 + (size_t)((V + 31) / 32) * 4 + 16 + (block / 64) * 32 * 4;
+    return ((head + 7) & ~(size_t)7) + (size_t)V * 8;
+}
+
+template <int BLOCK>
+static void launch_by_degree(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint64_t* d_lat,
+                             float* d_loss, uint32_t delta, uint32_t G) {
+    const size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK);
+    switch (G) {
+        case 64: launch_group<BLOCK, 64>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        case 32: launch_group<BLOCK, 32>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        case 16: launch_group<BLOCK, 16>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        case 8: launch_group<BLOCK, 8>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        default: launch_group<BLOCK, 4>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+    }
+}
+
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? (uint32_t)std::strtoul(v, nullptr, 10) : dflt;
+}
+
+static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re,
+                           uint64_t* d_lat, float* d_loss, uint32_t delta, bool* ovf) {
     PreparedGraph& P = ctx->prep;
     hipStream_t s = ctx->stream;
-    const uint32_t V = P.V;
-    const size_t lds = (size_t)V * 8 + (size_t)((V + 31) / 32) * 4 + 16;
+    const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
+    uint32_t G = deg >= 40 ? 64 : deg >= 20 ? 32 : deg >= 10 ? 16 : deg >= 5 ? 8 : 4;
+    G = env_u32("SHD_SSSP_G", G);          // tuning overrides (results are identical)
+    const uint32_t block = env_u32("SHD_SSSP_BLOCK", 256);
     SHD_HIP(hipEventRecord(ctx->ev[2], s));
-    sssp_lds_narrow<kSsspBlock><<<re - rb, kSsspBlock, lds, s>>>(
-        ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(), ctx->g_lat.as<uint32_t>(),
-        ctx->g_q.as<float>(), V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
-        ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
-        ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16));
+    if (block == 512 && sssp_lds_bytes(P.V, 512) <= ctx->max_lds)
+        launch_by_degree<512>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+    else
+        launch_by_degree<256>(ctx, A, rb, re, d_lat, d_loss, delta, G);
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(ctx->ev[3], s));
-    ctx->info.algo_used = SHD_ALGO_SSSP;
     uint32_t fl = 0;
     SHD_HIP(hipMemcpyAsync(&fl, ctx->g_flags.p, 4, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     *ovf = fl != 0;
+    if (ctx->stats_on) {
+        unsigned long long st[2];
+        SHD_HIP(hipMemcpy(st, ctx->g_flags.as<char>() + 32, 16, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "shd_sssp: rows=%u G=%u block=%u delta=%u expanded=%llu (%.2f per node) "
+                     "sweeps=%llu (%.1f per row) arcs=%llu\n", re - rb, G, block, delta, st[0],
+                     (double)st[0] / ((double)(re - rb) * P.V), st[1], (double)st[1] / (re - rb),
+                     (unsigned long long)A.n_arcs);
+    }
+    return SHD_OK;
+}
+
+constexpr uint32_t kPruneK = 32;
+constexpr uint32_t kPruneMaxV = 4096;
+
+// Dense arc matrix + k-nearest 2-hop prune over all V rows -> pruned arc lists (row stride V).
+static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
+    PreparedGraph& P = ctx->prep;
+    hipStream_t s = ctx->stream;
+    const uint32_t V = P.V;
+    const uint64_t nn = (uint64_t)V * V;
+    uint32_t Pw = 1;
+    while (Pw < V) Pw <<= 1;
+    SHD_TRY(ctx->g_dense.ensure(nn * 8));
+    SHD_TRY(ctx->g_labels.ensure(nn * 4));
+    SHD_TRY(ctx->g_prune_dst.ensure(nn * 16));
+    SHD_TRY(ctx->g_prune_cnt.ensure((size_t)V * 8 + 16));
+    uint64_t* Wk = ctx->g_dense.as<uint64_t>();
+    uint32_t* Wl = ctx->g_labels.as<uint32_t>();
+    uint32_t* pbeg = ctx->g_prune_cnt.as<uint32_t>();
+    uint32_t* pend = pbeg + V;
+    uint32_t* cursor = pend + V;
+    SHD_HIP(hipMemsetAsync(cursor, 0, 4, s));
+    dense_init<<<div_up(nn, 256), 256, 0, s>>>(Wk, nn);
+    dense_scatter<<<V, 256, 0, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
+                                    ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wk);
+    dense_lat<<<div_up(nn, 256), 256, 0, s>>>(Wk, Wl, nn);
+    prune_rows<256, kPruneK><<<V, 256, (size_t)Pw * 8 + (size_t)V * 16 + 16, s>>>(
+        Wl, Wk, V, Pw, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor);
+    SHD_HIP(hipGetLastError());
+    *out = ArcView{pbeg, pend, ctx->g_prune_dst.as<uint4>(), 0};
+    return SHD_OK;
+}
+
+static shd_status count_kept(shd_ctx* ctx, const ArcView& A) {
+    std::vector<uint32_t> b(ctx->prep.V), e(ctx->prep.V);
+    SHD_HIP(hipMemcpyAsync(b.data(), A.beg, b.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    SHD_HIP(hipMemcpyAsync(e.data(), A.end, e.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    SHD_HIP(hipStreamSynchronize(ctx->stream));
+    uint64_t k = 0;
+    for (size_t i = 0; i < b.size(); i++) k += e[i] - b[i];
+    ctx->info.arcs_kept = k;
+    ctx->prep.pruned_arcs = k;
     return SHD_OK;
 }
 
@@ -552,11 +812,25 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ctx->info.ms_total = ctx->info.ms_main = ms;
         return st;
     }
-    const size_t lds = (size_t)P.V * 8 + (size_t)((P.V + 31) / 32) * 4 + 16;
+    const size_t lds = sssp_lds_bytes(P.V, 256);
     if (P.narrow_arcs && lds <= ctx->max_lds) {
+        const bool dense = P.V <= kPruneMaxV && P.arcs * 8 >= (uint64_t)P.V * P.V;
+        const bool prune = (algo == SHD_ALGO_PRUNED || (algo == SHD_ALGO_AUTO && dense)) &&
+                           P.V <= kPruneMaxV;
+        ArcView A{ctx->g_off.as<uint32_t>(), ctx->g_off.as<uint32_t>() + 1, ctx->g_arc16.as<uint4>(),
+                  P.arcs};
+        if (prune) {
+            SHD_TRY(run_prune(ctx, &A));
+            // the kept-arc count steers the lane-group width; it is known after the first build
+            A.n_arcs = P.pruned_arcs ? P.pruned_arcs : (uint64_t)P.V * 64;
+        }
         bool ovf = false;
-        (void)algo;
-        SHD_TRY(run_sssp(ctx, rb, re, d_lat, d_loss, &ovf));
+        // delta-stepping bucket width: the mean kept-arc latency (env override for tuning)
+        uint32_t delta = kLat32Inf;
+        if (algo == SHD_ALGO_DELTA) delta = env_u32("SHD_SSSP_DELTA", P.mean_arc_lat);
+        SHD_TRY(run_sssp(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
+        ctx->info.algo_used = algo == SHD_ALGO_DELTA ? SHD_ALGO_DELTA
+                              : prune ? SHD_ALGO_PRUNED : SHD_ALGO_SSSP;
         SHD_HIP(hipEventRecord(ctx->ev[1], s));
         SHD_HIP(hipEventSynchronize(ctx->ev[1]));
         float ms = 0, ms_main = 0;
@@ -564,6 +838,8 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);
         ctx->info.ms_total = ms;
         ctx->info.ms_main = ms_main;
+        if (prune && P.pruned_arcs == 0) SHD_TRY(count_kept(ctx, A));  // once per prepared graph
+        ctx->info.arcs_kept = prune ? P.pruned_arcs : P.arcs;
         if (!ovf) return check_unreach(ctx, err);
         SHD_TRY(reset_flags(ctx));  // some path latency >= 2^32-1 ns: redo with u64 labels
     }

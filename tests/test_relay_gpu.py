@@ -46,10 +46,13 @@ def _c5_like(n_hosts, n_nodes, n_packets, seed, start=10**9, runahead=10**6):
     return lat, loss, synth.c5_host_nodes(n_hosts, n_nodes), synth.host_rng_states(n_hosts, 1), b
 
 
+@pytest.mark.parametrize("force_v1", [False, True])
 @pytest.mark.parametrize("chance_mode", [False, True])
-def test_multi_round_vs_c_oracle(engine, chance_mode):
-    """Three consecutive rounds on 20k hosts / 1M packets: streams and ids carry across rounds."""
+def test_multi_round_vs_c_oracle(engine, chance_mode, force_v1, monkeypatch):
+    """Three consecutive rounds on 20k hosts / 1M packets: streams and ids carry across rounds
+    (both the 16-byte-record pipeline and the 64-bit fallback pipeline)."""
     from shadow_amd.relay import Relay
+    monkeypatch.setenv("SHD_RELAY_FORCE_V1", "1" if force_v1 else "0")
     H, NN = 20_000, 200
     lat, loss, host_node, rng0, _ = _c5_like(H, NN, 1000, 11)
     nid0 = np.zeros(H, np.uint64)
@@ -127,3 +130,29 @@ def test_empty_and_all_skipped_rounds(engine):
     assert r.n_sent == 0 and (r.status == 0).all()
     st, _ = rl.host_state()
     assert (st == 1).all()   # no draw for completed sends
+
+
+def test_wide_latency_table_and_failed_round_keeps_state(engine):
+    """Paths >= 2^32 ns take the 64-bit pipeline; a round naming an unknown host fails with
+    NO_HOST and leaves every RNG stream and event id untouched."""
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    from shadow_amd._native import ShdError
+    H, NN = 300, 12
+    lat, loss, host_node, rng0, b = _c5_like(H, NN, 20_000, 8)
+    lat = lat * np.uint64(3)
+    lat[0, 1] = np.uint64(5 * 2**32)
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss,
+                         rng0.copy(), np.zeros(H, np.uint64), 10**9 + 10**6, 10**13, 0)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    bad = b.dst_host.copy()
+    bad[len(bad) // 2] = H + 5
+    with pytest.raises(ShdError, match="NO_HOST"):
+        rl.round(b.src_off, b.send_time, bad, b.payload, 10**9 + 10**6, 10**13, 0)
+    st, nid = rl.host_state()
+    assert np.array_equal(st, rng0) and (nid == 0).all()
+    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, 10**9 + 10**6, 10**13, 0)
+    assert np.array_equal(r.status, o["status"])
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(r, "ev_" + k), o["events"][k]), k
+    del synth

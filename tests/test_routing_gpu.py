@@ -145,3 +145,23 @@ def test_row_shards_concatenate(engine):
     parts = [g.compute_shortest_paths(used, engine, rows=(a, min(a + 64, 257))) for a in range(0, 257, 64)]
     assert np.array_equal(np.concatenate([p.lat for p in parts]), full.lat)
     assert np.array_equal(np.concatenate([p.loss for p in parts]).view(np.uint32), full.loss.view(np.uint32))
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_negative_zero_loss_and_parallel_edges(engine, algo):
+    """'packet_loss -0.0' passes the reference's range check; parallel arcs of equal latency."""
+    rng = np.random.default_rng(42)
+    ids, s, d, l, p, directed = random_graph(rng, 80, 0.3, False, max_ms=6)
+    k = len(s) // 3
+    s = np.concatenate([s, s[:k]]); d = np.concatenate([d, d[:k]])
+    l = np.concatenate([l, l[:k]]); p = np.concatenate([p, rng.uniform(0, 0.3, k).astype(np.float32)])
+    p[rng.random(len(p)) < 0.2] = np.float32(-0.0)
+    loops = s == d
+    keep = ~loops | (np.cumsum(loops) <= 80)          # exactly one self-loop per node
+    s, d, l, p = s[keep], d[keep], l[keep], p[keep]
+    used = np.arange(80, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(80, s, d, l, p, directed, used)
+    assert code == "OK"
+    from shadow_amd.routing import NetworkGraph
+    t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=algo)
+    _assert_table(t, lat, loss.view(np.uint32))
