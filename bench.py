@@ -132,7 +132,7 @@ def routing_leg(eng, world, rank, steps, warmup):
                 lat=full_lat[:n].cpu().numpy().view(np.uint64), loss=full_loss[:n].cpu().numpy(), el=el)
 
 
-def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table):
+def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=False):
     import torch
     from shadow_amd import _native as N
     from shadow_amd import synth
@@ -144,6 +144,10 @@ def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table):
     nid0 = np.zeros(H, np.uint64)
     N.check(eng.lib.shd_relay_setup(eng.ctx, H, N.ptr(host_node), 1000, N.ptr(lat_table),
                                     N.ptr(loss_table), N.ptr(rng0), N.ptr(nid0)), "relay_setup")
+    # per-path packet counters: the reference only reads them in log_packet_counts, which is
+    # never called, and the CPU baseline does not keep them either -> off in both legs; the
+    # cost with them on is reported separately (counters_on_ms_per_round)
+    N.check(eng.lib.shd_relay_set_counters(eng.ctx, 1 if counters else 0), "set_counters")
     dev = lambda a, dt: torch.from_numpy(a.view(dt)).cuda()  # noqa: E731
     d_off = dev(b.src_off, np.int32)
     d_time = dev(b.send_time, np.int64)
@@ -254,12 +258,16 @@ def main():
     if not args.no_relay:
         ks = args.relay_steps or max(3, args.steps // 2)
         rl = relay_leg(eng, world, rank, ks, min(args.warmup, 2), r["lat"], r["loss"])
+        rl_c = relay_leg(eng, world, rank, max(2, ks // 3), 1, r["lat"], r["loss"], counters=True)
         pv = ks * rl["P"] / rl["dt"]
         ms = rl["ms_per_step"]
         bytes_round = RELAY_BYTES_PER_PACKET * rl["P"] + RELAY_BYTES_PER_HOST * rl["H"]
         ach = bytes_round / (ms * 1e-3) / 1e9
         rel = {"metric": "packets relayed/s per round", "value": pv, "unit": "packets/s",
                "steps": ks, "ms_per_round": ms, "n_sent_last_round": int(rl["n_sent"]),
+               "path_counters": "off (reference reads them only in the never-called "
+                                "log_packet_counts; CPU baseline keeps none)",
+               "counters_on_ms_per_round": rl_c["ms_per_step"],
                "config": {"workload": "C5: 100k hosts on the C2 table, 10M packets per round "
                                       "(src uniform, dst != src, 20% ACK / 60% 1448 B / 20% U[1,1448])",
                           "hosts": rl["H"], "packets": rl["P"],

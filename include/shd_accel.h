@@ -211,6 +211,19 @@ shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round
 shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const shd_round* round,
                                   shd_relay_out* d_out);
 
+/*
+ * Multi-GPU receive side (device buffers).  n_runs event chunks laid end to end (chunk r starts
+ * at d_run_base[r]; d_run_base[n_runs] = n_events); chunk r is grouped by destination with local
+ * offsets d_run_off[r*(n_dst+1) + d] and each destination's run in EventQueue order, as
+ * shd_relay_round_device returns it.  Senders must own disjoint source-host ranges.  Writes the
+ * merged events (again in EventQueue order per destination) and d_out->ev_off[n_dst+1].
+ */
+shd_status shd_events_merge_device(shd_ctx* ctx, uint32_t n_runs, uint32_t n_dst,
+                                   const uint32_t* d_run_base, const uint32_t* d_run_off,
+                                   const uint64_t* d_deliver, const uint32_t* d_src,
+                                   const uint64_t* d_seq, const uint32_t* d_pkt,
+                                   uint64_t n_events, shd_relay_out* d_out);
+
 /* Read back the per-host RNG states / next event ids (e.g. to hand RNG use back to the CPU). */
 shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t* next_event_id);
 

@@ -25,7 +25,8 @@ EXPORTED = [
     "shd_routing_build", "shd_routing_prepare", "shd_routing_run", "shd_routing_build_device",
     "shd_routing_last_info",
     "shd_routing_lookup", "shd_routing_smallest_latency", "shd_relay_setup", "shd_relay_round",
-    "shd_relay_round_device", "shd_relay_get_host_state", "shd_relay_set_counters",
+    "shd_relay_round_device", "shd_events_merge_device", "shd_relay_get_host_state",
+    "shd_relay_set_counters",
     "shd_path_packet_counts",
 ]
 
@@ -107,6 +108,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_relay_round_device": (I32, [P, P, P, P]),
         "shd_relay_get_host_state": (I32, [P, P, P]),
         "shd_relay_set_counters": (I32, [P, I32]),
+        "shd_events_merge_device": (I32, [P, U32, U32, P, P, P, P, P, P, U64, P]),
         "shd_path_packet_counts": (I32, [P, P]),
     }
     for name, (res, args) in sig.items():

@@ -282,18 +282,14 @@ __global__ __launch_bounds__(256) void segment_sort_big(
 // ==========================================================================================
 // Relay v2 (every path latency < 2^32 ns and every deliver - round_end < 2^32): 16-byte event
 // records {deliver - round_end, src host, seq - seq_base[src], packet index}.
-//
-// K1 relay_stamp_v2: a workgroup owns BLOCK consecutive source hosts, i.e. one contiguous range
-// of the source-grouped batch, and walks it in chunks of C packets staged through LDS:
-//   (a) coalesced loads of the chunk's send times / destinations / payloads (/ chances);
-//   (b) each host marks its packets in the chunk (owner map in LDS);
-//   (c) lane-per-packet gather of the path entry (host_node[dst], lat, loss);
-//   (d) lane-per-host sequential pass: RNG draw, drop rule, deliver stamp, event id -- the only
-//       part that must follow each host's send order;
-//   (e) lane-per-packet: claim a destination-bucket slot, coalesced stores of status/record/slot.
+//   K1 relay_stamp_v2   lane per source host, sends in batches (below)
+//   K2 rocPRIM radix sort of the records by destination -- stable, LSD: the batch is in
+//      (source host, event id) order, so every destination's run stays in that order and no
+//      per-packet global atomic is needed
+//   K3 bucket_offsets   lower bound of every destination in the sorted keys
+//   K4 segment_sort_v3  stable rank sort of each destination run by deliver time
 // ==========================================================================================
-constexpr uint32_t kStampHosts = 256;
-constexpr uint32_t kStampChunk = 1024;
+constexpr uint32_t kStampBatch = 8;
 
 struct RelayArgs2 {
     uint32_t n_hosts, n_nodes;
@@ -313,115 +309,78 @@ struct RelayArgs2 {
     uint64_t round_end, sim_end, bootstrap_end;
     uint8_t* status;
     uint4* rec;          // per packet (valid when SENT)
-    uint32_t* slot;      // per packet
-    uint32_t* dst_cnt;
+    uint32_t* key;       // per packet: destination host if SENT, else n_hosts (sorts last)
     unsigned long long* red;   // [0] min deliver [1] min latency [2] n_sent [3] bad dst [4] wide
 };
 
-__global__ __launch_bounds__(kStampHosts) void relay_stamp_v2(RelayArgs2 a) {
-    constexpr uint32_t B = kStampHosts, C = kStampChunk;
-    __shared__ uint32_t s_off[B + 1];
-    __shared__ uint64_t t_time[C];
-    __shared__ uint32_t t_dst[C];
-    __shared__ uint32_t t_pay[C];
-    __shared__ uint32_t t_lat[C];
-    __shared__ float t_loss[C];
-    __shared__ uint32_t t_aux[C];    // owner lane, then the event record's deliver offset
-    __shared__ uint32_t t_seq[C];    // seq offset (SENT) | status in the top byte
-    const uint32_t tid = threadIdx.x;
-    const uint32_t h0 = blockIdx.x * B;
-    const uint32_t nh = min(B, a.n_hosts - h0);
-    for (uint32_t i = tid; i <= nh; i += B) s_off[i] = a.src_off[h0 + i];
-    __syncthreads();
-    const bool mine = tid < nh;
-    const uint32_t h = h0 + tid;
-    uint32_t my_b = 0, my_e = 0;
-    Xoshiro r{0, 0, 0, 0};
-    uint64_t id0 = 0;
-    uint32_t nsent = 0;
-    if (mine) {
-        my_b = s_off[tid];
-        my_e = s_off[tid + 1];
-        r = Xoshiro{a.rng[4 * (size_t)h], a.rng[4 * (size_t)h + 1], a.rng[4 * (size_t)h + 2],
-                    a.rng[4 * (size_t)h + 3]};
-        id0 = a.next_id[h];
-    }
+// Lane per source host (its RNG stream and event ids are sequential), kStampBatch sends at a
+// time: the batch's loads, its host_node[dst] gathers and its path gathers are each issued
+// together, so every lane keeps kStampBatch independent memory requests in flight.
+__global__ __launch_bounds__(256) void relay_stamp_v2(RelayArgs2 a) {
+    constexpr uint32_t R = kStampBatch;
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
     uint64_t min_d = ~0ull, min_l = ~0ull;
+    uint32_t nsent = 0;
     bool wide = false;
-    const uint32_t P0 = s_off[0], P1 = s_off[nh];
-    for (uint32_t c0 = P0; c0 < P1; c0 += C) {
-        const uint32_t cn = min(C, P1 - c0);
-        for (uint32_t j = tid; j < cn; j += B) {   // (a)
-            t_time[j] = a.send_time[c0 + j];
-            t_dst[j] = a.dst_host[c0 + j];
-            t_pay[j] = a.payload[c0 + j];
-        }
-        if (mine)                                    // (b)
-            for (uint32_t i = max(my_b, c0); i < min(my_e, c0 + cn); ++i) t_aux[i - c0] = tid;
-        __syncthreads();
-        for (uint32_t j = tid; j < cn; j += B) {   // (c)
-            const uint32_t d = t_dst[j];
-            if (d >= a.n_hosts) {
-                atomicMin(&a.red[3], (unsigned long long)(c0 + j));
-                t_lat[j] = 0;
-                t_loss[j] = 0.0f;
-                continue;
+    if (h < a.n_hosts) {
+        Xoshiro r{a.rng[4 * (size_t)h], a.rng[4 * (size_t)h + 1], a.rng[4 * (size_t)h + 2],
+                  a.rng[4 * (size_t)h + 3]};
+        const uint64_t id0 = a.next_id[h];
+        const uint32_t b0 = a.src_off[h], b1 = a.src_off[h + 1];
+        const size_t srow = (size_t)a.host_node[h] * a.n_nodes;
+        for (uint32_t i0 = b0; i0 < b1; i0 += R) {
+            uint64_t now[R];
+            uint32_t dst[R], pay[R], dn[R];
+#pragma unroll
+            for (uint32_t t = 0; t < R; ++t) {
+                const uint32_t i = i0 + t;
+                const bool v = i < b1;
+                now[t] = v ? a.send_time[i] : ~0ull;
+                dst[t] = v ? a.dst_host[i] : 0u;
+                pay[t] = v ? a.payload[i] : 0u;
             }
-            const size_t pi = (size_t)a.host_node[h0 + t_aux[j]] * a.n_nodes + a.host_node[d];
-            const uint64_t l = a.lat[pi];
-            if (l >> 32) wide = true;
-            t_lat[j] = (uint32_t)l;
-            t_loss[j] = a.loss[pi];
-        }
-        __syncthreads();
-        if (mine) {                                  // (d) sequential per source host
-            for (uint32_t i = max(my_b, c0); i < min(my_e, c0 + cn); ++i) {
-                const uint32_t j = i - c0;
-                const uint64_t now = t_time[j];
-                uint32_t st = kStSkipped, off = 0;
-                if (now < a.sim_end && t_dst[j] < a.n_hosts) {
-                    const double reliability = (double)one_minus(t_loss[j]);
+#pragma unroll
+            for (uint32_t t = 0; t < R; ++t) {
+                if (dst[t] >= a.n_hosts && i0 + t < b1) {   // "No host ID for dest address"
+                    atomicMin(&a.red[3], (unsigned long long)(i0 + t));
+                    now[t] = ~0ull;
+                }
+                dn[t] = dst[t] < a.n_hosts ? a.host_node[dst[t]] : 0u;
+            }
+            uint64_t lat[R];
+            float loss[R];
+#pragma unroll
+            for (uint32_t t = 0; t < R; ++t) {
+                const bool v = now[t] < a.sim_end;
+                lat[t] = v ? a.lat[srow + dn[t]] : 0ull;
+                loss[t] = v ? a.loss[srow + dn[t]] : 0.0f;
+            }
+#pragma unroll
+            for (uint32_t t = 0; t < R; ++t) {
+                const uint32_t i = i0 + t;
+                if (i >= b1) break;
+                uint32_t st = kStSkipped;
+                if (now[t] < a.sim_end) {
+                    const double reliability = (double)one_minus(loss[t]);
                     const double ch = a.chance ? a.chance[i] : r.gen_f64();
-                    if (!(now < a.bootstrap_end) && ch >= reliability && t_pay[j] > 0) {
+                    if (!(now[t] < a.bootstrap_end) && ch >= reliability && pay[t] > 0) {
                         st = kStDropped;
                     } else {
-                        const uint64_t lat = t_lat[j];
-                        uint64_t t = now + lat;
-                        if (t < a.round_end) t = a.round_end;
-                        const uint64_t dd = t - a.round_end;
-                        if (dd >> 32) wide = true;
-                        off = (uint32_t)dd;
-                        min_d = t < min_d ? t : min_d;
-                        min_l = lat < min_l ? lat : min_l;
+                        uint64_t tt = now[t] + lat[t];
+                        if (tt < a.round_end) tt = a.round_end;
+                        const uint64_t dd = tt - a.round_end;
+                        if ((dd >> 32) || (lat[t] >> 32)) wide = true;
+                        min_d = tt < min_d ? tt : min_d;
+                        min_l = lat[t] < min_l ? lat[t] : min_l;
                         st = kStSent;
-                        t_seq[j] = nsent++;
+                        a.rec[i] = make_uint4((uint32_t)dd, h, nsent++, i);
+                        if (a.counts) atomicAdd(&a.counts[srow + dn[t]], 1ull);
                     }
                 }
-                t_aux[j] = off;
-                t_pay[j] = st;   // payload no longer needed: reuse as status
+                a.status[i] = (uint8_t)st;
+                a.key[i] = st == kStSent ? dst[t] : a.n_hosts;
             }
         }
-        __syncthreads();
-        for (uint32_t j = tid; j < cn; j += B) {   // (e)
-            const uint32_t st = t_pay[j];
-            a.status[c0 + j] = (uint8_t)st;
-            if (st == kStSent) {
-                const uint32_t d = t_dst[j];
-                a.slot[c0 + j] = atomicAdd(&a.dst_cnt[d], 1u);
-                // owner recomputed from the chunk range: binary search in s_off
-                uint32_t lo = 0, hi = nh;
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_off[mid] <= c0 + j) lo = mid; else hi = mid;
-                }
-                a.rec[c0 + j] = make_uint4(t_aux[j], h0 + lo, t_seq[j], c0 + j);
-                if (a.counts)
-                    atomicAdd(&a.counts[(size_t)a.host_node[h0 + lo] * a.n_nodes + a.host_node[d]], 1ull);
-            }
-        }
-        __syncthreads();
-    }
-    if (mine) {
         a.rng_out[4 * (size_t)h] = r.s0;
         a.rng_out[4 * (size_t)h + 1] = r.s1;
         a.rng_out[4 * (size_t)h + 2] = r.s2;
@@ -433,7 +392,7 @@ __global__ __launch_bounds__(kStampHosts) void relay_stamp_v2(RelayArgs2 a) {
     uint64_t ns = nsent;
     for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
     const bool any_wide = __ballot(wide) != 0;
-    if ((tid & 63) == 0) {
+    if ((threadIdx.x & 63) == 0) {
         if (min_d != ~0ull) atomicMin(&a.red[0], (unsigned long long)min_d);
         if (min_l != ~0ull) atomicMin(&a.red[1], (unsigned long long)min_l);
         if (ns) atomicAdd(&a.red[2], (unsigned long long)ns);
@@ -441,13 +400,17 @@ __global__ __launch_bounds__(kStampHosts) void relay_stamp_v2(RelayArgs2 a) {
     }
 }
 
-__global__ __launch_bounds__(256) void relay_scatter_v2(
-    uint64_t n, const uint8_t* __restrict__ status, const uint32_t* __restrict__ dst_host,
-    const uint32_t* __restrict__ slot, const uint4* __restrict__ rec,
-    const uint32_t* __restrict__ ev_off, uint4* __restrict__ brec) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n || status[i] != kStSent) return;
-    brec[ev_off[dst_host[i]] + slot[i]] = rec[i];
+// ev_off[d] = first position of destination d in the sorted keys (lower bound), d in [0, H]
+__global__ __launch_bounds__(256) void bucket_offsets(const uint32_t* __restrict__ key, uint64_t n,
+                                                      uint32_t n_hosts, uint32_t* __restrict__ ev_off) {
+    const uint32_t d = blockIdx.x * 256 + threadIdx.x;
+    if (d > n_hosts) return;
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t m = (lo + hi) >> 1;
+        if (key[m] < d) lo = m + 1; else hi = m;
+    }
+    ev_off[d] = (uint32_t)lo;
 }
 
 __device__ __forceinline__ bool rec_less(const uint4& a, const uint4& b) {
@@ -456,60 +419,82 @@ __device__ __forceinline__ bool rec_less(const uint4& a, const uint4& b) {
     return a.z < b.z;                     // event id offset
 }
 
-// One wave per destination bucket (<= kWaveSeg events): bitonic network in the wave's LDS
-// slice, wave-synchronous (no workgroup barrier); then SoA output in EventQueue pop order.
 constexpr uint32_t kWaveSeg = 256;
 
-__global__ __launch_bounds__(256) void segment_sort_v2(
+// One wave per destination run at a time (persistent waves walk the destinations): the run is
+// already in (src host, event id) order, so a STABLE sort by deliver offset gives EventQueue
+// order.  Rank sort: rank(i) = #{j : k_j < k_i} + #{j < i : k_j == k_i}; the keys are read from
+// LDS by broadcast, 4 at a time.  Runs longer than kWaveSeg go to the merge kernel.
+__global__ __launch_bounds__(256) void segment_sort_v3(
     uint32_t n_hosts, const uint32_t* __restrict__ ev_off, const uint4* __restrict__ brec,
     uint64_t round_end, const uint64_t* __restrict__ seq_base, uint64_t* __restrict__ ev_deliver,
     uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq, uint32_t* __restrict__ ev_pkt,
     uint32_t* __restrict__ big) {
-    __shared__ uint4 s[4][kWaveSeg];
+    __shared__ __attribute__((aligned(16))) uint32_t sk[4][kWaveSeg];
+    __shared__ uint4 sr[4][kWaveSeg];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t d = blockIdx.x * 4 + w;
-    if (d >= n_hosts) return;
-    const uint32_t b = ev_off[d], n = ev_off[d + 1] - b;
-    if (n == 0) return;
-    if (n > kWaveSeg) {
-        if (lane == 0) big[atomicAdd(&big[0], 1u) + 1] = d;
-        return;
-    }
-    uint4* x = s[w];
-    uint32_t P = 1;
-    while (P < n) P <<= 1;
-    for (uint32_t i = lane; i < P; i += 64)
-        x[i] = i < n ? brec[b + i] : make_uint4(~0u, ~0u, ~0u, ~0u);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = lane; i < P; i += 64) {
-                const uint32_t l = i ^ j;
-                if (l > i) {
-                    const uint4 p = x[i], q = x[l];
-                    if (rec_less(q, p) == ((i & k) == 0)) {
-                        x[i] = q;
-                        x[l] = p;
-                    }
+    const uint32_t nwaves = gridDim.x * 4;
+    uint32_t* k = sk[w];
+    uint4* x = sr[w];
+    for (uint32_t d = blockIdx.x * 4 + w; d < n_hosts; d += nwaves) {
+        const uint32_t b = ev_off[d], n = ev_off[d + 1] - b;
+        if (n == 0) continue;
+        if (n > kWaveSeg) {
+            if (lane == 0) big[atomicAdd(&big[0], 1u) + 1] = d;
+            continue;
+        }
+        uint4 mine[kWaveSeg / 64];
+        uint32_t mk[kWaveSeg / 64];
+#pragma unroll
+        for (uint32_t c = 0; c < kWaveSeg / 64; ++c) {
+            const uint32_t i = lane + 64 * c;
+            if (i < n) {
+                mine[c] = brec[b + i];
+                mk[c] = mine[c].x;
+                k[i] = mk[c];
+            }
+        }
+        // pad to a multiple of 4 with +inf so the 4-wide key reads stay in bounds
+        if (lane < ((4 - (n & 3)) & 3)) k[n + lane] = ~0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t rank[kWaveSeg / 64];
+#pragma unroll
+        for (uint32_t c = 0; c < kWaveSeg / 64; ++c) rank[c] = 0;
+        const uint4* k4 = reinterpret_cast<const uint4*>(k);
+        for (uint32_t j4 = 0; j4 < (n + 3) / 4; ++j4) {
+            const uint4 q = k4[j4];
+            const uint32_t kk[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) {
+                const uint32_t j = 4 * j4 + e;
+#pragma unroll
+                for (uint32_t c = 0; c < kWaveSeg / 64; ++c) {
+                    const uint32_t i = lane + 64 * c;
+                    rank[c] += (kk[e] < mk[c] || (kk[e] == mk[c] && j < i)) && j < n ? 1u : 0u;
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-    }
-    for (uint32_t i = lane; i < n; i += 64) {
-        const uint4 e = x[i];
-        ev_deliver[b + i] = round_end + e.x;
-        ev_src[b + i] = e.y;
-        ev_seq[b + i] = seq_base[e.y] + e.z;
-        ev_pkt[b + i] = e.w;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (uint32_t c = 0; c < kWaveSeg / 64; ++c)
+            if (lane + 64 * c < n) x[rank[c]] = mine[c];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint4 e = x[i];
+            ev_deliver[b + i] = round_end + e.x;
+            ev_src[b + i] = e.y;
+            ev_seq[b + i] = seq_base[e.y] + e.z;
+            ev_pkt[b + i] = e.w;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
-// Buckets larger than one wave's LDS slice: bottom-up merge passes by one workgroup in a
+// Runs longer than kWaveSeg: bottom-up merge passes by one workgroup in a
 // global scratch copy of the bucket (rank by binary search in the sibling run; keys unique).
 __global__ __launch_bounds__(256) void segment_sort_v2_big(
     const uint32_t* __restrict__ big, const uint32_t* __restrict__ ev_off, uint4* __restrict__ brec,
@@ -557,6 +542,70 @@ __global__ __launch_bounds__(256) void segment_sort_v2_big(
         }
         __syncthreads();
     }
+}
+
+// ------------------------------------------------------------------------------------------
+// Multi-GPU receive side: k-way merge of per-sender runs.  The input is n_runs chunks laid end
+// to end; chunk r holds its events grouped by destination (local offsets off[r][0..n_dst]) and
+// each destination's run sorted in EventQueue order.  Senders own disjoint source-host ranges,
+// so the merged order is again (deliver, src, seq): every event finds its output rank by a
+// binary search in each sibling run (keys are unique) -- no atomics, deterministic.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool ev3_less(uint64_t ta, uint32_t sa, uint64_t qa, uint64_t tb,
+                                         uint32_t sb, uint64_t qb) {
+    if (ta != tb) return ta < tb;
+    if (sa != sb) return sa < sb;
+    return qa < qb;
+}
+
+__global__ __launch_bounds__(256) void merge_runs(
+    uint32_t n_runs, uint32_t n_dst, const uint32_t* __restrict__ base,   // [n_runs+1] chunk starts
+    const uint32_t* __restrict__ off,                                     // [n_runs][n_dst+1]
+    const uint64_t* __restrict__ in_t, const uint32_t* __restrict__ in_s,
+    const uint64_t* __restrict__ in_q, const uint32_t* __restrict__ in_p,
+    const uint32_t* __restrict__ out_off,                                 // [n_dst+1]
+    uint64_t* __restrict__ out_t, uint32_t* __restrict__ out_s, uint64_t* __restrict__ out_q,
+    uint32_t* __restrict__ out_p) {
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= base[n_runs]) return;
+    uint32_t r = 0;
+    while (r + 1 < n_runs && base[r + 1] <= e) ++r;
+    const uint32_t le = e - base[r];
+    const uint32_t* o = off + (size_t)r * (n_dst + 1);
+    uint32_t lo = 0, hi = n_dst;   // d with o[d] <= le < o[d+1]
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (o[m] <= le) lo = m; else hi = m;
+    }
+    const uint32_t d = lo;
+    const uint64_t t = in_t[e], q = in_q[e];
+    const uint32_t sv = in_s[e];
+    uint32_t rank = le - o[d];
+    for (uint32_t r2 = 0; r2 < n_runs; ++r2) {
+        if (r2 == r) continue;
+        const uint32_t* o2 = off + (size_t)r2 * (n_dst + 1);
+        uint32_t a = base[r2] + o2[d], b = base[r2] + o2[d + 1];
+        while (a < b) {   // count of run r2's events less than this one
+            const uint32_t m = (a + b) >> 1;
+            if (ev3_less(in_t[m], in_s[m], in_q[m], t, sv, q)) a = m + 1; else b = m;
+        }
+        rank += a - (base[r2] + o2[d]);
+    }
+    const uint32_t pos = out_off[d] + rank;
+    out_t[pos] = t;
+    out_s[pos] = sv;
+    out_q[pos] = q;
+    out_p[pos] = in_p[e];
+}
+
+__global__ __launch_bounds__(256) void merge_offsets(uint32_t n_runs, uint32_t n_dst,
+                                                     const uint32_t* __restrict__ off,
+                                                     uint32_t* __restrict__ out_off) {
+    const uint32_t d = blockIdx.x * 256 + threadIdx.x;
+    if (d > n_dst) return;
+    uint32_t t = 0;
+    for (uint32_t r = 0; r < n_runs; ++r) t += off[(size_t)r * (n_dst + 1) + d] - off[(size_t)r * (n_dst + 1)];
+    out_off[d] = t;
 }
 
 __global__ void max_u64_kernel(const uint64_t* __restrict__ d, uint64_t n,
@@ -674,12 +723,11 @@ static shd_status relay_device_v2(shd_ctx* ctx, const shd_batch* b, const shd_ro
     const size_t nn = std::max<uint64_t>(n, 1);
     SHD_TRY(R.rec.ensure(nn * 16));
     SHD_TRY(R.brec.ensure(nn * 16));
-    SHD_TRY(R.tmp.ensure(nn * 16));
-    SHD_TRY(R.ev_val.ensure(nn * 4));
+    SHD_TRY(R.ev_val.ensure(nn * 4));    // keys
+    SHD_TRY(R.ev_key.ensure(nn * 4));    // keys (second buffer)
     SHD_TRY(R.ev_val2.ensure((size_t)(H + 2) * 4));
     unsigned long long init[8] = {~0ull, ~0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
     SHD_HIP(hipMemcpyAsync(R.red.p, init, sizeof(init), hipMemcpyHostToDevice, s));
-    SHD_HIP(hipMemsetAsync(R.dst_cnt.p, 0, (size_t)(H + 1) * 4, s));
     SHD_HIP(hipMemsetAsync(R.ev_val2.p, 0, 4, s));
     RelayArgs2 a{};
     a.n_hosts = H;
@@ -702,26 +750,28 @@ static shd_status relay_device_v2(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.bootstrap_end = rd->bootstrap_end;
     a.status = o->status;
     a.rec = R.rec.as<uint4>();
-    a.slot = R.ev_val.as<uint32_t>();
-    a.dst_cnt = R.dst_cnt.as<uint32_t>();
+    a.key = R.ev_val.as<uint32_t>();
     a.red = R.red.as<unsigned long long>();
-    relay_stamp_v2<<<div_up(H, kStampHosts), kStampHosts, 0, s>>>(a);
+    relay_stamp_v2<<<div_up(H, 256), 256, 0, s>>>(a);
     SHD_HIP(hipGetLastError());
+    // stable LSD radix sort of the records by destination (keys <= H)
+    uint32_t bits = 1;
+    while (bits < 32 && (H >> bits) != 0) ++bits;
+    rocprim::double_buffer<uint32_t> kb(R.ev_val.as<uint32_t>(), R.ev_key.as<uint32_t>());
+    rocprim::double_buffer<uint4> vb(R.rec.as<uint4>(), R.brec.as<uint4>());
     size_t tmp_bytes = 0;
-    SHD_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off, 0u,
-                                    (size_t)H + 1, rocprim::plus<uint32_t>(), s));
+    SHD_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, kb, vb, (size_t)n, 0u, bits, s));
     SHD_TRY(R.scan_tmp.ensure(tmp_bytes));
-    SHD_HIP(rocprim::exclusive_scan(R.scan_tmp.p, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off,
-                                    0u, (size_t)H + 1, rocprim::plus<uint32_t>(), s));
-    if (n)
-        relay_scatter_v2<<<div_up(n, 256), 256, 0, s>>>(n, o->status, b->dst_host,
-                                                        R.ev_val.as<uint32_t>(), R.rec.as<uint4>(),
-                                                        o->ev_off, R.brec.as<uint4>());
-    segment_sort_v2<<<div_up(H, 4), 256, 0, s>>>(H, o->ev_off, R.brec.as<uint4>(), rd->round_end,
+    if (n) SHD_HIP(rocprim::radix_sort_pairs(R.scan_tmp.p, tmp_bytes, kb, vb, (size_t)n, 0u, bits, s));
+    uint4* sorted = vb.current();
+    uint4* spare = sorted == R.rec.as<uint4>() ? R.brec.as<uint4>() : R.rec.as<uint4>();
+    bucket_offsets<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(kb.current(), n, H, o->ev_off);
+    segment_sort_v3<<<std::min<uint32_t>(div_up(H, 4), (uint32_t)ctx->n_cu * 8), 256, 0, s>>>(
+                                                 H, o->ev_off, sorted, rd->round_end,
                                                  R.next_id.as<uint64_t>(), o->ev_deliver, o->ev_src,
                                                  o->ev_seq, o->ev_pkt, R.ev_val2.as<uint32_t>());
-    segment_sort_v2_big<<<64, 256, 0, s>>>(R.ev_val2.as<uint32_t>(), o->ev_off, R.brec.as<uint4>(),
-                                           R.tmp.as<uint4>(), rd->round_end, R.next_id.as<uint64_t>(),
+    segment_sort_v2_big<<<64, 256, 0, s>>>(R.ev_val2.as<uint32_t>(), o->ev_off, sorted,
+                                           spare, rd->round_end, R.next_id.as<uint64_t>(),
                                            o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt);
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipMemcpyAsync(R.red_host, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -900,6 +950,29 @@ shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t*
     if (next_event_id)
         SHD_HIP(hipMemcpyAsync(next_event_id, R.next_id.p, (size_t)R.n_hosts * 8, hipMemcpyDeviceToHost, ctx->stream));
     SHD_HIP(hipStreamSynchronize(ctx->stream));
+    return SHD_OK;
+}
+
+shd_status shd_events_merge_device(shd_ctx* ctx, uint32_t n_runs, uint32_t n_dst,
+                                   const uint32_t* d_run_base, const uint32_t* d_run_off,
+                                   const uint64_t* d_deliver, const uint32_t* d_src,
+                                   const uint64_t* d_seq, const uint32_t* d_pkt,
+                                   uint64_t n_events, shd_relay_out* d_out) {
+    if (!ctx || n_runs == 0 || !d_run_base || !d_run_off || !d_out || !d_out->ev_off) return SHD_ERR_INVALID;
+    if (n_events && (!d_deliver || !d_src || !d_seq || !d_pkt || !d_out->ev_deliver ||
+                     !d_out->ev_src || !d_out->ev_seq || !d_out->ev_pkt))
+        return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    merge_offsets<<<div_up((uint64_t)n_dst + 1, 256), 256, 0, s>>>(n_runs, n_dst, d_run_off, d_out->ev_off);
+    if (n_events)
+        merge_runs<<<div_up(n_events, 256), 256, 0, s>>>(n_runs, n_dst, d_run_base, d_run_off, d_deliver,
+                                                        d_src, d_seq, d_pkt, d_out->ev_off,
+                                                        d_out->ev_deliver, d_out->ev_src, d_out->ev_seq,
+                                                        d_out->ev_pkt);
+    SHD_HIP(hipGetLastError());
+    SHD_HIP(hipStreamSynchronize(s));
+    d_out->n_sent = n_events;
     return SHD_OK;
 }
 

@@ -33,7 +33,46 @@ namespace shd {
 // nodes whose latency is <= (min active latency + delta), which keeps the expansion order close
 // to Dijkstra's and cuts re-expansions.  delta = 0xFFFFFFFF expands every active node (plain
 // chaotic Bellman-Ford).  Both converge to the same unique fixed point.
-template <int BLOCK, int G>
+template <int G, int R, bool CACHE>
+__device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* lab, uint32_t* bits,
+                                           const uint2* rng, const uint32_t* __restrict__ abeg,
+                                           const uint32_t* __restrict__ aend,
+                                           const uint4* __restrict__ arcs, bool& ovf, bool& dirty) {
+    const uint64_t ku = __hip_atomic_load(&lab[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t lu = key_lat(ku);
+    const float qu = one_minus(key_loss(ku));
+    const uint2 r = CACHE ? rng[u] : make_uint2(abeg[u], aend[u]);
+    for (uint32_t k0 = r.x + gl; k0 < r.y; k0 += G * R) {
+        // issue R independent arc loads, then R relaxations: R arcs in flight per lane
+        uint4 a[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const uint32_t k = k0 + i * G;
+            a[i] = k < r.y ? arcs[k] : make_uint4(0u, kLat32Inf, 0u, 0u);
+        }
+        uint64_t cand[R], old[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const uint32_t cl = lu + a[i].y;
+            const bool ok = a[i].y != kLat32Inf && cl >= lu && cl != kLat32Inf;
+            if (a[i].y != kLat32Inf && !ok) ovf = true;   // path latency leaves u32: wide rerun
+            cand[i] = ok ? pack_key(cl, fold_q(qu, __uint_as_float(a[i].z))) : kKeyInf;
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            old[i] = cand[i] != kKeyInf ? atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[i].x]),
+                                                    (unsigned long long)cand[i])
+                                        : 0ull;
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            if (cand[i] < old[i]) {
+                atomicOr(&bits[a[i].x >> 5], 1u << (a[i].x & 31));
+                dirty = true;
+            }
+    }
+}
+
+template <int BLOCK, int G, int R, bool CACHE>
 __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
     const uint4* __restrict__ arcs, uint32_t V, const uint32_t* __restrict__ used,
@@ -43,30 +82,31 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
+    constexpr uint32_t NW = BLOCK / 64, NG = 64 / G, QCAP = 64;
     uint64_t* lab = reinterpret_cast<uint64_t*>(smem);
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V);
     uint32_t* ctl = bits + W;            // [0] dirty  [1] min active latency
-    uint32_t* wq = ctl + 4;              // per-wave queue of up to 32 node ids
+    uint32_t* wq = ctl + 4;              // per-wave queue (QCAP + 32 node ids)
     // [V] arc range {beg, end}, 8-byte aligned after the queues
-    const uint32_t rng_off = (((uint32_t)((wq + NW * 32) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
+    const uint32_t rng_off =
+        (((uint32_t)((wq + NW * (QCAP + 32)) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
     uint2* rng = reinterpret_cast<uint2*>(smem + rng_off);
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t grp = lane / G, gl = lane % G;
-    uint32_t* q = wq + wave * 32;
+    uint32_t* q = wq + wave * (QCAP + 32);
     const uint32_t row = row_begin + blockIdx.x;
     const uint32_t src = used[row];
     const bool use_delta = delta != kLat32Inf;
 
     for (uint32_t v = tid; v < V; v += BLOCK) {
         lab[v] = kKeyInf;
-        rng[v] = make_uint2(abeg[v], aend[v]);
+        if (CACHE) rng[v] = make_uint2(abeg[v], aend[v]);
     }
     for (uint32_t w = tid; w < W; w += BLOCK) bits[w] = 0;
     __syncthreads();
     if (tid == 0) {
-        lab[src] = 0;
+        lab[src] = 0;  // PathProperties::default() = (0 ns, 0.0)
         bits[src >> 5] = 1u << (src & 31);
     }
     bool ovf = false;
@@ -93,47 +133,37 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
             thr = lo + delta < lo ? kLat32Inf - 1 : lo + delta;
         }
         bool dirty = false;
-        for (uint32_t widx = wave; widx < W; widx += NW) {
-            const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (word == 0) continue;  // wave-uniform
-            bool sel = lane < 32 && ((word >> lane) & 1u);
-            if (use_delta && sel) sel = key_lat(lab[widx * 32 + lane]) <= thr;
-            const uint32_t mask = (uint32_t)__ballot(sel);
-            if (mask == 0) continue;
-            // words are owned by one wave; other waves only set bits, so clearing `mask` is exact
-            if (lane == 0) atomicAnd(&bits[widx], ~mask);
-            const uint32_t n = __popc(mask);
-            if (sel) q[__popc(mask & ((1u << lane) - 1u))] = widx * 32 + lane;
-            expanded += n;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (uint32_t t = 0; t < n; t += NG) {
-                const uint32_t qi = t + grp;
-                if (qi < n) {
-                    const uint32_t u = q[qi];
-                    const uint64_t ku = __hip_atomic_load(&lab[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    const uint32_t lu = key_lat(ku);
-                    const float qu = one_minus(key_loss(ku));
-                    const uint2 r = rng[u];
-                    for (uint32_t k = r.x + gl; k < r.y; k += G) {
-                        const uint4 a = arcs[k];
-                        const uint32_t cl = lu + a.y;
-                        if (cl < lu || cl == kLat32Inf) {
-                            ovf = true;
-                            continue;
-                        }
-                        const uint64_t cand = pack_key(cl, fold_q(qu, __uint_as_float(a.z)));
-                        const uint64_t old = atomicMin(reinterpret_cast<unsigned long long*>(&lab[a.x]),
-                                                       (unsigned long long)cand);
-                        if (cand < old) {
-                            atomicOr(&bits[a.x >> 5], 1u << (a.x & 31));
-                            dirty = true;
-                        }
+        uint32_t qn = 0;  // wave-uniform queue length
+        for (uint32_t widx = wave;; widx += NW) {
+            const bool more = widx < W;
+            if (more) {
+                const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (word != 0) {  // wave-uniform
+                    bool sel = lane < 32 && ((word >> lane) & 1u);
+                    if (use_delta && sel) sel = key_lat(lab[widx * 32 + lane]) <= thr;
+                    const uint32_t mask = (uint32_t)__ballot(sel);
+                    if (mask) {
+                        // words are owned by one wave; other waves only set bits: clearing is exact
+                        if (lane == 0) atomicAnd(&bits[widx], ~mask);
+                        if (sel) q[qn + __popc(mask & ((1u << lane) - 1u))] = widx * 32 + lane;
+                        qn += __popc(mask);
                     }
                 }
             }
-            __builtin_amdgcn_wave_barrier();
+            if (qn >= QCAP || (!more && qn > 0)) {   // flush: NG nodes per step, G lanes each
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                expanded += qn;
+                for (uint32_t t = 0; t < qn; t += NG) {
+                    const uint32_t qi = t + grp;
+                    if (qi < qn)
+                        relax_node<G, R, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, ovf, dirty);
+                }
+                qn = 0;
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (!more) break;
         }
         ++sweeps;
         if (!use_delta) {
@@ -256,12 +286,14 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
         const uint32_t w = row[v];
         if (w == kLat32Inf) continue;
         uint32_t z = kLat32Inf;
+        uint32_t bv[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)   // all K detour loads in flight together
+            bv[j] = as[j] != kLat32Inf ? Wl[(size_t)xs[j] * V + v] : kLat32Inf;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            if (as[j] == kLat32Inf) break;
-            const uint32_t b = Wl[(size_t)xs[j] * V + v];
-            const uint32_t t = as[j] + b;
-            if (b != kLat32Inf && t >= as[j]) z = min(z, t);
+            const uint32_t t = as[j] + bv[j];
+            if (as[j] != kLat32Inf && bv[j] != kLat32Inf && t >= as[j]) z = min(z, t);
         }
         if (w <= z) {
             const uint32_t slot = atomicAdd(&cnt[0], 1u);
@@ -683,33 +715,34 @@ struct ArcView {
     uint64_t n_arcs;
 };
 
-template <int BLOCK, int G>
+template <int BLOCK, int G, bool CACHE>
 static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, size_t lds,
                          uint64_t* d_lat, float* d_loss, uint32_t delta) {
     PreparedGraph& P = ctx->prep;
-    sssp_lds_group<BLOCK, G><<<re - rb, BLOCK, lds, ctx->stream>>>(
+    constexpr int R = G >= 32 ? 2 : 4;   // arcs in flight per lane
+    sssp_lds_group<BLOCK, G, R, CACHE><<<re - rb, BLOCK, lds, ctx->stream>>>(
         A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
         ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
         delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr);
 }
 
-static size_t sssp_lds_bytes(uint32_t V, uint32_t block) {
-    // labels + bitmap + control + per-wave queues + arc ranges (8-byte aligned)
-    const size_t head = (size_t)V * 8 + (size_t)((V + 31) / 32) * 4 + 16 + (block / 64) * 32 * 4;
-    return ((head + 7) & ~(size_t)7) + (size_t)V * 8;
+static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
+    // labels + bitmap + control + per-wave queues (+ arc ranges, 8-byte aligned)
+    const size_t head = (size_t)V * 8 + (size_t)((V + 31) / 32) * 4 + 16 + (block / 64) * 96 * 4;
+    return cache ? ((head + 7) & ~(size_t)7) + (size_t)V * 8 : head;
 }
 
-template <int BLOCK>
+template <int BLOCK, bool CACHE>
 static void launch_by_degree(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint64_t* d_lat,
                              float* d_loss, uint32_t delta, uint32_t G) {
-    const size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK);
+    const size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK, CACHE);
     switch (G) {
-        case 64: launch_group<BLOCK, 64>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
-        case 32: launch_group<BLOCK, 32>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
-        case 16: launch_group<BLOCK, 16>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
-        case 8: launch_group<BLOCK, 8>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
-        default: launch_group<BLOCK, 4>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        case 16: launch_group<BLOCK, 16, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        case 8: launch_group<BLOCK, 8, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        default: launch_group<BLOCK, 4, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
     }
 }
 
@@ -723,14 +756,29 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
     PreparedGraph& P = ctx->prep;
     hipStream_t s = ctx->stream;
     const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
-    uint32_t G = deg >= 40 ? 64 : deg >= 20 ? 32 : deg >= 10 ? 16 : deg >= 5 ? 8 : 4;
+    // G lanes x R arcs (R = 4 below G = 32) per node; measured best on C2 (pruned, ~48 arcs
+    // per node) at G = 8 and on C3 (BA, ~6 arcs per node) at G = 4
+    uint32_t G = deg >= 64 ? 16 : deg >= 24 ? 8 : 4;
     G = env_u32("SHD_SSSP_G", G);          // tuning overrides (results are identical)
-    const uint32_t block = env_u32("SHD_SSSP_BLOCK", 256);
+    // Workgroup shape: while two workgroups fit a CU's LDS keep 256 threads (several sources per
+    // CU); once a source's labels need most of the LDS, one 1024-thread workgroup per CU.  The
+    // LDS arc-range cache is dropped when it no longer fits.
+    const size_t half = ctx->max_lds / 2;
+    uint32_t block = sssp_lds_bytes(P.V, 256, true) <= half ? 256 : 1024;
+    block = env_u32("SHD_SSSP_BLOCK", block);
+    if (block != 256 && block != 512 && block != 1024) block = 256;
+    const bool cache = sssp_lds_bytes(P.V, block, true) <= ctx->max_lds;
     SHD_HIP(hipEventRecord(ctx->ev[2], s));
-    if (block == 512 && sssp_lds_bytes(P.V, 512) <= ctx->max_lds)
-        launch_by_degree<512>(ctx, A, rb, re, d_lat, d_loss, delta, G);
-    else
-        launch_by_degree<256>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+    if (block == 1024) {
+        if (cache) launch_by_degree<1024, true>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+        else launch_by_degree<1024, false>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+    } else if (block == 512) {
+        if (cache) launch_by_degree<512, true>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+        else launch_by_degree<512, false>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+    } else {
+        if (cache) launch_by_degree<256, true>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+        else launch_by_degree<256, false>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+    }
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(ctx->ev[3], s));
     uint32_t fl = 0;
@@ -812,10 +860,11 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ctx->info.ms_total = ctx->info.ms_main = ms;
         return st;
     }
-    const size_t lds = sssp_lds_bytes(P.V, 256);
+    const size_t lds = sssp_lds_bytes(P.V, 1024, false);
     if (P.narrow_arcs && lds <= ctx->max_lds) {
         const bool dense = P.V <= kPruneMaxV && P.arcs * 8 >= (uint64_t)P.V * P.V;
-        const bool prune = (algo == SHD_ALGO_PRUNED || (algo == SHD_ALGO_AUTO && dense)) &&
+        const bool prune = (algo == SHD_ALGO_PRUNED ||
+                            ((algo == SHD_ALGO_AUTO || algo == SHD_ALGO_DELTA) && dense)) &&
                            P.V <= kPruneMaxV;
         ArcView A{ctx->g_off.as<uint32_t>(), ctx->g_off.as<uint32_t>() + 1, ctx->g_arc16.as<uint4>(),
                   P.arcs};
