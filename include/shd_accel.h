@@ -97,6 +97,7 @@ typedef struct shd_routing_info {
     uint64_t arcs_kept;        /* arcs after pruning (== arcs when no prune ran) */
     double ms_total;           /* device time of the last build (HIP events) */
     double ms_main;            /* device time of the dominant kernel */
+    double ms_minplus;         /* SHD_ALGO_BLOCKED: device time of the min-plus closure */
 } shd_routing_info;
 
 /* ---------------------------------------------------------------- context */

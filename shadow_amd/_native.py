@@ -53,7 +53,8 @@ class Error(C.Structure):
 
 class RoutingInfo(C.Structure):
     _fields_ = [("algo_used", C.c_uint32), ("wide_latency", C.c_uint32), ("arcs", C.c_uint64),
-                ("arcs_kept", C.c_uint64), ("ms_total", C.c_double), ("ms_main", C.c_double)]
+                ("arcs_kept", C.c_uint64), ("ms_total", C.c_double), ("ms_main", C.c_double),
+                ("ms_minplus", C.c_double)]
 
 
 class Round(C.Structure):

@@ -1,0 +1,288 @@
+// Blocked min-plus APSP (SHD_ALGO_BLOCKED) on gfx950: Floyd-Warshall over u32 latencies tiled
+// through LDS on integer VALU (saturating v_add_u32 + v_min3_u32), then a left-fold loss pass
+// restricted to the tight arcs.
+//
+// Why this reproduces the reference bits (FlyearthR/shadow src/main/network/graph/mod.rs):
+//  * latency (PathProperties.latency_ns, :300-333): u64 addition is associative and min is exact,
+//    so a min-plus closure in any bracketing gives Dijkstra's (:196-201) latency.  The adds
+//    saturate at 2^32-1: a candidate that reaches it becomes INF, but a true distance d < 2^32-1
+//    is still produced by its own unsaturated candidate, so every finite entry is exact.  An INF
+//    entry (unreachable, or a path >= 2^32-1 ns) sends the build to the u64 path.
+//  * loss: the f32 fold 1-(1-p)(1-e) is NOT associative, so segment composition is
+//    never applied to it.  Dijkstra's loss label is the minimum LEFT fold over the
+//    shortest-latency walks; every arc (u,v) on such a walk satisfies D[s][u] + w == D[s][v] and
+//    hence w == D[u][v] (a "globally tight" arc).  The loss pass keeps exactly those arcs and
+//    runs the label-correcting kernel (sssp_lds_group, routing.hip) with every label seeded at
+//    (D[s][v], +inf loss): it only appends one arc on the right at a time, and a label can only
+//    improve through a tight arc, so it converges to Dijkstra's loss bits.
+//
+// Layout: D is Vp x Vp u32 row-major (Vp = V rounded up to the tile T), INF = 2^32-1, D[i][i] = 0.
+// One round per diagonal block r (Vp / T rounds), three launches each:
+//   fw_diag    1 workgroup      closes the T x T diagonal block (T sequential steps in LDS)
+//   fw_panels  2 (nb-1) WGs     row panel D[r][j] = Drr* (x) D[r][j]; column panel D[i][r] = D[i][r] (x) Drr*
+//   fw_rest    (nb-1)^2 WGs     D[i][j] = min(D[i][j], D[i][r] (x) D[r][j])
+// (x) is the min-plus product of two T x T tiles, k streamed through LDS in chunks of KC; each
+// thread owns a TM x TM register block (two 4-wide row/column groups spaced T/2 apart when TM
+// = 8, so every ds_read_b128 of a wave is contiguous).
+#include "ctx.h"
+
+namespace shd {
+
+__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) {
+    return __builtin_elementwise_add_sat(a, b);   // v_add_u32 ... clamp
+}
+
+__global__ __launch_bounds__(256) void fw_fill(uint32_t* __restrict__ D, uint32_t Vp) {
+    const uint64_t nn = (uint64_t)Vp * Vp;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nn; i += (uint64_t)gridDim.x * 256)
+        D[i] = (i / Vp == i % Vp) ? 0u : kLat32Inf;
+}
+
+// parallel arcs: only the lowest latency can be on a shortest path
+__global__ __launch_bounds__(256) void fw_scatter(const uint32_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ adst,
+                                                  const uint32_t* __restrict__ alat, uint32_t Vp,
+                                                  uint32_t* __restrict__ D) {
+    const uint32_t u = blockIdx.x;
+    for (uint32_t k = off[u] + threadIdx.x; k < off[u + 1]; k += 256)
+        atomicMin(&D[(size_t)u * Vp + adst[k]], alat[k]);
+}
+
+// Phase 1: close the diagonal block r in LDS.  Thread (i0, j) holds rows i0, i0+RS, ... of
+// column j in registers; after step k only column k+1 and row k+1 are published to LDS (the
+// only entries step k+1 reads; neither changes during its own step since D[k][k] = 0).
+template <int T>
+__global__ __launch_bounds__(256) void fw_diag(uint32_t* __restrict__ D, uint32_t Vp, uint32_t r) {
+    constexpr int RS = 256 / T;          // row step between a thread's entries
+    constexpr int E = T / RS;            // entries per thread
+    __shared__ uint32_t s[T][T + 1];
+    const uint32_t tid = threadIdx.x, j = tid % T, i0 = tid / T;
+    uint32_t* base = D + (size_t)r * T * Vp + (size_t)r * T;
+    uint32_t v[E];
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        v[m] = base[(size_t)(i0 + m * RS) * Vp + j];
+        s[i0 + m * RS][j] = v[m];
+    }
+    __syncthreads();
+    for (int k = 0; k < T; ++k) {
+        const uint32_t bkj = s[k][j];
+#pragma unroll
+        for (int m = 0; m < E; ++m) v[m] = min(v[m], sat_add(s[i0 + m * RS][k], bkj));
+        const int kn = k + 1;
+        if (kn < T) {
+            if ((int)j == kn) {
+#pragma unroll
+                for (int m = 0; m < E; ++m) s[i0 + m * RS][j] = v[m];
+            }
+            if ((int)i0 == kn % RS) {
+#pragma unroll
+                for (int m = 0; m < E; ++m)
+                    if (m == kn / RS) s[kn][j] = v[m];
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int m = 0; m < E; ++m) base[(size_t)(i0 + m * RS) * Vp + j] = v[m];
+}
+
+// acc = min(acc, A (x) B) over one T x T output tile; A rows i / cols k and B rows k / cols j are
+// T x T tiles in global memory (row stride Vp).  k streams through LDS in chunks of KC: At holds
+// A transposed (At[k][i]) and Bs holds B (Bs[k][j]), both with row stride T + 4 (keeps the
+// 16-byte alignment of every 4-wide group and spreads the transposing stores over banks).
+template <int T, int TM, int KC>
+__device__ __forceinline__ void tile_minplus(const uint32_t* __restrict__ A,
+                                             const uint32_t* __restrict__ B, uint32_t Vp,
+                                             uint32_t (&acc)[TM][TM], uint32_t* At, uint32_t* Bs) {
+    constexpr int S = T + 4;
+    constexpr int NT = (T / TM) * (T / TM);   // threads
+    constexpr int G4 = TM / 4;                 // 4-wide groups per thread and dimension
+    constexpr int GS = T / G4;                 // spacing of the groups
+    const uint32_t tid = threadIdx.x, ty = tid / (T / TM), tx = tid % (T / TM);
+    for (int k0 = 0; k0 < T; k0 += KC) {
+        // stage A[:, k0:k0+KC] transposed and B[k0:k0+KC, :] (16-byte global loads)
+        for (uint32_t q = tid; q < (uint32_t)(T * KC / 4); q += NT) {
+            const uint32_t i = q / (KC / 4), kq = (q % (KC / 4)) * 4;
+            const uint4 a = *reinterpret_cast<const uint4*>(A + (size_t)i * Vp + k0 + kq);
+            At[(kq + 0) * S + i] = a.x;
+            At[(kq + 1) * S + i] = a.y;
+            At[(kq + 2) * S + i] = a.z;
+            At[(kq + 3) * S + i] = a.w;
+            const uint32_t kb = q / (T / 4), jq = (q % (T / 4)) * 4;
+            *reinterpret_cast<uint4*>(Bs + kb * S + jq) =
+                *reinterpret_cast<const uint4*>(B + (size_t)(k0 + kb) * Vp + jq);
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int k = 0; k < KC; k += 2) {
+            uint32_t a0[TM], b0[TM], a1[TM], b1[TM];
+#pragma unroll
+            for (int g = 0; g < G4; ++g) {
+                *reinterpret_cast<uint4*>(&a0[4 * g]) = *reinterpret_cast<const uint4*>(At + k * S + g * GS + ty * 4);
+                *reinterpret_cast<uint4*>(&b0[4 * g]) = *reinterpret_cast<const uint4*>(Bs + k * S + g * GS + tx * 4);
+                *reinterpret_cast<uint4*>(&a1[4 * g]) = *reinterpret_cast<const uint4*>(At + (k + 1) * S + g * GS + ty * 4);
+                *reinterpret_cast<uint4*>(&b1[4 * g]) = *reinterpret_cast<const uint4*>(Bs + (k + 1) * S + g * GS + tx * 4);
+            }
+#pragma unroll
+            for (int r = 0; r < TM; ++r)
+#pragma unroll
+                for (int c = 0; c < TM; ++c)
+                    acc[r][c] = min(min(acc[r][c], sat_add(a0[r], b0[c])), sat_add(a1[r], b1[c]));  // v_min3_u32
+        }
+        __syncthreads();
+    }
+}
+
+// a thread's register block <-> global tile (4-wide groups)
+template <int T, int TM>
+__device__ __forceinline__ void tile_load(const uint32_t* __restrict__ C, uint32_t Vp,
+                                          uint32_t (&acc)[TM][TM]) {
+    constexpr int G4 = TM / 4, GS = T / G4;
+    const uint32_t ty = threadIdx.x / (T / TM), tx = threadIdx.x % (T / TM);
+#pragma unroll
+    for (int gr = 0; gr < G4; ++gr)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int gc = 0; gc < G4; ++gc) {
+                const uint4 v = *reinterpret_cast<const uint4*>(
+                    C + (size_t)(gr * GS + ty * 4 + rr) * Vp + gc * GS + tx * 4);
+                acc[gr * 4 + rr][gc * 4 + 0] = v.x;
+                acc[gr * 4 + rr][gc * 4 + 1] = v.y;
+                acc[gr * 4 + rr][gc * 4 + 2] = v.z;
+                acc[gr * 4 + rr][gc * 4 + 3] = v.w;
+            }
+}
+
+template <int T, int TM>
+__device__ __forceinline__ void tile_store(uint32_t* __restrict__ C, uint32_t Vp,
+                                           const uint32_t (&acc)[TM][TM]) {
+    constexpr int G4 = TM / 4, GS = T / G4;
+    const uint32_t ty = threadIdx.x / (T / TM), tx = threadIdx.x % (T / TM);
+#pragma unroll
+    for (int gr = 0; gr < G4; ++gr)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+            for (int gc = 0; gc < G4; ++gc)
+                *reinterpret_cast<uint4*>(C + (size_t)(gr * GS + ty * 4 + rr) * Vp + gc * GS + tx * 4) =
+                    make_uint4(acc[gr * 4 + rr][gc * 4 + 0], acc[gr * 4 + rr][gc * 4 + 1],
+                               acc[gr * 4 + rr][gc * 4 + 2], acc[gr * 4 + rr][gc * 4 + 3]);
+}
+
+constexpr int kFwKC = 32;
+
+// Phase 2: the row and column panels of round r against the closed diagonal block.
+template <int T, int TM>
+__global__ __launch_bounds__((T / TM) * (T / TM)) void fw_panels(uint32_t* __restrict__ D,
+                                                                 uint32_t Vp, uint32_t r) {
+    __shared__ __attribute__((aligned(16))) uint32_t At[kFwKC * (T + 4)];
+    __shared__ __attribute__((aligned(16))) uint32_t Bs[kFwKC * (T + 4)];
+    const uint32_t nb = Vp / T, n1 = nb - 1;
+    const bool row = blockIdx.x < n1;
+    uint32_t t = row ? blockIdx.x : blockIdx.x - n1;
+    t += (t >= r);
+    const uint32_t* Drr = D + (size_t)r * T * Vp + (size_t)r * T;
+    uint32_t* C = row ? D + (size_t)r * T * Vp + (size_t)t * T : D + (size_t)t * T * Vp + (size_t)r * T;
+    uint32_t acc[TM][TM];
+    tile_load<T, TM>(C, Vp, acc);
+    if (row) tile_minplus<T, TM, kFwKC>(Drr, C, Vp, acc, At, Bs);
+    else tile_minplus<T, TM, kFwKC>(C, Drr, Vp, acc, At, Bs);
+    tile_store<T, TM>(C, Vp, acc);
+}
+
+// Phase 3: every tile outside row/column r of the tile grid.
+template <int T, int TM>
+__global__ __launch_bounds__((T / TM) * (T / TM)) void fw_rest(uint32_t* __restrict__ D,
+                                                               uint32_t Vp, uint32_t r) {
+    __shared__ __attribute__((aligned(16))) uint32_t At[kFwKC * (T + 4)];
+    __shared__ __attribute__((aligned(16))) uint32_t Bs[kFwKC * (T + 4)];
+    const uint32_t nb = Vp / T, n1 = nb - 1;
+    uint32_t bi = blockIdx.x / n1, bj = blockIdx.x % n1;
+    bi += (bi >= r);
+    bj += (bj >= r);
+    uint32_t* C = D + (size_t)bi * T * Vp + (size_t)bj * T;
+    uint32_t acc[TM][TM];
+    tile_load<T, TM>(C, Vp, acc);
+    tile_minplus<T, TM, kFwKC>(D + (size_t)bi * T * Vp + (size_t)r * T, D + (size_t)r * T * Vp + (size_t)bj * T,
+                               Vp, acc, At, Bs);
+    tile_store<T, TM>(C, Vp, acc);
+}
+
+// Keep arc (u -> v) iff its latency equals D[u][v]; compact node u's kept arcs contiguously
+// (rows in any order) as {dst, lat32, q = 1f32 - loss, 0}.
+__global__ __launch_bounds__(256) void fw_tight_arcs(const uint32_t* __restrict__ off,
+                                                     const uint4* __restrict__ arcs,
+                                                     const uint32_t* __restrict__ D, uint32_t Vp,
+                                                     uint32_t* __restrict__ pbeg,
+                                                     uint32_t* __restrict__ pend,
+                                                     uint4* __restrict__ parcs,
+                                                     uint32_t* __restrict__ cursor) {
+    __shared__ uint32_t cnt[2];
+    const uint32_t u = blockIdx.x, tid = threadIdx.x;
+    const uint32_t b = off[u], e = off[u + 1];
+    const uint32_t* Du = D + (size_t)u * Vp;
+    if (tid == 0) cnt[0] = cnt[1] = 0;
+    __syncthreads();
+    uint32_t mine = 0;
+    for (uint32_t k = b + tid; k < e; k += 256) {
+        const uint4 a = arcs[k];
+        mine += a.y == Du[a.x] ? 1u : 0u;
+    }
+    if (mine) atomicAdd(&cnt[0], mine);
+    __syncthreads();
+    if (tid == 0) cnt[1] = atomicAdd(cursor, cnt[0]);
+    __syncthreads();
+    const uint32_t at = cnt[1];
+    if (tid == 0) {
+        pbeg[u] = at;
+        pend[u] = at + cnt[0];
+        cnt[0] = 0;
+    }
+    __syncthreads();
+    for (uint32_t k = b + tid; k < e; k += 256) {
+        const uint4 a = arcs[k];
+        if (a.y == Du[a.x]) parcs[at + atomicAdd(&cnt[0], 1u)] = a;
+    }
+}
+
+// Host side: D (device) <- latency closure of the prepared narrow-arc graph.
+shd_status fw_latency(shd_ctx* ctx, uint32_t* D, uint32_t Vp, uint32_t T) {
+    PreparedGraph& P = ctx->prep;
+    hipStream_t s = ctx->stream;
+    const uint32_t V = P.V, nb = Vp / T;
+    fw_fill<<<2048, 256, 0, s>>>(D, Vp);
+    fw_scatter<<<V, 256, 0, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
+                                 ctx->g_lat.as<uint32_t>(), Vp, D);
+    for (uint32_t r = 0; r < nb; ++r) {
+        if (T == 64) {
+            fw_diag<64><<<1, 256, 0, s>>>(D, Vp, r);
+            if (nb > 1) {
+                fw_panels<64, 4><<<2 * (nb - 1), 256, 0, s>>>(D, Vp, r);
+                fw_rest<64, 4><<<(nb - 1) * (nb - 1), 256, 0, s>>>(D, Vp, r);
+            }
+        } else {
+            fw_diag<128><<<1, 256, 0, s>>>(D, Vp, r);
+            if (nb > 1) {
+                fw_panels<128, 8><<<2 * (nb - 1), 256, 0, s>>>(D, Vp, r);
+                fw_rest<128, 8><<<(nb - 1) * (nb - 1), 256, 0, s>>>(D, Vp, r);
+            }
+        }
+    }
+    SHD_HIP(hipGetLastError());
+    return SHD_OK;
+}
+
+shd_status fw_tight(shd_ctx* ctx, const uint32_t* D, uint32_t Vp, uint32_t* pbeg, uint32_t* pend,
+                    uint4* parcs, uint32_t* cursor) {
+    PreparedGraph& P = ctx->prep;
+    hipStream_t s = ctx->stream;
+    SHD_HIP(hipMemsetAsync(cursor, 0, 4, s));
+    fw_tight_arcs<<<P.V, 256, 0, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_arc16.as<uint4>(), D, Vp,
+                                      pbeg, pend, parcs, cursor);
+    SHD_HIP(hipGetLastError());
+    return SHD_OK;
+}
+
+}  // namespace shd

@@ -280,18 +280,24 @@ __global__ __launch_bounds__(256) void segment_sort_big(
 }
 
 // ==========================================================================================
-// Relay v2 (every path latency < 2^32 ns and every deliver - round_end < 2^32): 16-byte event
-// records {deliver - round_end, src host, seq - seq_base[src], packet index}.
-//   K1 relay_stamp_v2   lane per source host, sends in batches (below)
-//   K2 rocPRIM radix sort of the records by destination -- stable, LSD: the batch is in
-//      (source host, event id) order, so every destination's run stays in that order and no
-//      per-packet global atomic is needed
+// Narrow pipeline (every path latency < 2^32 ns and every deliver - round_end < 2^32): 16-byte
+// event records {deliver - round_end, src host, seq - seq_base[src], packet index}.
+//   K1 relay_stamp_v3   workgroup per kS3Hosts consecutive source hosts; their sends (one
+//                       contiguous range of the batch) stream through LDS in chunks:
+//                       coalesced loads, lane-per-packet path gathers, lane-per-host decisions
+//                       (only the RNG draws and event ids are sequential per host), coalesced
+//                       stores of status / record / destination key
+//   K2 rocPRIM onesweep radix sort of the records by destination -- stable: the batch is in
+//      (source host, event id) order, so every destination's run stays in that order
 //   K3 bucket_offsets   lower bound of every destination in the sorted keys
-//   K4 segment_sort_v3  stable rank sort of each destination run by deliver time
+//   K4 segment_sort_v4  wave per destination run: bitonic sort in registers of the unique key
+//                       (deliver offset << 32 | position in the run); ties on the deliver time
+//                       fall back to run order = (src host, event id) order
 // ==========================================================================================
-constexpr uint32_t kStampBatch = 8;
+constexpr uint32_t kS3Hosts = 64;      // source hosts per workgroup (one lane each in phase c)
+constexpr uint32_t kS3Chunk = 512;     // packets per LDS chunk (2 per thread)
 
-struct RelayArgs2 {
+struct RelayArgs3 {
     uint32_t n_hosts, n_nodes;
     const uint32_t* src_off;
     const uint64_t* send_time;
@@ -299,8 +305,7 @@ struct RelayArgs2 {
     const uint32_t* payload;
     const double* chance;
     const uint32_t* host_node;
-    const uint64_t* lat;
-    const float* loss;
+    const uint2* path;         // {latency ns (u32), packet loss bits} per node pair
     const uint64_t* rng;
     const uint64_t* next_id;
     uint64_t* rng_out;
@@ -313,91 +318,140 @@ struct RelayArgs2 {
     unsigned long long* red;   // [0] min deliver [1] min latency [2] n_sent [3] bad dst [4] wide
 };
 
-// Lane per source host (its RNG stream and event ids are sequential), kStampBatch sends at a
-// time: the batch's loads, its host_node[dst] gathers and its path gathers are each issued
-// together, so every lane keeps kStampBatch independent memory requests in flight.
-__global__ __launch_bounds__(256) void relay_stamp_v2(RelayArgs2 a) {
-    constexpr uint32_t R = kStampBatch;
-    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(256) void relay_stamp_v3(RelayArgs3 a) {
+    __shared__ uint64_t s_now[kS3Chunk];
+    __shared__ uint2 s_path[kS3Chunk];
+    __shared__ uint32_t s_pay[kS3Chunk];
+    __shared__ uint32_t s_own[kS3Chunk];    // owning host (local index)
+    __shared__ uint32_t s_doff[kS3Chunk];
+    __shared__ uint32_t s_seq[kS3Chunk];
+    __shared__ uint8_t s_st[kS3Chunk];
+    __shared__ uint32_t s_off[kS3Hosts + 1];
+    __shared__ uint32_t s_node[kS3Hosts];
+    const uint32_t tid = threadIdx.x, h0 = blockIdx.x * kS3Hosts;
+    const uint32_t nh = min(kS3Hosts, a.n_hosts - h0);
+    if (tid <= nh) s_off[tid] = a.src_off[h0 + tid];
+    if (tid < nh) s_node[tid] = a.host_node[h0 + tid];
+    __syncthreads();
+    const uint32_t p0 = s_off[0], p1 = s_off[nh];
+    const bool host_lane = tid < nh;
+    Xoshiro r{0, 0, 0, 0};
+    uint32_t hb = 0, he = 0, nsent = 0;
+    if (host_lane) {
+        const size_t h = h0 + tid;
+        r = Xoshiro{a.rng[4 * h], a.rng[4 * h + 1], a.rng[4 * h + 2], a.rng[4 * h + 3]};
+        hb = s_off[tid];
+        he = s_off[tid + 1];
+    }
     uint64_t min_d = ~0ull, min_l = ~0ull;
-    uint32_t nsent = 0;
     bool wide = false;
-    if (h < a.n_hosts) {
-        Xoshiro r{a.rng[4 * (size_t)h], a.rng[4 * (size_t)h + 1], a.rng[4 * (size_t)h + 2],
-                  a.rng[4 * (size_t)h + 3]};
-        const uint64_t id0 = a.next_id[h];
-        const uint32_t b0 = a.src_off[h], b1 = a.src_off[h + 1];
-        const size_t srow = (size_t)a.host_node[h] * a.n_nodes;
-        for (uint32_t i0 = b0; i0 < b1; i0 += R) {
-            uint64_t now[R];
-            uint32_t dst[R], pay[R], dn[R];
+    for (uint32_t c0 = p0; c0 < p1; c0 += kS3Chunk) {
+        const uint32_t c1 = min(c0 + kS3Chunk, p1);
+        // (a) owner map (lane per host) + coalesced loads of the chunk (lane per packet)
+        if (host_lane)
+            for (uint32_t i = max(hb, c0); i < min(he, c1); ++i) s_own[i - c0] = tid;
+        uint64_t now[2];
+        uint32_t dst[2], pay[2];
 #pragma unroll
-            for (uint32_t t = 0; t < R; ++t) {
-                const uint32_t i = i0 + t;
-                const bool v = i < b1;
-                now[t] = v ? a.send_time[i] : ~0ull;
-                dst[t] = v ? a.dst_host[i] : 0u;
-                pay[t] = v ? a.payload[i] : 0u;
-            }
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t i = c0 + tid + 256 * q;
+            const bool v = i < c1;
+            now[q] = v ? a.send_time[i] : ~0ull;
+            dst[q] = v ? a.dst_host[i] : 0u;
+            pay[q] = v ? a.payload[i] : 0u;
+        }
+        __syncthreads();
+        // (b) path gathers (lane per packet)
+        size_t pidx[2];
 #pragma unroll
-            for (uint32_t t = 0; t < R; ++t) {
-                if (dst[t] >= a.n_hosts && i0 + t < b1) {   // "No host ID for dest address"
-                    atomicMin(&a.red[3], (unsigned long long)(i0 + t));
-                    now[t] = ~0ull;
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t i = c0 + tid + 256 * q;
+            pidx[q] = 0;
+            if (i < c1) {
+                if (dst[q] >= a.n_hosts) {   // "No host ID for dest address" (worker.rs:350-355)
+                    atomicMin(&a.red[3], (unsigned long long)i);
+                    now[q] = ~0ull;
+                } else {
+                    pidx[q] = (size_t)s_node[s_own[i - c0]] * a.n_nodes + a.host_node[dst[q]];
+                    s_path[i - c0] = a.path[pidx[q]];
                 }
-                dn[t] = dst[t] < a.n_hosts ? a.host_node[dst[t]] : 0u;
-            }
-            uint64_t lat[R];
-            float loss[R];
-#pragma unroll
-            for (uint32_t t = 0; t < R; ++t) {
-                const bool v = now[t] < a.sim_end;
-                lat[t] = v ? a.lat[srow + dn[t]] : 0ull;
-                loss[t] = v ? a.loss[srow + dn[t]] : 0.0f;
-            }
-#pragma unroll
-            for (uint32_t t = 0; t < R; ++t) {
-                const uint32_t i = i0 + t;
-                if (i >= b1) break;
-                uint32_t st = kStSkipped;
-                if (now[t] < a.sim_end) {
-                    const double reliability = (double)one_minus(loss[t]);
-                    const double ch = a.chance ? a.chance[i] : r.gen_f64();
-                    if (!(now[t] < a.bootstrap_end) && ch >= reliability && pay[t] > 0) {
-                        st = kStDropped;
-                    } else {
-                        uint64_t tt = now[t] + lat[t];
-                        if (tt < a.round_end) tt = a.round_end;
-                        const uint64_t dd = tt - a.round_end;
-                        if ((dd >> 32) || (lat[t] >> 32)) wide = true;
-                        min_d = tt < min_d ? tt : min_d;
-                        min_l = lat[t] < min_l ? lat[t] : min_l;
-                        st = kStSent;
-                        a.rec[i] = make_uint4((uint32_t)dd, h, nsent++, i);
-                        if (a.counts) atomicAdd(&a.counts[srow + dn[t]], 1ull);
-                    }
-                }
-                a.status[i] = (uint8_t)st;
-                a.key[i] = st == kStSent ? dst[t] : a.n_hosts;
+                s_now[i - c0] = now[q];
+                s_pay[i - c0] = pay[q];
             }
         }
-        a.rng_out[4 * (size_t)h] = r.s0;
-        a.rng_out[4 * (size_t)h + 1] = r.s1;
-        a.rng_out[4 * (size_t)h + 2] = r.s2;
-        a.rng_out[4 * (size_t)h + 3] = r.s3;
-        a.next_id_out[h] = id0 + nsent;
+        __syncthreads();
+        // (c) decisions in send order (lane per host): RNG draw, drop rule, deliver stamp, id
+        if (host_lane) {
+            for (uint32_t i = max(hb, c0); i < min(he, c1); ++i) {
+                const uint32_t j = i - c0;
+                const uint64_t t0 = s_now[j];
+                uint8_t st = kStSkipped;
+                if (t0 < a.sim_end) {
+                    const uint2 pp = s_path[j];
+                    const double reliability = (double)one_minus(__uint_as_float(pp.y));
+                    const double ch = a.chance ? a.chance[i] : r.gen_f64();
+                    if (!(t0 < a.bootstrap_end) && ch >= reliability && s_pay[j] > 0) {
+                        st = kStDropped;
+                    } else {
+                        uint64_t tt = t0 + pp.x;
+                        if (tt < a.round_end) tt = a.round_end;
+                        const uint64_t dd = tt - a.round_end;
+                        wide |= (dd >> 32) != 0;
+                        min_d = tt < min_d ? tt : min_d;
+                        min_l = pp.x < min_l ? pp.x : min_l;
+                        s_doff[j] = (uint32_t)dd;
+                        s_seq[j] = nsent++;
+                        st = kStSent;
+                    }
+                }
+                s_st[j] = st;
+            }
+        }
+        __syncthreads();
+        // (d) coalesced stores (lane per packet)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint32_t i = c0 + tid + 256 * q;
+            if (i < c1) {
+                const uint32_t j = i - c0;
+                const uint8_t st = s_st[j];
+                a.status[i] = st;
+                a.key[i] = st == kStSent ? dst[q] : a.n_hosts;
+                if (st == kStSent) {
+                    a.rec[i] = make_uint4(s_doff[j], h0 + s_own[j], s_seq[j], i);
+                    if (a.counts) atomicAdd(&a.counts[pidx[q]], 1ull);
+                }
+            }
+        }
+        __syncthreads();   // the next chunk rewrites the LDS arrays
+    }
+    if (host_lane) {
+        const size_t h = h0 + tid;
+        a.rng_out[4 * h] = r.s0;
+        a.rng_out[4 * h + 1] = r.s1;
+        a.rng_out[4 * h + 2] = r.s2;
+        a.rng_out[4 * h + 3] = r.s3;
+        a.next_id_out[h] = a.next_id[h] + nsent;
     }
     min_d = wave_min_u64(min_d);
     min_l = wave_min_u64(min_l);
     uint64_t ns = nsent;
     for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
     const bool any_wide = __ballot(wide) != 0;
-    if ((threadIdx.x & 63) == 0) {
+    if ((tid & 63) == 0) {
         if (min_d != ~0ull) atomicMin(&a.red[0], (unsigned long long)min_d);
         if (min_l != ~0ull) atomicMin(&a.red[1], (unsigned long long)min_l);
         if (ns) atomicAdd(&a.red[2], (unsigned long long)ns);
         if (any_wide) atomicOr(&a.red[4], 1ull);
     }
+}
+
+// pack the routing table for the narrow pipeline: one 8-byte gather per packet
+__global__ __launch_bounds__(256) void pack_path(const uint64_t* __restrict__ lat,
+                                                 const float* __restrict__ loss, uint64_t nn,
+                                                 uint2* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nn) out[i] = make_uint2((uint32_t)lat[i], __float_as_uint(loss[i]));
 }
 
 // ev_off[d] = first position of destination d in the sorted keys (lower bound), d in [0, H]
@@ -421,20 +475,76 @@ __device__ __forceinline__ bool rec_less(const uint4& a, const uint4& b) {
 
 constexpr uint32_t kWaveSeg = 256;
 
-// One wave per destination run at a time (persistent waves walk the destinations): the run is
-// already in (src host, event id) order, so a STABLE sort by deliver offset gives EventQueue
-// order.  Rank sort: rank(i) = #{j : k_j < k_i} + #{j < i : k_j == k_i}; the keys are read from
-// LDS by broadcast, 4 at a time.  Runs longer than kWaveSeg go to the merge kernel.
-__global__ __launch_bounds__(256) void segment_sort_v3(
+// Bitonic sort of 64 * NPL keys held NPL per lane (element e = lane + 64 c), ascending.
+template <int NPL>
+__device__ __forceinline__ void wave_bitonic(uint64_t (&k)[NPL], uint32_t lane) {
+#pragma unroll
+    for (uint32_t kk = 2; kk <= 64u * NPL; kk <<= 1) {
+#pragma unroll
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {               // partner in another register of the same lane
+                const uint32_t cj = j / 64;
+#pragma unroll
+                for (int c = 0; c < NPL; ++c) {
+                    if ((c & cj) == 0) {
+                        const uint32_t e = lane + 64u * c;
+                        const bool asc = (e & kk) == 0;
+                        const uint64_t x = k[c], y = k[c | cj];
+                        const bool sw = asc ? (y < x) : (x < y);
+                        k[c] = sw ? y : x;
+                        k[c | cj] = sw ? x : y;
+                    }
+                }
+            } else {                     // partner lane ^ j
+#pragma unroll
+                for (int c = 0; c < NPL; ++c) {
+                    const uint32_t e = lane + 64u * c;
+                    const uint64_t o = __shfl_xor(k[c], (int)j);
+                    const bool lower = (lane & j) == 0;
+                    const bool asc = (e & kk) == 0;
+                    const bool take_min = lower == asc;
+                    k[c] = take_min ? (o < k[c] ? o : k[c]) : (o > k[c] ? o : k[c]);
+                }
+            }
+        }
+    }
+}
+
+template <int NPL>
+__device__ __forceinline__ void sort_run(uint32_t n, uint32_t b, uint32_t lane, const uint4* x,
+                                         uint64_t round_end, const uint64_t* __restrict__ seq_base,
+                                         uint64_t* __restrict__ ev_deliver,
+                                         uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq,
+                                         uint32_t* __restrict__ ev_pkt) {
+    uint64_t k[NPL];
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t e = lane + 64u * c;
+        k[c] = e < n ? (((uint64_t)x[e].x << 32) | e) : ~0ull;
+    }
+    wave_bitonic<NPL>(k, lane);
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t e = lane + 64u * c;
+        if (e < n) {
+            const uint4 r = x[(uint32_t)k[c]];
+            ev_deliver[b + e] = round_end + r.x;
+            ev_src[b + e] = r.y;
+            ev_seq[b + e] = seq_base[r.y] + r.z;
+            ev_pkt[b + e] = r.w;
+        }
+    }
+}
+
+// Persistent waves walk the destinations; runs longer than kWaveSeg go to the merge kernel.
+__global__ __launch_bounds__(256) void segment_sort_v4(
     uint32_t n_hosts, const uint32_t* __restrict__ ev_off, const uint4* __restrict__ brec,
     uint64_t round_end, const uint64_t* __restrict__ seq_base, uint64_t* __restrict__ ev_deliver,
     uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq, uint32_t* __restrict__ ev_pkt,
     uint32_t* __restrict__ big) {
-    __shared__ __attribute__((aligned(16))) uint32_t sk[4][kWaveSeg];
     __shared__ uint4 sr[4][kWaveSeg];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t nwaves = gridDim.x * 4;
-    uint32_t* k = sk[w];
     uint4* x = sr[w];
     for (uint32_t d = blockIdx.x * 4 + w; d < n_hosts; d += nwaves) {
         const uint32_t b = ev_off[d], n = ev_off[d + 1] - b;
@@ -443,57 +553,19 @@ __global__ __launch_bounds__(256) void segment_sort_v3(
             if (lane == 0) big[atomicAdd(&big[0], 1u) + 1] = d;
             continue;
         }
-        uint4 mine[kWaveSeg / 64];
-        uint32_t mk[kWaveSeg / 64];
-#pragma unroll
-        for (uint32_t c = 0; c < kWaveSeg / 64; ++c) {
-            const uint32_t i = lane + 64 * c;
-            if (i < n) {
-                mine[c] = brec[b + i];
-                mk[c] = mine[c].x;
-                k[i] = mk[c];
-            }
-        }
-        // pad to a multiple of 4 with +inf so the 4-wide key reads stay in bounds
-        if (lane < ((4 - (n & 3)) & 3)) k[n + lane] = ~0u;
+        for (uint32_t e = lane; e < n; e += 64) x[e] = brec[b + e];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint32_t rank[kWaveSeg / 64];
-#pragma unroll
-        for (uint32_t c = 0; c < kWaveSeg / 64; ++c) rank[c] = 0;
-        const uint4* k4 = reinterpret_cast<const uint4*>(k);
-        for (uint32_t j4 = 0; j4 < (n + 3) / 4; ++j4) {
-            const uint4 q = k4[j4];
-            const uint32_t kk[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-            for (uint32_t e = 0; e < 4; ++e) {
-                const uint32_t j = 4 * j4 + e;
-#pragma unroll
-                for (uint32_t c = 0; c < kWaveSeg / 64; ++c) {
-                    const uint32_t i = lane + 64 * c;
-                    rank[c] += (kk[e] < mk[c] || (kk[e] == mk[c] && j < i)) && j < n ? 1u : 0u;
-                }
-            }
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (uint32_t c = 0; c < kWaveSeg / 64; ++c)
-            if (lane + 64 * c < n) x[rank[c]] = mine[c];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint4 e = x[i];
-            ev_deliver[b + i] = round_end + e.x;
-            ev_src[b + i] = e.y;
-            ev_seq[b + i] = seq_base[e.y] + e.z;
-            ev_pkt[b + i] = e.w;
-        }
+        if (n <= 64)
+            sort_run<1>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
+        else if (n <= 128)
+            sort_run<2>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
+        else
+            sort_run<4>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
         __builtin_amdgcn_wave_barrier();
     }
 }
-
 // Runs longer than kWaveSeg: bottom-up merge passes by one workgroup in a
 // global scratch copy of the bucket (rank by binary search in the sibling run; keys unique).
 __global__ __launch_bounds__(256) void segment_sort_v2_big(
@@ -713,8 +785,28 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
     return SHD_OK;
 }
 
-// v2 pipeline: 16-byte records, chunked stamp, wave-per-destination sort; one host sync.
-static shd_status relay_device_v2(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+// rocPRIM onesweep by destination: RB bits per pass (the default for this key/value pair on
+// gfx950 is 8 -> three passes for 100k hosts; 9 bits covers 2^18 hosts in two passes)
+template <unsigned RB>
+using DstSortCfg = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 6>, rocprim::kernel_config<1024, 6>,
+                                        RB, rocprim::block_radix_rank_algorithm::match>>;
+
+template <unsigned RB>
+static shd_status sort_by_dst(RelayState& R, rocprim::double_buffer<uint32_t>& kb,
+                              rocprim::double_buffer<uint4>& vb, size_t n, uint32_t bits,
+                              hipStream_t s) {
+    size_t tmp_bytes = 0;
+    SHD_HIP((rocprim::radix_sort_pairs<DstSortCfg<RB>>(nullptr, tmp_bytes, kb, vb, n, 0u, bits, s)));
+    SHD_TRY(R.scan_tmp.ensure(tmp_bytes));
+    if (n) SHD_HIP((rocprim::radix_sort_pairs<DstSortCfg<RB>>(R.scan_tmp.p, tmp_bytes, kb, vb, n, 0u, bits, s)));
+    return SHD_OK;
+}
+
+// Narrow pipeline: K1 stamp, K2 radix sort by destination, K3 offsets, K4 per-run sort; one
+// host sync (for the round reductions).
+static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
                                   shd_relay_out* o) {
     RelayState& R = ctx->relay;
     hipStream_t s = ctx->stream;
@@ -729,7 +821,7 @@ static shd_status relay_device_v2(shd_ctx* ctx, const shd_batch* b, const shd_ro
     unsigned long long init[8] = {~0ull, ~0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
     SHD_HIP(hipMemcpyAsync(R.red.p, init, sizeof(init), hipMemcpyHostToDevice, s));
     SHD_HIP(hipMemsetAsync(R.ev_val2.p, 0, 4, s));
-    RelayArgs2 a{};
+    RelayArgs3 a{};
     a.n_hosts = H;
     a.n_nodes = R.n_nodes;
     a.src_off = b->src_off;
@@ -738,8 +830,7 @@ static shd_status relay_device_v2(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.payload = b->payload;
     a.chance = b->chance;
     a.host_node = R.host_node.as<uint32_t>();
-    a.lat = R.own_table ? R.lat.as<uint64_t>() : ctx->t_lat.as<uint64_t>();
-    a.loss = R.own_table ? R.loss.as<float>() : ctx->t_loss.as<float>();
+    a.path = R.path.as<uint2>();
     a.rng = R.rng.as<uint64_t>();
     a.next_id = R.next_id.as<uint64_t>();
     a.rng_out = R.rng2.as<uint64_t>();
@@ -752,24 +843,24 @@ static shd_status relay_device_v2(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.rec = R.rec.as<uint4>();
     a.key = R.ev_val.as<uint32_t>();
     a.red = R.red.as<unsigned long long>();
-    relay_stamp_v2<<<div_up(H, 256), 256, 0, s>>>(a);
+    relay_stamp_v3<<<div_up(H, kS3Hosts), 256, 0, s>>>(a);
     SHD_HIP(hipGetLastError());
     // stable LSD radix sort of the records by destination (keys <= H)
     uint32_t bits = 1;
     while (bits < 32 && (H >> bits) != 0) ++bits;
     rocprim::double_buffer<uint32_t> kb(R.ev_val.as<uint32_t>(), R.ev_key.as<uint32_t>());
     rocprim::double_buffer<uint4> vb(R.rec.as<uint4>(), R.brec.as<uint4>());
-    size_t tmp_bytes = 0;
-    SHD_HIP(rocprim::radix_sort_pairs(nullptr, tmp_bytes, kb, vb, (size_t)n, 0u, bits, s));
-    SHD_TRY(R.scan_tmp.ensure(tmp_bytes));
-    if (n) SHD_HIP(rocprim::radix_sort_pairs(R.scan_tmp.p, tmp_bytes, kb, vb, (size_t)n, 0u, bits, s));
+    const char* ev = std::getenv("SHD_RADIX_BITS");   // tuning override (results identical)
+    const uint32_t rb = ev && *ev ? (uint32_t)std::atoi(ev) : (bits > 16 && bits <= 18 ? 9u : 8u);
+    if (rb == 11) SHD_TRY(sort_by_dst<11>(R, kb, vb, (size_t)n, bits, s));
+    else if (rb == 9) SHD_TRY(sort_by_dst<9>(R, kb, vb, (size_t)n, bits, s));
+    else SHD_TRY(sort_by_dst<8>(R, kb, vb, (size_t)n, bits, s));
     uint4* sorted = vb.current();
     uint4* spare = sorted == R.rec.as<uint4>() ? R.brec.as<uint4>() : R.rec.as<uint4>();
     bucket_offsets<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(kb.current(), n, H, o->ev_off);
-    segment_sort_v3<<<std::min<uint32_t>(div_up(H, 4), (uint32_t)ctx->n_cu * 8), 256, 0, s>>>(
-                                                 H, o->ev_off, sorted, rd->round_end,
-                                                 R.next_id.as<uint64_t>(), o->ev_deliver, o->ev_src,
-                                                 o->ev_seq, o->ev_pkt, R.ev_val2.as<uint32_t>());
+    segment_sort_v4<<<std::min<uint32_t>(div_up(H, 4), (uint32_t)ctx->n_cu * 8), 256, 0, s>>>(
+        H, o->ev_off, sorted, rd->round_end, R.next_id.as<uint64_t>(), o->ev_deliver, o->ev_src,
+        o->ev_seq, o->ev_pkt, R.ev_val2.as<uint32_t>());
     segment_sort_v2_big<<<64, 256, 0, s>>>(R.ev_val2.as<uint32_t>(), o->ev_off, sorted,
                                            spare, rd->round_end, R.next_id.as<uint64_t>(),
                                            o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt);
@@ -790,7 +881,7 @@ static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round
     SHD_TRY(R.scan_tmp.ensure(64));
     bool v2 = R.table_narrow && !R.force_v1;
     if (v2) {
-        SHD_TRY(relay_device_v2(ctx, b, rd, o));
+        SHD_TRY(relay_device_v3(ctx, b, rd, o));
         if (R.red_host[4]) v2 = false;   // a deliver offset needs 64 bits: redo with v1
     }
     if (!v2) SHD_TRY(relay_device_v1(ctx, b, rd, o));
@@ -856,6 +947,13 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
         SHD_HIP(hipMemcpyAsync(&mx, ctx->g_aux.p, 8, hipMemcpyDeviceToHost, s));
         SHD_HIP(hipStreamSynchronize(s));
         R.table_narrow = (mx >> 32) == 0;
+        if (R.table_narrow) {   // packed {lat32, loss} table: one 8-byte gather per packet
+            const float* tp = R.own_table ? R.loss.as<float>() : ctx->t_loss.as<float>();
+            SHD_TRY(R.path.ensure(nn * 8));
+            pack_path<<<div_up(nn, 256), 256, 0, s>>>(tl, tp, nn, R.path.as<uint2>());
+            SHD_HIP(hipGetLastError());
+            SHD_HIP(hipStreamSynchronize(s));
+        }
     }
     {
         const char* v = std::getenv("SHD_RELAY_FORCE_V1");

@@ -80,7 +80,8 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     const float* __restrict__ diag_loss, uint64_t* __restrict__ out_lat,
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
-    unsigned long long* __restrict__ stats) {
+    unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
+    uint32_t seed_stride) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G, QCAP = 64;
     uint64_t* lab = reinterpret_cast<uint64_t*>(smem);
@@ -99,8 +100,16 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     const uint32_t src = used[row];
     const bool use_delta = delta != kLat32Inf;
 
+    // seed_lat (blocked path): labels start at (final latency, +inf loss) so only the loss
+    // part can still improve, and only through tight arcs
+    const uint32_t* seed = seed_lat ? seed_lat + (size_t)src * seed_stride : nullptr;
     for (uint32_t v = tid; v < V; v += BLOCK) {
-        lab[v] = kKeyInf;
+        uint64_t l0 = kKeyInf;
+        if (seed) {
+            const uint32_t d = seed[v];
+            if (d != kLat32Inf) l0 = ((uint64_t)d << 32) | 0xFFFFFFFFull;
+        }
+        lab[v] = l0;
         if (CACHE) rng[v] = make_uint2(abeg[v], aend[v]);
     }
     for (uint32_t w = tid; w < W; w += BLOCK) bits[w] = 0;
@@ -662,6 +671,7 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
                     ctx->g_dst.as<uint32_t>(), ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(),
                     ctx->g_arc16.as<uint4>(), H.loss.size());
             P.pruned_arcs = 0;
+            P.tight_arcs = 0;
         }
     }
     SHD_HIP(hipStreamSynchronize(s));
@@ -717,14 +727,16 @@ struct ArcView {
 
 template <int BLOCK, int G, bool CACHE>
 static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, size_t lds,
-                         uint64_t* d_lat, float* d_loss, uint32_t delta) {
+                         uint64_t* d_lat, float* d_loss, uint32_t delta, const uint32_t* seed,
+                         uint32_t seed_stride) {
     PreparedGraph& P = ctx->prep;
     constexpr int R = G >= 32 ? 2 : 4;   // arcs in flight per lane
     sssp_lds_group<BLOCK, G, R, CACHE><<<re - rb, BLOCK, lds, ctx->stream>>>(
         A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
         ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
-        delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr);
+        delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
+        seed, seed_stride);
 }
 
 static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
@@ -735,14 +747,15 @@ static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
 
 template <int BLOCK, bool CACHE>
 static void launch_by_degree(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint64_t* d_lat,
-                             float* d_loss, uint32_t delta, uint32_t G) {
+                             float* d_loss, uint32_t delta, uint32_t G, const uint32_t* seed,
+                             uint32_t ss) {
     const size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK, CACHE);
     switch (G) {
-        case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
-        case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
-        case 16: launch_group<BLOCK, 16, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
-        case 8: launch_group<BLOCK, 8, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
-        default: launch_group<BLOCK, 4, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta); break;
+        case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        case 16: launch_group<BLOCK, 16, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        case 8: launch_group<BLOCK, 8, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        default: launch_group<BLOCK, 4, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
     }
 }
 
@@ -752,7 +765,8 @@ static uint32_t env_u32(const char* name, uint32_t dflt) {
 }
 
 static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re,
-                           uint64_t* d_lat, float* d_loss, uint32_t delta, bool* ovf) {
+                           uint64_t* d_lat, float* d_loss, uint32_t delta, bool* ovf,
+                           const uint32_t* seed = nullptr, uint32_t ss = 0) {
     PreparedGraph& P = ctx->prep;
     hipStream_t s = ctx->stream;
     const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
@@ -770,14 +784,14 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
     const bool cache = sssp_lds_bytes(P.V, block, true) <= ctx->max_lds;
     SHD_HIP(hipEventRecord(ctx->ev[2], s));
     if (block == 1024) {
-        if (cache) launch_by_degree<1024, true>(ctx, A, rb, re, d_lat, d_loss, delta, G);
-        else launch_by_degree<1024, false>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+        if (cache) launch_by_degree<1024, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
+        else launch_by_degree<1024, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
     } else if (block == 512) {
-        if (cache) launch_by_degree<512, true>(ctx, A, rb, re, d_lat, d_loss, delta, G);
-        else launch_by_degree<512, false>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+        if (cache) launch_by_degree<512, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
+        else launch_by_degree<512, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
     } else {
-        if (cache) launch_by_degree<256, true>(ctx, A, rb, re, d_lat, d_loss, delta, G);
-        else launch_by_degree<256, false>(ctx, A, rb, re, d_lat, d_loss, delta, G);
+        if (cache) launch_by_degree<256, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
+        else launch_by_degree<256, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
     }
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(ctx->ev[3], s));
@@ -796,8 +810,49 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
     return SHD_OK;
 }
 
+shd_status fw_latency(shd_ctx* ctx, uint32_t* D, uint32_t Vp, uint32_t T);
+shd_status fw_tight(shd_ctx* ctx, const uint32_t* D, uint32_t Vp, uint32_t* pbeg, uint32_t* pend,
+                    uint4* parcs, uint32_t* cursor);
+
+// SHD_ALGO_BLOCKED (blocked.hip): latency closure by blocked min-plus, then the loss pass over
+// the globally tight arcs with labels seeded from the closure rows.
+static shd_status run_blocked(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d_lat,
+                              float* d_loss, bool* ovf) {
+    PreparedGraph& P = ctx->prep;
+    hipStream_t s = ctx->stream;
+    const uint32_t V = P.V;
+    const uint32_t T = env_u32("SHD_FW_TILE", V > 2048 ? 128 : 64) == 128 ? 128 : 64;
+    const uint32_t Vp = (V + T - 1) / T * T;
+    SHD_TRY(ctx->g_fw.ensure((size_t)Vp * Vp * 4));
+    SHD_TRY(ctx->g_prune_dst.ensure(std::max<uint64_t>(P.arcs, 1) * 16));
+    SHD_TRY(ctx->g_prune_cnt.ensure((size_t)V * 8 + 16));
+    uint32_t* D = ctx->g_fw.as<uint32_t>();
+    uint32_t* pbeg = ctx->g_prune_cnt.as<uint32_t>();
+    uint32_t* pend = pbeg + V;
+    uint32_t* cursor = pend + V;
+    SHD_HIP(hipEventRecord(ctx->ev[4], s));
+    SHD_TRY(fw_latency(ctx, D, Vp, T));
+    SHD_HIP(hipEventRecord(ctx->ev[5], s));
+    SHD_TRY(fw_tight(ctx, D, Vp, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor));
+    if (P.tight_arcs == 0) {   // the kept-arc count steers the lane-group width (once per graph)
+        uint32_t k = 0;
+        SHD_HIP(hipMemcpyAsync(&k, cursor, 4, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipStreamSynchronize(s));
+        P.tight_arcs = std::max<uint32_t>(k, 1);
+    }
+    ArcView A{pbeg, pend, ctx->g_prune_dst.as<uint4>(), P.tight_arcs};
+    SHD_TRY(run_sssp(ctx, A, rb, re, d_lat, d_loss, kLat32Inf, ovf, D, Vp));
+    float ms = 0;
+    SHD_HIP(hipEventSynchronize(ctx->ev[5]));
+    (void)hipEventElapsedTime(&ms, ctx->ev[4], ctx->ev[5]);
+    ctx->info.ms_minplus = ms;
+    ctx->info.arcs_kept = P.tight_arcs;
+    return SHD_OK;
+}
+
 constexpr uint32_t kPruneK = 32;
 constexpr uint32_t kPruneMaxV = 4096;
+constexpr uint32_t kBlockedMaxV = 16384;   // closure matrix <= 1 GiB
 
 // Dense arc matrix + k-nearest 2-hop prune over all V rows -> pruned arc lists (row stride V).
 static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
@@ -861,6 +916,26 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         return st;
     }
     const size_t lds = sssp_lds_bytes(P.V, 1024, false);
+    if (algo == SHD_ALGO_BLOCKED && P.narrow_arcs && lds <= ctx->max_lds && P.V <= kBlockedMaxV) {
+        bool ovf = false;
+        SHD_TRY(run_blocked(ctx, rb, re, d_lat, d_loss, &ovf));
+        ctx->info.algo_used = SHD_ALGO_BLOCKED;
+        SHD_HIP(hipEventRecord(ctx->ev[1], s));
+        SHD_HIP(hipEventSynchronize(ctx->ev[1]));
+        float ms = 0, ms_main = 0;
+        (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+        (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);
+        ctx->info.ms_total = ms;
+        ctx->info.ms_main = ms_main;
+        if (!ovf) {
+            // an INF closure entry is unreachable OR >= 2^32-1 ns: let the u64 path decide
+            const shd_status st = check_unreach(ctx, err);
+            if (st != SHD_ERR_UNREACHABLE) return st;
+            if (err) *err = shd_error{SHD_OK, 0, 0};
+        }
+        SHD_TRY(reset_flags(ctx));
+        return run_wide(ctx, rb, re, d_lat, d_loss, err);
+    }
     if (P.narrow_arcs && lds <= ctx->max_lds) {
         const bool dense = P.V <= kPruneMaxV && P.arcs * 8 >= (uint64_t)P.V * P.V;
         const bool prune = (algo == SHD_ALGO_PRUNED ||

@@ -156,3 +156,26 @@ def test_wide_latency_table_and_failed_round_keeps_state(engine):
     for k in ("deliver", "src", "seq", "pkt"):
         assert np.array_equal(getattr(r, "ev_" + k), o["events"][k]), k
     del synth
+
+
+@pytest.mark.parametrize("n_hosts", [300, 2000, 5000])
+def test_bucket_size_classes(engine, n_hosts):
+    """Destination runs of every size class of the per-run sort (<= 64, <= 128, <= 256 events
+    per destination, and longer runs on the merge path) against the C restatement."""
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    NN = 50
+    lat, loss, host_node, rng0, b = _c5_like(n_hosts, NN, 400_000, 13)
+    nid0 = np.arange(n_hosts, dtype=np.uint64) * np.uint64(7)
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss,
+                         rng0.copy(), nid0.copy(), 10**9 + 10**6, 10**12, 0)
+    rl = Relay(host_node, rng0, nid0, lat, loss, engine=engine)
+    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, 10**9 + 10**6, 10**12, 0)
+    ev = o["events"]
+    sizes = np.diff(ev["off"].astype(np.int64))
+    assert sizes.max() > 64
+    assert np.array_equal(r.status, o["status"])
+    assert np.array_equal(r.ev_off, ev["off"])
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(r, "ev_" + k), ev[k]), k
+    del synth

@@ -75,7 +75,8 @@ def test_random_graphs_vs_c_oracle(engine, seed, algo):
     _assert_table(t, lat, loss.view(np.uint32))
 
 
-def test_wide_latency_fallback(engine):
+@pytest.mark.parametrize("algo", [0, 4])
+def test_wide_latency_fallback(engine, algo):
     """Path latencies >= 2^32 ns take the u64 kernels; still bit-exact."""
     rng = np.random.default_rng(7)
     ids, s, d, l, p, directed = random_graph(rng, 60, 0.05, False)
@@ -84,7 +85,7 @@ def test_wide_latency_fallback(engine):
     code, lat, loss, _ = corc.routing(60, s, d, l, p, directed, used)
     assert code == "OK" and lat.max() > 2**32
     from shadow_amd.routing import NetworkGraph
-    t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine)
+    t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=algo)
     _assert_table(t, lat, loss.view(np.uint32))
     assert engine.last_info()["wide_latency"] == 1
 
@@ -117,7 +118,7 @@ def test_c3_rows_bit_exact(engine):
     code, lat, loss, _ = corc.routing(10_000, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
     assert code == "OK"
     g = engine_graph_from_edges(el)
-    for algo in (1, 3):
+    for algo in (1, 3, 4):
         t = g.compute_shortest_paths(used, engine, algo=algo, rows=(0, 64))
         _assert_table(t, lat[:64], loss[:64].view(np.uint32))
         t = g.compute_shortest_paths(used, engine, algo=algo, rows=(5000, 5100))
@@ -165,3 +166,23 @@ def test_negative_zero_loss_and_parallel_edges(engine, algo):
     from shadow_amd.routing import NetworkGraph
     t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=algo)
     _assert_table(t, lat, loss.view(np.uint32))
+
+
+def test_blocked_closure_padding_and_directed(engine):
+    """Blocked min-plus on sizes that are not tile multiples (padding rows/columns), directed
+    graphs, and both tile shapes; the closure time is reported."""
+    from shadow_amd.routing import NetworkGraph
+    for n, tile, directed in ((65, "64", True), (200, "128", False), (130, "64", False)):
+        rng = np.random.default_rng(n)
+        ids, s, d, l, p, _ = random_graph(rng, n, 0.08, directed, max_ms=20)
+        used = rng.permutation(n).astype(np.uint32)
+        code, lat, loss, _ = corc.routing(n, s, d, l, p, directed, used)
+        assert code == "OK"
+        os.environ["SHD_FW_TILE"] = tile
+        try:
+            t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=4)
+        finally:
+            del os.environ["SHD_FW_TILE"]
+        _assert_table(t, lat, loss.view(np.uint32))
+        info = engine.last_info()
+        assert info["algo_used"] == 4 and info["ms_minplus"] > 0

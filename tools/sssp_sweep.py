@@ -32,13 +32,14 @@ def one(cfg, algo, reps=5):
     for _ in range(reps):
         N.check(eng.lib.shd_routing_run(eng.ctx, algo, 0, rows, N.ptr(lat), N.ptr(loss), C.byref(err)), "run")
         info = eng.last_info()
-        ts.append((info["ms_main"], info["ms_total"]))
+        ts.append((info["ms_main"], info["ms_total"], info["ms_minplus"]))
     h = int(np.frombuffer(lat.cpu().numpy().tobytes(), np.uint8).astype(np.uint64).sum() * 31 +
             np.frombuffer(loss.cpu().numpy().tobytes(), np.uint8).astype(np.uint64).sum())
     ts = np.array(ts[1:])
     print(f"RESULT cfg={cfg} algo={algo} G={os.environ.get('SHD_SSSP_G','auto')} "
           f"block={os.environ.get('SHD_SSSP_BLOCK','256')} delta={os.environ.get('SHD_SSSP_DELTA','auto')} "
-          f"main_ms={ts[:,0].mean():.3f} total_ms={ts[:,1].mean():.3f} hash={h}", flush=True)
+          f"main_ms={ts[:,0].mean():.3f} total_ms={ts[:,1].mean():.3f} minplus_ms={ts[:,2].mean():.3f} "
+          f"kept={info['arcs_kept']} hash={h}", flush=True)
 
 
 if __name__ == "__main__":
