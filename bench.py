@@ -1,19 +1,28 @@
 #!/usr/bin/env python3
-"""Benchmark: APSP node-pairs/s (routing build, C2) + packets relayed/s per round (relay, C5).
+"""Benchmark: APSP node-pairs/s (routing build) + packets relayed/s per round (relay).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A step is one routing build of BASELINE config 2 (1000-node complete GML graph, 1000 used
-nodes) from the device-resident arc CSR to the full 1000 x 1000 (latency u64, loss f32) table
-resident in HBM.  At N > 1 the source rows are sharded over the ranks (no collective inside the
-SSSP) and the table is all-gathered over RCCL so every rank ends with the full table; the timed
-region includes that all-gather.  The relay leg times one round of config 5 (100k hosts, 10M
-packets) per step: stamp + loss draw + bucket + per-destination sort, inputs resident in HBM.
+Headline (``value``): one step is one routing build of BASELINE config 2 (1000-node complete GML
+graph, 1000 used nodes) from the device-resident arc CSR to the full 1000 x 1000 (latency u64,
+loss f32) table resident in HBM.  At N > 1 the source rows are sharded over the ranks (no
+collective inside the SSSP) and the table is all-gathered over RCCL so every rank ends with the
+full table; the timed region includes that all-gather (strong scaling: the graph is fixed).
+
+Side legs, each its own JSON object in the same line:
+  * ``relay`` -- C5: one round of 100k hosts / 10M packets per step (stamp + loss draw + bucket
+    by destination + per-destination sort), inputs resident in HBM.  At N > 1 the hosts are
+    sharded by id, every rank stamps its own sources, events are exchanged with one RCCL
+    all-to-all(v) and merged per destination (strong scaling: the round is fixed).
+  * ``c3`` (N = 1) -- the 10k-node sparse graph: label-correcting SSSP vs delta-stepping vs the
+    blocked min-plus APSP, all bit-identical; the blocked kernel's VALU roofline.
+  * ``c4`` -- the 50k-node graph, source rows sharded over the ranks, global-label SSSP
+    (delta-stepping) + RCCL all-gather of the 30 GB table.
 Rank 0 prints ONE JSON line.  Timing: barrier + device sync on both sides of exactly K steps,
-max over ranks.  The CPU baseline (rank 0, N = 1) times the C restatement of the reference
-(oracle/c) on the same workload.
+max over ranks.  The CPU baselines (rank 0, N = 1) time the C restatement of the reference
+(oracle/c) on bounded samples of the same workloads.
 """
 from __future__ import annotations
 
@@ -81,12 +90,9 @@ def load_pmc(name):
     return None
 
 
-def routing_leg(eng, world, rank, steps, warmup):
-    import torch
+def prepare(eng, el):
     from shadow_amd import _native as N
-    from shadow_amd import synth
     from shadow_amd.routing import NetworkGraph
-    el = synth.complete_graph(1000, 1)
     g = NetworkGraph(el.node_ids, el.src, el.dst, el.latency_ns, el.packet_loss, el.directed)
     n = g.n_nodes
     used = np.arange(n, dtype=np.uint32)
@@ -94,16 +100,24 @@ def routing_leg(eng, world, rank, steps, warmup):
     err = N.Error()
     N.check(eng.lib.shd_routing_prepare(eng.ctx, C.byref(cg), N.ptr(used), n, N.ROUTE_SHORTEST,
                                         C.byref(err)), "prepare", err)
+    return n
+
+
+def sharded_build(eng, world, rank, n, algo, steps, warmup, keep=False):
+    """Rows [rb, re) of an n x n build on this rank + all-gather; returns timings."""
+    import torch
+    from shadow_amd import _native as N
     per = (n + world - 1) // world
     rb, re = min(rank * per, n), min((rank + 1) * per, n)
     full_lat = torch.empty((world * per, n), dtype=torch.int64, device="cuda")
     full_loss = torch.empty((world * per, n), dtype=torch.float32, device="cuda")
     shard_lat = full_lat[rank * per:(rank + 1) * per]
     shard_loss = full_loss[rank * per:(rank + 1) * per]
+    err = N.Error()
 
     def step():
         if re > rb:
-            st = eng.lib.shd_routing_run(eng.ctx, N.ALGO_AUTO, rb, re, N.ptr(shard_lat), N.ptr(shard_loss),
+            st = eng.lib.shd_routing_run(eng.ctx, algo, rb, re, N.ptr(shard_lat), N.ptr(shard_loss),
                                          C.byref(err))
             N.check(st, "shd_routing_run", err)
         if world > 1:
@@ -114,33 +128,100 @@ def routing_leg(eng, world, rank, steps, warmup):
     for _ in range(warmup):
         step()
     barrier_sync(world)
-    main_ms = []
+    infos = []
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-        main_ms.append(eng.last_info()["ms_main"])
+        infos.append(eng.last_info())
     barrier_sync(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
-    info = eng.last_info()
-    arcs = info["arcs"]
-    kernel_ms = float(np.mean(main_ms)) if main_ms else 0.0
-    kernel_ms = max_over_ranks(kernel_ms, world)
-    ops_per_launch = 2.0 * (re - rb) * arcs          # one add + one min per arc per source row
+    out = dict(dt=dt, ms_per_step=dt / steps * 1e3, rows=re - rb, infos=infos)
+    if keep:
+        out["lat"] = full_lat[:n].cpu().numpy().view(np.uint64)
+        out["loss"] = full_loss[:n].cpu().numpy()
+    del full_lat, full_loss, shard_lat, shard_loss
+    torch.cuda.empty_cache()
+    return out
+
+
+def routing_leg(eng, world, rank, steps, warmup):
+    from shadow_amd import _native as N
+    from shadow_amd import synth
+    el = synth.complete_graph(1000, 1)
+    n = prepare(eng, el)
+    r = sharded_build(eng, world, rank, n, N.ALGO_AUTO, steps, warmup, keep=True)
+    info = r["infos"][-1]
+    kernel_ms = max_over_ranks(float(np.mean([i["ms_main"] for i in r["infos"]])), world)
+    ops_per_launch = 2.0 * r["rows"] * info["arcs"]      # one add + one min per arc per source row
     achieved = ops_per_launch / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
-    return dict(n=n, arcs=arcs, dt=dt, ms_per_step=dt / steps * 1e3, kernel_ms=kernel_ms,
-                achieved=achieved, algo=info["algo_used"], arcs_kept=info["arcs_kept"],
-                lat=full_lat[:n].cpu().numpy().view(np.uint64), loss=full_loss[:n].cpu().numpy(), el=el)
+    r.update(n=n, arcs=info["arcs"], kernel_ms=kernel_ms, achieved=achieved, algo=info["algo_used"],
+             arcs_kept=info["arcs_kept"], el=el)
+    return r
+
+
+def c3_leg(eng, reps=2):
+    """C3 (10k-node sparse, BA m=3): the three algorithms on the same rows, bit-identical."""
+    import torch
+    from shadow_amd import _native as N
+    from shadow_amd import synth
+    el = synth.barabasi_albert(10_000, 3, 2)
+    n = prepare(eng, el)
+    lat = torch.empty((n, n), dtype=torch.int64, device="cuda")
+    loss = torch.empty((n, n), dtype=torch.float32, device="cuda")
+    err = N.Error()
+    res, ref = {}, None
+    for name, algo in (("sssp", N.ALGO_SSSP), ("delta", N.ALGO_DELTA), ("blocked", N.ALGO_BLOCKED)):
+        infos = []
+        for _ in range(reps):
+            N.check(eng.lib.shd_routing_run(eng.ctx, algo, 0, n, N.ptr(lat), N.ptr(loss), C.byref(err)),
+                    "c3 run", err)
+            infos.append(eng.last_info())
+        i = infos[-1]
+        h = (int(lat.view(torch.int64).sum().item()), int(loss.view(torch.int32).to(torch.int64).sum().item()))
+        ref = ref or h
+        res[name] = dict(ms_total=i["ms_total"], ms_main=i["ms_main"], identical_to_sssp=h == ref)
+        if name == "blocked":
+            ops = 2.0 * n ** 3
+            ach = ops / (i["ms_minplus"] * 1e-3) / 1e12
+            res[name].update(ms_minplus=i["ms_minplus"], arcs_tight=i["arcs_kept"],
+                             roofline={"bound": "valu", "achieved": ach, "peak": VALU_PEAK_TOPS,
+                                       "unit": "Tops/s", "frac": ach / VALU_PEAK_TOPS,
+                                       "work": "2 V^3 int ops (add + min) of the min-plus closure"})
+    best = min(v["ms_total"] for v in res.values())
+    del lat, loss
+    torch.cuda.empty_cache()
+    return dict(workload="C3: 10k-node Barabasi-Albert m=3 + self-loops, all 10k rows",
+                nodes=n, arcs=int(eng.last_info()["arcs"]), node_pairs_per_s=n * n / (best * 1e-3),
+                algorithms=res)
+
+
+def c4_leg(eng, world, rank, steps):
+    from shadow_amd import _native as N
+    from shadow_amd import synth
+    el = synth.barabasi_albert(50_000, 4, 3)
+    n = prepare(eng, el)
+    r = sharded_build(eng, world, rank, n, N.ALGO_DELTA, steps, 0 if steps > 1 else 1)
+    kernel_ms = max_over_ranks(float(np.mean([i["ms_main"] for i in r["infos"]])), world)
+    return dict(workload="C4: 50k-node Barabasi-Albert m=4 + self-loops, all 50k rows, global-label "
+                         "delta-stepping SSSP, source rows sharded + RCCL all-gather of the table",
+                nodes=n, arcs=int(r["infos"][-1]["arcs"]), steps=steps, ms_per_build=r["ms_per_step"],
+                sssp_kernel_ms_per_rank=kernel_ms, value=n * n / (r["ms_per_step"] * 1e-3),
+                unit="node-pairs/s", scaling="strong")
+
+
+def relay_inputs():
+    from shadow_amd import synth
+    H, P = 100_000, 10_000_000
+    start, runahead = synth.SIM_START + 10**9, 10**6
+    b = synth.packet_batch(H, P, start, start + runahead, seed=4)
+    return H, P, start, runahead, b, synth.c5_host_nodes(H, 1000), synth.host_rng_states(H, 1)
 
 
 def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=False):
     import torch
     from shadow_amd import _native as N
-    from shadow_amd import synth
-    H, P = 100_000, 10_000_000
-    start, runahead = synth.SIM_START + 10**9, 10**6
-    b = synth.packet_batch(H, P, start, start + runahead, seed=4)
-    host_node = synth.c5_host_nodes(H, 1000)
-    rng0 = synth.host_rng_states(H, 1)
+    from shadow_amd import dist as D
+    H, P, start, runahead, b, host_node, rng0 = relay_inputs()
     nid0 = np.zeros(H, np.uint64)
     N.check(eng.lib.shd_relay_setup(eng.ctx, H, N.ptr(host_node), 1000, N.ptr(lat_table),
                                     N.ptr(loss_table), N.ptr(rng0), N.ptr(nid0)), "relay_setup")
@@ -148,37 +229,51 @@ def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=F
     # never called, and the CPU baseline does not keep them either -> off in both legs; the
     # cost with them on is reported separately (counters_on_ms_per_round)
     N.check(eng.lib.shd_relay_set_counters(eng.ctx, 1 if counters else 0), "set_counters")
-    dev = lambda a, dt: torch.from_numpy(a.view(dt)).cuda()  # noqa: E731
-    d_off = dev(b.src_off, np.int32)
-    d_time = dev(b.send_time, np.int64)
-    d_dst = dev(b.dst_host, np.int32)
-    d_pay = dev(b.payload, np.int32)
-    st = torch.empty(P, dtype=torch.uint8, device="cuda")
-    ev_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
-    ev_deliver = torch.empty(P, dtype=torch.int64, device="cuda")
-    ev_src = torch.empty(P, dtype=torch.int32, device="cuda")
-    ev_seq = torch.empty(P, dtype=torch.int64, device="cuda")
-    ev_pkt = torch.empty(P, dtype=torch.int32, device="cuda")
-    batch = N.Batch(P, N.ptr(d_off).value, N.ptr(d_time).value, N.ptr(d_dst).value,
-                    N.ptr(d_pay).value, None)
-    out = N.RelayOut(N.ptr(st).value, N.ptr(ev_off).value, N.ptr(ev_deliver).value,
-                     N.ptr(ev_src).value, N.ptr(ev_seq).value, N.ptr(ev_pkt).value, 0, 0, 0)
-    rd = N.Round(start + runahead, start + 10**12, 0)
+    dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()  # noqa: E731
+    rd = (start + runahead, start + 10**12, 0)
+    if world == 1:
+        d_off, d_time = dev(b.src_off, np.int32), dev(b.send_time, np.int64)
+        d_dst, d_pay = dev(b.dst_host, np.int32), dev(b.payload, np.int32)
+        st = torch.empty(P, dtype=torch.uint8, device="cuda")
+        ev_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+        ev_deliver = torch.empty(P, dtype=torch.int64, device="cuda")
+        ev_src = torch.empty(P, dtype=torch.int32, device="cuda")
+        ev_seq = torch.empty(P, dtype=torch.int64, device="cuda")
+        ev_pkt = torch.empty(P, dtype=torch.int32, device="cuda")
+        batch = N.Batch(P, N.ptr(d_off).value, N.ptr(d_time).value, N.ptr(d_dst).value,
+                        N.ptr(d_pay).value, None)
+        out = N.RelayOut(N.ptr(st).value, N.ptr(ev_off).value, N.ptr(ev_deliver).value,
+                         N.ptr(ev_src).value, N.ptr(ev_seq).value, N.ptr(ev_pkt).value, 0, 0, 0)
+        rnd = N.Round(*rd)
 
-    def step():
-        N.check(eng.lib.shd_relay_round_device(eng.ctx, C.byref(batch), C.byref(rd), C.byref(out)),
-                "relay_round_device")
+        def step():
+            N.check(eng.lib.shd_relay_round_device(eng.ctx, C.byref(batch), C.byref(rnd), C.byref(out)),
+                    "relay_round_device")
+            return out.n_sent
+    else:
+        # hosts sharded by id: this rank stamps its own sources; all-to-all + merge per round
+        lo, hi = D.host_shard(H, world, rank)
+        a, e = int(b.src_off[lo]), int(b.src_off[hi])
+        off = np.zeros(H + 1, np.uint32)
+        off[lo + 1:hi + 1] = b.src_off[lo + 1:hi + 1] - a
+        off[hi + 1:] = e - a
+        d_off, d_time = dev(off, np.int32), dev(b.send_time[a:e], np.int64)
+        d_dst, d_pay = dev(b.dst_host[a:e], np.int32), dev(b.payload[a:e], np.int32)
+        ops = D.DeviceOps(eng, torch.device("cuda", torch.cuda.current_device()))
+
+        def step():
+            return D.sharded_relay_round(ops, H, d_off, d_time, d_dst, d_pay, rd)["n_sent"]
 
     for _ in range(warmup):
         step()
     barrier_sync(world)
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        n_sent = step()
     barrier_sync(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
-    return dict(H=H, P=P, dt=dt, ms_per_step=dt / steps * 1e3, n_sent=out.n_sent, batch=b,
-                host_node=host_node, rng0=rng0)
+    return dict(H=H, P=P, dt=dt, ms_per_step=dt / steps * 1e3, n_sent=int(n_sent), batch=b,
+                host_node=host_node, rng0=rng0, start=start)
 
 
 def cpu_baseline_routing(el, budget_s=8.0):
@@ -200,17 +295,15 @@ def cpu_baseline_routing(el, budget_s=8.0):
 
 def cpu_baseline_relay(rl, lat_table, loss_table, budget_s=8.0):
     from oracle import corc
-    from shadow_amd import synth
     b = rl["batch"]
     threads = corc.max_threads()
-    start = synth.SIM_START + 10**9
     reps, t0 = 0, time.perf_counter()
     while True:
         rng = rl["rng0"].copy()
         nid = np.zeros(rl["H"], np.uint64)
         corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, rl["host_node"], lat_table,
-                         loss_table, rng, nid, start + 10**6, start + 10**12, 0, threads=threads,
-                         want_events=False)
+                         loss_table, rng, nid, rl["start"] + 10**6, rl["start"] + 10**12, 0,
+                         threads=threads, want_events=False)
         reps += 1
         if time.perf_counter() - t0 > budget_s or reps >= 5:
             break
@@ -226,8 +319,11 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--relay-steps", type=int, default=None)
+    ap.add_argument("--c4-steps", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-relay", action="store_true")
+    ap.add_argument("--no-c3", action="store_true")
+    ap.add_argument("--no-c4", action="store_true")
     args = ap.parse_args()
     world, rank, local = dist_setup(args.gpus)
     from shadow_amd.routing import Engine
@@ -248,8 +344,9 @@ def main():
         "roofline": {"bound": "valu", "achieved": r["achieved"], "peak": VALU_PEAK_TOPS,
                      "unit": "Tops/s", "frac": r["achieved"] / VALU_PEAK_TOPS,
                      "traffic": load_pmc("routing"),
-                     "kernel_ms": r["kernel_ms"],
-                     "work": "2 int ops (add, min) per arc relaxation per source row = 2*n*A"},
+                     "kernel": "sssp_lds_group", "kernel_ms": r["kernel_ms"],
+                     "work": "2 int ops (add, min) per arc relaxation per source row = 2*n*A "
+                             "(A = arcs before pruning: the reference's Dijkstra work)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, lat_cpu = cpu_baseline_routing(r["el"])
@@ -258,26 +355,33 @@ def main():
     if not args.no_relay:
         ks = args.relay_steps or max(3, args.steps // 2)
         rl = relay_leg(eng, world, rank, ks, min(args.warmup, 2), r["lat"], r["loss"])
-        rl_c = relay_leg(eng, world, rank, max(2, ks // 3), 1, r["lat"], r["loss"], counters=True)
         pv = ks * rl["P"] / rl["dt"]
         ms = rl["ms_per_step"]
         bytes_round = RELAY_BYTES_PER_PACKET * rl["P"] + RELAY_BYTES_PER_HOST * rl["H"]
         ach = bytes_round / (ms * 1e-3) / 1e9
         rel = {"metric": "packets relayed/s per round", "value": pv, "unit": "packets/s",
                "steps": ks, "ms_per_round": ms, "n_sent_last_round": int(rl["n_sent"]),
+               "scaling": "strong",
                "path_counters": "off (reference reads them only in the never-called "
                                 "log_packet_counts; CPU baseline keeps none)",
-               "counters_on_ms_per_round": rl_c["ms_per_step"],
                "config": {"workload": "C5: 100k hosts on the C2 table, 10M packets per round "
                                       "(src uniform, dst != src, 20% ACK / 60% 1448 B / 20% U[1,1448])",
                           "hosts": rl["H"], "packets": rl["P"],
-                          "parallelism": "replica per GPU" if world > 1 else "1 GPU"},
+                          "parallelism": (f"hosts sharded x{world}, RCCL all-to-all(v) + device "
+                                          f"k-way merge") if world > 1 else "1 GPU"},
                "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ach / HBM_PEAK_GBS, "traffic": load_pmc("relay"),
                             "work": "84 B/packet + 80 B/host algorithmic (SURVEY 8(d)), whole round"}}
+        if world == 1:
+            rl_c = relay_leg(eng, world, rank, max(2, ks // 3), 1, r["lat"], r["loss"], counters=True)
+            rel["counters_on_ms_per_round"] = rl_c["ms_per_step"]
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             rel["cpu_baseline"] = cpu_baseline_relay(rl, r["lat"], r["loss"])
         res["relay"] = rel
+    if world == 1 and not args.no_c3:
+        res["c3"] = c3_leg(eng)
+    if not args.no_c4:
+        res["c4"] = c4_leg(eng, world, rank, args.c4_steps)
     if rank == 0:
         print(json.dumps(res), flush=True)
     eng.close()

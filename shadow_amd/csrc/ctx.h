@@ -50,7 +50,7 @@ struct RelayState {
     bool count_on = true;       // per-path packet counters (RoutingInfo::increment_packet_count)
     bool last_v2 = false;
     unsigned long long red_host[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    DevBuf host_node, lat, loss, path, rng, next_id, rng2, next_id2, counts;
+    DevBuf host_node, order, lat, loss, path, rng, next_id, rng2, next_id2, counts;
     // per-round scratch
     DevBuf pk_off, pk_time, pk_dst, pk_pay, pk_chance, st, ev_key, ev_key2, ev_val, ev_val2,
         ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, scan_tmp, red, rec, brec, tmp;
@@ -100,7 +100,7 @@ struct shd_ctx {
     shd::DevBuf d_es, d_ed, d_el, d_ep, d_col;   // direct mode edge arrays
     // routing scratch
     shd::DevBuf g_off, g_dst, g_lat, g_q, g_lat64, g_used, g_diag_lat, g_diag_loss, g_flags,
-        g_dense, g_prune_dst, g_prune_cnt, g_labels, g_aux, g_arc16, g_fw;
+        g_dense, g_prune_dst, g_prune_cnt, g_labels, g_aux, g_arc16, g_fw, g_glab;
 
     shd::RelayState relay;
 };

@@ -19,6 +19,7 @@
 //   K3 relay_scatter   one lane per packet scatters its event into the destination bucket.
 //   K4 segment_sort    one workgroup per destination sorts its bucket by the full event key
 //                      (unique), so the atomic slot order never shows in the output.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -305,6 +306,7 @@ struct RelayArgs3 {
     const uint32_t* payload;
     const double* chance;
     const uint32_t* host_node;
+    const uint32_t* order;     // host ids sorted by host_node (workgroup -> hosts)
     const uint2* path;         // {latency ns (u32), packet loss bits} per node pair
     const uint64_t* rng;
     const uint64_t* next_id;
@@ -316,129 +318,206 @@ struct RelayArgs3 {
     uint4* rec;          // per packet (valid when SENT)
     uint32_t* key;       // per packet: destination host if SENT, else n_hosts (sorts last)
     unsigned long long* red;   // [0] min deliver [1] min latency [2] n_sent [3] bad dst [4] wide
+    unsigned long long* prof;  // nullable: phase timings (SHD_RELAY_PROF=1, tuning only)
 };
 
+// K1: a workgroup owns kS3Hosts source hosts, taken in source-node order (R.order: hosts sorted
+// by host_node at setup), so a workgroup's path gathers stay inside a few rows of the table and
+// hit L2.  Chunk k holds the slice [k*S, (k+1)*S) of every host's sends (S = kS3Slice); 8
+// consecutive lanes own the 8 sends of one host in the slice (coalesced loads and stores).
+//   (ab) lane per send: raw loads (prefetched one chunk ahead), path gathers, skip test; a
+//        ballot gives each host its mask of sends that draw (now < sim_end)
+//   (c1) lane per host: the host's Xoshiro256++ stream fills the draws of the masked sends in
+//        send order -- the only sequential work
+//   (c2) lane per send: drop rule, deliver stamp, event id (ballot prefix inside the host's
+//        8-lane group plus the host's running count), stores
+constexpr uint32_t kS3Slice = kS3Chunk / kS3Hosts;   // sends per host per chunk (8)
+constexpr uint32_t kS3Lds = kS3Slice * (kS3Hosts + 1);
+
 __global__ __launch_bounds__(256) void relay_stamp_v3(RelayArgs3 a) {
-    __shared__ uint64_t s_now[kS3Chunk];
-    __shared__ uint2 s_path[kS3Chunk];
-    __shared__ uint32_t s_pay[kS3Chunk];
-    __shared__ uint32_t s_own[kS3Chunk];    // owning host (local index)
-    __shared__ uint32_t s_doff[kS3Chunk];
-    __shared__ uint32_t s_seq[kS3Chunk];
-    __shared__ uint8_t s_st[kS3Chunk];
-    __shared__ uint32_t s_off[kS3Hosts + 1];
-    __shared__ uint32_t s_node[kS3Hosts];
-    const uint32_t tid = threadIdx.x, h0 = blockIdx.x * kS3Hosts;
+    constexpr uint32_t SPT = kS3Chunk / 256;          // sends per thread per chunk
+    __shared__ uint64_t s_draw[kS3Lds];               // raw generator outputs, slot j*65 + host
+    __shared__ uint32_t s_host[kS3Hosts], s_beg[kS3Hosts], s_len[kS3Hosts], s_node[kS3Hosts];
+    __shared__ uint32_t s_mask[kS3Hosts], s_nsent[kS3Hosts];
+    __shared__ uint32_t s_maxlen;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t h0 = blockIdx.x * kS3Hosts;
     const uint32_t nh = min(kS3Hosts, a.n_hosts - h0);
-    if (tid <= nh) s_off[tid] = a.src_off[h0 + tid];
-    if (tid < nh) s_node[tid] = a.host_node[h0 + tid];
+    if (tid == 0) s_maxlen = 0;
     __syncthreads();
-    const uint32_t p0 = s_off[0], p1 = s_off[nh];
+    if (tid < nh) {
+        const uint32_t h = a.order[h0 + tid];
+        const uint32_t b = a.src_off[h];
+        s_host[tid] = h;
+        s_beg[tid] = b;
+        s_len[tid] = a.src_off[h + 1] - b;
+        s_node[tid] = a.host_node[h];
+        s_nsent[tid] = 0;
+        atomicMax(&s_maxlen, s_len[tid]);
+    }
     const bool host_lane = tid < nh;
     Xoshiro r{0, 0, 0, 0};
-    uint32_t hb = 0, he = 0, nsent = 0;
-    if (host_lane) {
-        const size_t h = h0 + tid;
+    if (host_lane && !a.chance) {
+        const size_t h = a.order[h0 + tid];
         r = Xoshiro{a.rng[4 * h], a.rng[4 * h + 1], a.rng[4 * h + 2], a.rng[4 * h + 3]};
-        hb = s_off[tid];
-        he = s_off[tid + 1];
     }
-    uint64_t min_d = ~0ull, min_l = ~0ull;
-    bool wide = false;
-    for (uint32_t c0 = p0; c0 < p1; c0 += kS3Chunk) {
-        const uint32_t c1 = min(c0 + kS3Chunk, p1);
-        // (a) owner map (lane per host) + coalesced loads of the chunk (lane per packet)
-        if (host_lane)
-            for (uint32_t i = max(hb, c0); i < min(he, c1); ++i) s_own[i - c0] = tid;
-        uint64_t now[2];
-        uint32_t dst[2], pay[2];
+    __syncthreads();
+    const uint32_t n_chunks = (s_maxlen + kS3Slice - 1) / kS3Slice;
+    uint32_t hl[SPT], jj[SPT], len[SPT], base[SPT], ls[SPT];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t i = c0 + tid + 256 * q;
-            const bool v = i < c1;
+    for (uint32_t q = 0; q < SPT; ++q) {
+        const uint32_t g = tid + 256 * q;
+        hl[q] = g / kS3Slice;
+        jj[q] = g % kS3Slice;
+        ls[q] = jj[q] * (kS3Hosts + 1) + hl[q];
+        const bool hv = hl[q] < nh;
+        base[q] = hv ? s_beg[hl[q]] : 0u;
+        len[q] = hv ? s_len[hl[q]] : 0u;
+    }
+    uint64_t now[SPT];
+    uint32_t dst[SPT], pay[SPT];
+    auto load_raw = [&](uint32_t k) {
+#pragma unroll
+        for (uint32_t q = 0; q < SPT; ++q) {
+            const uint32_t t = k * kS3Slice + jj[q];
+            const bool v = t < len[q];
+            const uint32_t i = base[q] + t;
             now[q] = v ? a.send_time[i] : ~0ull;
             dst[q] = v ? a.dst_host[i] : 0u;
             pay[q] = v ? a.payload[i] : 0u;
         }
-        __syncthreads();
-        // (b) path gathers (lane per packet)
-        size_t pidx[2];
+    };
+    // SHD_RELAY_PROF=1: per-phase s_memtime totals of thread 0 (tuning only)
+    uint64_t tp0 = a.prof ? __builtin_amdgcn_s_memtime() : 0, tab = 0, tc = 0, td = 0, tt0 = tp0;
+    if (n_chunks) load_raw(0);
+    uint64_t min_d = ~0ull, min_l = ~0ull;
+    bool wide = false;
+    const uint32_t gshift = lane & ~(kS3Slice - 1);    // first lane of this lane's host group
+    for (uint32_t k = 0; k < n_chunks; ++k) {
+        // (ab) path gathers and the draw mask (lane per send)
+        uint2 pp[SPT];
+        size_t pidx[SPT];
+        bool valid[SPT], draws[SPT];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t i = c0 + tid + 256 * q;
+        for (uint32_t q = 0; q < SPT; ++q) {
+            const uint32_t t = k * kS3Slice + jj[q];
+            valid[q] = t < len[q];
             pidx[q] = 0;
-            if (i < c1) {
-                if (dst[q] >= a.n_hosts) {   // "No host ID for dest address" (worker.rs:350-355)
-                    atomicMin(&a.red[3], (unsigned long long)i);
-                    now[q] = ~0ull;
-                } else {
-                    pidx[q] = (size_t)s_node[s_own[i - c0]] * a.n_nodes + a.host_node[dst[q]];
-                    s_path[i - c0] = a.path[pidx[q]];
-                }
-                s_now[i - c0] = now[q];
-                s_pay[i - c0] = pay[q];
+            pp[q] = make_uint2(0u, 0u);
+            if (valid[q] && dst[q] >= a.n_hosts) {   // "No host ID for dest address" (worker.rs:350-355)
+                atomicMin(&a.red[3], (unsigned long long)(base[q] + t));
+                now[q] = ~0ull;                       // the round fails; no draw
+            } else if (valid[q]) {
+                pidx[q] = (size_t)s_node[hl[q]] * a.n_nodes + a.host_node[dst[q]];
+                pp[q] = a.path[pidx[q]];
+            }
+            draws[q] = valid[q] && now[q] < a.sim_end;
+            const uint32_t gm = (uint32_t)(__ballot(draws[q]) >> gshift) & ((1u << kS3Slice) - 1u);
+            if (jj[q] == 0) s_mask[hl[q]] = gm;
+        }
+        __syncthreads();
+        if (a.prof) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            tab += t1 - tp0;
+            tp0 = t1;
+        }
+        // (c1) the host's generator, in send order, for the sends that draw (lane per host)
+        if (host_lane && !a.chance) {
+            uint32_t m = s_mask[tid];
+            while (m) {
+                const uint32_t j = __builtin_ctz(m);
+                m &= m - 1;
+                s_draw[j * (kS3Hosts + 1) + tid] = r.next();
             }
         }
         __syncthreads();
-        // (c) decisions in send order (lane per host): RNG draw, drop rule, deliver stamp, id
-        if (host_lane) {
-            for (uint32_t i = max(hb, c0); i < min(he, c1); ++i) {
-                const uint32_t j = i - c0;
-                const uint64_t t0 = s_now[j];
-                uint8_t st = kStSkipped;
-                if (t0 < a.sim_end) {
-                    const uint2 pp = s_path[j];
-                    const double reliability = (double)one_minus(__uint_as_float(pp.y));
-                    const double ch = a.chance ? a.chance[i] : r.gen_f64();
-                    if (!(t0 < a.bootstrap_end) && ch >= reliability && s_pay[j] > 0) {
-                        st = kStDropped;
-                    } else {
-                        uint64_t tt = t0 + pp.x;
-                        if (tt < a.round_end) tt = a.round_end;
-                        const uint64_t dd = tt - a.round_end;
-                        wide |= (dd >> 32) != 0;
-                        min_d = tt < min_d ? tt : min_d;
-                        min_l = pp.x < min_l ? pp.x : min_l;
-                        s_doff[j] = (uint32_t)dd;
-                        s_seq[j] = nsent++;
-                        st = kStSent;
-                    }
-                }
-                s_st[j] = st;
-            }
+        if (a.prof) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            tc += t1 - tp0;
+            tp0 = t1;
         }
-        __syncthreads();
-        // (d) coalesced stores (lane per packet)
+        uint64_t now_cur[SPT];
+        uint32_t dst_cur[SPT], pay_cur[SPT];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t i = c0 + tid + 256 * q;
-            if (i < c1) {
-                const uint32_t j = i - c0;
-                const uint8_t st = s_st[j];
+        for (uint32_t q = 0; q < SPT; ++q) {
+            now_cur[q] = now[q];
+            dst_cur[q] = dst[q];
+            pay_cur[q] = pay[q];
+        }
+        if (k + 1 < n_chunks) load_raw(k + 1);   // in flight during the decisions and stores
+        // (c2) decisions, event ids, stores (lane per send)
+#pragma unroll
+        for (uint32_t q = 0; q < SPT; ++q) {
+            const uint32_t t = k * kS3Slice + jj[q];
+            const uint32_t i = base[q] + t;
+            uint8_t st = kStSkipped;
+            uint32_t doff = 0;
+            if (draws[q]) {
+                const double reliability = (double)one_minus(__uint_as_float(pp[q].y));
+                const double ch = a.chance ? a.chance[i]
+                                           : (double)(s_draw[ls[q]] >> 11) * (1.0 / 9007199254740992.0);
+                if (!(now_cur[q] < a.bootstrap_end) && ch >= reliability && pay_cur[q] > 0) {
+                    st = kStDropped;
+                } else {
+                    uint64_t tt = now_cur[q] + pp[q].x;
+                    if (tt < a.round_end) tt = a.round_end;
+                    const uint64_t dd = tt - a.round_end;
+                    wide |= (dd >> 32) != 0;
+                    min_d = tt < min_d ? tt : min_d;
+                    min_l = pp[q].x < min_l ? pp[q].x : min_l;
+                    doff = (uint32_t)dd;
+                    st = kStSent;
+                }
+            }
+            // event id: the host's running count + sent sends before this one in its group
+            const uint64_t sm = __ballot(st == kStSent);
+            const uint32_t gm = (uint32_t)(sm >> gshift) & ((1u << kS3Slice) - 1u);
+            const uint32_t below = __popc(gm & ((1u << (lane - gshift)) - 1u));
+            const uint32_t run = hl[q] < nh ? s_nsent[hl[q]] : 0u;
+            if (valid[q]) {
                 a.status[i] = st;
-                a.key[i] = st == kStSent ? dst[q] : a.n_hosts;
+                a.key[i] = st == kStSent ? dst_cur[q] : a.n_hosts;
                 if (st == kStSent) {
-                    a.rec[i] = make_uint4(s_doff[j], h0 + s_own[j], s_seq[j], i);
+                    a.rec[i] = make_uint4(doff, s_host[hl[q]], run + below, i);
                     if (a.counts) atomicAdd(&a.counts[pidx[q]], 1ull);
                 }
             }
+            if (jj[q] == 0 && hl[q] < nh) s_nsent[hl[q]] = run + __popc(gm);
         }
-        __syncthreads();   // the next chunk rewrites the LDS arrays
+        if (a.prof) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            td += t1 - tp0;
+            tp0 = t1;
+        }
     }
+    __syncthreads();
+    if (a.prof && tid == 0) {
+        atomicAdd(&a.prof[0], (unsigned long long)tab);
+        atomicAdd(&a.prof[1], (unsigned long long)tc);
+        atomicAdd(&a.prof[2], (unsigned long long)td);
+        atomicAdd(&a.prof[3], (unsigned long long)n_chunks);
+        atomicAdd(&a.prof[4], 1ull);
+        atomicAdd(&a.prof[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - tt0));
+    }
+    uint64_t ns = 0;
     if (host_lane) {
-        const size_t h = h0 + tid;
-        a.rng_out[4 * h] = r.s0;
-        a.rng_out[4 * h + 1] = r.s1;
-        a.rng_out[4 * h + 2] = r.s2;
-        a.rng_out[4 * h + 3] = r.s3;
-        a.next_id_out[h] = a.next_id[h] + nsent;
+        const size_t h = s_host[tid];
+        if (!a.chance) {
+            a.rng_out[4 * h] = r.s0;
+            a.rng_out[4 * h + 1] = r.s1;
+            a.rng_out[4 * h + 2] = r.s2;
+            a.rng_out[4 * h + 3] = r.s3;
+        } else {
+            for (int w = 0; w < 4; ++w) a.rng_out[4 * h + w] = a.rng[4 * h + w];
+        }
+        ns = s_nsent[tid];
+        a.next_id_out[h] = a.next_id[h] + ns;
     }
     min_d = wave_min_u64(min_d);
     min_l = wave_min_u64(min_l);
-    uint64_t ns = nsent;
     for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
     const bool any_wide = __ballot(wide) != 0;
-    if ((tid & 63) == 0) {
+    if (lane == 0) {
         if (min_d != ~0ull) atomicMin(&a.red[0], (unsigned long long)min_d);
         if (min_l != ~0ull) atomicMin(&a.red[1], (unsigned long long)min_l);
         if (ns) atomicAdd(&a.red[2], (unsigned long long)ns);
@@ -536,6 +615,96 @@ __device__ __forceinline__ void sort_run(uint32_t n, uint32_t b, uint32_t lane, 
     }
 }
 
+// xor lane exchange inside a wave for a compile-time distance (the bitonic loops below are fully
+// unrolled, so j folds): DPP quad_perm for 1 and 2, DPP row_ror:8 for 8, ds_swizzle (bitmask
+// mode) for 4, v_permlane16_swap / v_permlane32_swap (gfx950) for 16 and 32.
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, uint32_t j, uint32_t lane) {
+    switch (j) {
+        case 1: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+        case 2: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+        case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (4 << 10) | 0x1F);
+        case 8: return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);
+        case 16: {
+            const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+            return (lane & 16) ? r[0] : r[1];
+        }
+        default: {
+            const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            return (lane & 32) ? r[0] : r[1];
+        }
+    }
+}
+
+// Bitonic sort of 64 * NPL 32-bit keys held NPL per lane (element e = lane + 64 c), ascending.
+template <int NPL>
+__device__ __forceinline__ void wave_bitonic32(uint32_t (&k)[NPL], uint32_t lane) {
+#pragma unroll
+    for (uint32_t kk = 2; kk <= 64u * NPL; kk <<= 1) {
+#pragma unroll
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+                const uint32_t cj = j / 64;
+#pragma unroll
+                for (int c = 0; c < NPL; ++c) {
+                    if ((c & cj) == 0) {
+                        const bool asc = ((lane + 64u * c) & kk) == 0;
+                        const uint32_t x = k[c], y = k[c | cj];
+                        k[c] = asc ? min(x, y) : max(x, y);
+                        k[c | cj] = asc ? max(x, y) : min(x, y);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < NPL; ++c) {
+                    const uint32_t o = xor_lane(k[c], j, lane);
+                    const bool take_min = ((lane & j) == 0) == (((lane + 64u * c) & kk) == 0);
+                    k[c] = take_min ? min(o, k[c]) : max(o, k[c]);
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) v = min(v, xor_lane(v, o, lane));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) v = max(v, xor_lane(v, o, lane));
+    return v;
+}
+
+// The run's deliver offsets usually span far less than 2^32 ns: then (offset - min) and the
+// position in the run fit one 32-bit key (PB position bits), which halves every exchange.
+template <int NPL, int PB>
+__device__ __forceinline__ void sort_run32(uint32_t n, uint32_t b, uint32_t lane, const uint4* x,
+                                           uint32_t dmin, uint64_t round_end,
+                                           const uint64_t* __restrict__ seq_base,
+                                           uint64_t* __restrict__ ev_deliver,
+                                           uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq,
+                                           uint32_t* __restrict__ ev_pkt) {
+    uint32_t k[NPL];
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t e = lane + 64u * c;
+        k[c] = e < n ? ((x[e].x - dmin) << PB) | e : ~0u;
+    }
+    wave_bitonic32<NPL>(k, lane);
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t e = lane + 64u * c;
+        if (e < n) {
+            const uint4 r = x[k[c] & ((1u << PB) - 1u)];
+            ev_deliver[b + e] = round_end + r.x;
+            ev_src[b + e] = r.y;
+            ev_seq[b + e] = seq_base[r.y] + r.z;
+            ev_pkt[b + e] = r.w;
+        }
+    }
+}
+
 // Persistent waves walk the destinations; runs longer than kWaveSeg go to the merge kernel.
 __global__ __launch_bounds__(256) void segment_sort_v4(
     uint32_t n_hosts, const uint32_t* __restrict__ ev_off, const uint4* __restrict__ brec,
@@ -553,16 +722,35 @@ __global__ __launch_bounds__(256) void segment_sort_v4(
             if (lane == 0) big[atomicAdd(&big[0], 1u) + 1] = d;
             continue;
         }
-        for (uint32_t e = lane; e < n; e += 64) x[e] = brec[b + e];
+        uint32_t lo = ~0u, hi = 0;
+        for (uint32_t e = lane; e < n; e += 64) {
+            const uint4 v = brec[b + e];
+            x[e] = v;
+            lo = min(lo, v.x);
+            hi = max(hi, v.x);
+        }
+        lo = wave_min_u32(lo, lane);
+        const uint32_t span = wave_max_u32(hi, lane) - lo;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (n <= 64)
-            sort_run<1>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
-        else if (n <= 128)
-            sort_run<2>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
-        else
-            sort_run<4>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
+        // 32-bit keys (offset - min) << PB | position when the span leaves room for PB bits
+        if (n <= 64) {
+            if (span < (1u << 26) - 1u)
+                sort_run32<1, 6>(n, b, lane, x, lo, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
+            else
+                sort_run<1>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
+        } else if (n <= 128) {
+            if (span < (1u << 25) - 1u)
+                sort_run32<2, 7>(n, b, lane, x, lo, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
+            else
+                sort_run<2>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
+        } else {
+            if (span < (1u << 24) - 1u)
+                sort_run32<4, 8>(n, b, lane, x, lo, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
+            else
+                sort_run<4>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
+        }
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -831,6 +1019,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.chance = b->chance;
     a.host_node = R.host_node.as<uint32_t>();
     a.path = R.path.as<uint2>();
+    a.order = R.order.as<uint32_t>();
     a.rng = R.rng.as<uint64_t>();
     a.next_id = R.next_id.as<uint64_t>();
     a.rng_out = R.rng2.as<uint64_t>();
@@ -843,8 +1032,23 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.rec = R.rec.as<uint4>();
     a.key = R.ev_val.as<uint32_t>();
     a.red = R.red.as<unsigned long long>();
+    const char* pe = std::getenv("SHD_RELAY_PROF");
+    const bool prof = pe && *pe == '1';
+    if (prof) {
+        SHD_TRY(R.tmp.ensure(64));
+        SHD_HIP(hipMemsetAsync(R.tmp.p, 0, 64, s));
+        a.prof = R.tmp.as<unsigned long long>();
+    }
     relay_stamp_v3<<<div_up(H, kS3Hosts), 256, 0, s>>>(a);
     SHD_HIP(hipGetLastError());
+    if (prof) {
+        unsigned long long p[6];
+        SHD_HIP(hipMemcpyAsync(p, R.tmp.p, 48, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipStreamSynchronize(s));
+        std::fprintf(stderr, "relay_stamp_v3 prof: WGs=%llu chunks/WG=%.1f  per chunk: ab=%.0f c=%.0f d=%.0f "
+                     "cycles (s_memtime)  per WG total=%.0f\n", p[4], (double)p[3] / p[4],
+                     (double)p[0] / p[3], (double)p[1] / p[3], (double)p[2] / p[3], (double)p[5] / p[4]);
+    }
     // stable LSD radix sort of the records by destination (keys <= H)
     uint32_t bits = 1;
     while (bits < 32 && (H >> bits) != 0) ++bits;
@@ -858,7 +1062,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     uint4* sorted = vb.current();
     uint4* spare = sorted == R.rec.as<uint4>() ? R.brec.as<uint4>() : R.rec.as<uint4>();
     bucket_offsets<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(kb.current(), n, H, o->ev_off);
-    segment_sort_v4<<<std::min<uint32_t>(div_up(H, 4), (uint32_t)ctx->n_cu * 8), 256, 0, s>>>(
+    segment_sort_v4<<<std::min<uint32_t>(div_up(H, 4), (uint32_t)ctx->n_cu * 6), 256, 0, s>>>(
         H, o->ev_off, sorted, rd->round_end, R.next_id.as<uint64_t>(), o->ev_deliver, o->ev_src,
         o->ev_seq, o->ev_pkt, R.ev_val2.as<uint32_t>());
     segment_sort_v2_big<<<64, 256, 0, s>>>(R.ev_val2.as<uint32_t>(), o->ev_off, sorted,
@@ -930,6 +1134,15 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
     SHD_TRY(R.next_id2.ensure((size_t)n_hosts * 8));
     SHD_TRY(R.counts.ensure((size_t)n_nodes * n_nodes * 8));
     SHD_HIP(hipMemcpyAsync(R.host_node.p, host_node, (size_t)n_hosts * 4, hipMemcpyHostToDevice, s));
+    {   // stamp workgroups take hosts in source-node order: their path gathers share table rows
+        std::vector<uint32_t> ord(n_hosts);
+        for (uint32_t h = 0; h < n_hosts; h++) ord[h] = h;
+        std::stable_sort(ord.begin(), ord.end(),
+                         [&](uint32_t x, uint32_t y) { return host_node[x] < host_node[y]; });
+        SHD_TRY(R.order.ensure((size_t)n_hosts * 4));
+        SHD_HIP(hipMemcpyAsync(R.order.p, ord.data(), (size_t)n_hosts * 4, hipMemcpyHostToDevice, s));
+        SHD_HIP(hipStreamSynchronize(s));
+    }
     SHD_HIP(hipMemcpyAsync(R.rng.p, rng_state, (size_t)n_hosts * 32, hipMemcpyHostToDevice, s));
     SHD_HIP(hipMemcpyAsync(R.next_id.p, next_event_id, (size_t)n_hosts * 8, hipMemcpyHostToDevice, s));
     SHD_HIP(hipMemsetAsync(R.counts.p, 0, (size_t)n_nodes * n_nodes * 8, s));

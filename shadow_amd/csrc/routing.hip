@@ -33,12 +33,20 @@ namespace shd {
 // nodes whose latency is <= (min active latency + delta), which keeps the expansion order close
 // to Dijkstra's and cuts re-expansions.  delta = 0xFFFFFFFF expands every active node (plain
 // chaotic Bellman-Ford).  Both converge to the same unique fixed point.
-template <int G, int R, bool CACHE>
+// Label loads: labels in LDS are read at workgroup scope; labels in global memory (kernel 1b)
+// at agent scope, which bypasses the CU's L1 -- the L2 atomics never update it.
+template <bool GLAB>
+__device__ __forceinline__ uint64_t ld_lab(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED,
+                             GLAB ? __HIP_MEMORY_SCOPE_AGENT : __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int G, int R, bool CACHE, bool GLAB>
 __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* lab, uint32_t* bits,
                                            const uint2* rng, const uint32_t* __restrict__ abeg,
                                            const uint32_t* __restrict__ aend,
                                            const uint4* __restrict__ arcs, bool& ovf, bool& dirty) {
-    const uint64_t ku = __hip_atomic_load(&lab[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint64_t ku = ld_lab<GLAB>(&lab[u]);
     const uint32_t lu = key_lat(ku);
     const float qu = one_minus(key_loss(ku));
     const uint2 r = CACHE ? rng[u] : make_uint2(abeg[u], aend[u]);
@@ -72,31 +80,25 @@ __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* la
     }
 }
 
-template <int BLOCK, int G, int R, bool CACHE>
-__global__ __launch_bounds__(BLOCK) void sssp_lds_group(
+constexpr uint32_t kQCap = 64;   // per-wave expansion queue (+32 overflow slots)
+
+// One source row: init, sweeps until nothing improves, emit the used columns.
+template <int BLOCK, int G, int R, bool CACHE, bool GLAB>
+__device__ __forceinline__ void sssp_row(
+    uint64_t* lab, uint32_t* bits, uint32_t* ctl, uint32_t* wq, uint2* rng,
     const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
     const uint4* __restrict__ arcs, uint32_t V, const uint32_t* __restrict__ used,
-    uint32_t n_used, uint32_t row_begin, const uint64_t* __restrict__ diag_lat,
+    uint32_t n_used, uint32_t row, size_t orow, const uint64_t* __restrict__ diag_lat,
     const float* __restrict__ diag_loss, uint64_t* __restrict__ out_lat,
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
     uint32_t seed_stride) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr uint32_t NW = BLOCK / 64, NG = 64 / G, QCAP = 64;
-    uint64_t* lab = reinterpret_cast<uint64_t*>(smem);
+    constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
     const uint32_t W = (V + 31) >> 5;
-    uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V);
-    uint32_t* ctl = bits + W;            // [0] dirty  [1] min active latency
-    uint32_t* wq = ctl + 4;              // per-wave queue (QCAP + 32 node ids)
-    // [V] arc range {beg, end}, 8-byte aligned after the queues
-    const uint32_t rng_off =
-        (((uint32_t)((wq + NW * (QCAP + 32)) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
-    uint2* rng = reinterpret_cast<uint2*>(smem + rng_off);
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t grp = lane / G, gl = lane % G;
-    uint32_t* q = wq + wave * (QCAP + 32);
-    const uint32_t row = row_begin + blockIdx.x;
+    uint32_t* q = wq + wave * (kQCap + 32);
     const uint32_t src = used[row];
     const bool use_delta = delta != kLat32Inf;
 
@@ -109,13 +111,21 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
             const uint32_t d = seed[v];
             if (d != kLat32Inf) l0 = ((uint64_t)d << 32) | 0xFFFFFFFFull;
         }
-        lab[v] = l0;
+        if (GLAB) {
+            if (v == src) l0 = 0;   // PathProperties::default() = (0 ns, 0.0)
+            __hip_atomic_store(&lab[v], l0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            lab[v] = l0;
+        }
         if (CACHE) rng[v] = make_uint2(abeg[v], aend[v]);
     }
     for (uint32_t w = tid; w < W; w += BLOCK) bits[w] = 0;
+    // global labels: every storing wave drains its stores before the barrier, so the L2 holds
+    // them before any wave's atomics
+    if (GLAB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        lab[src] = 0;  // PathProperties::default() = (0 ns, 0.0)
+        if (!GLAB) lab[src] = 0;  // PathProperties::default() = (0 ns, 0.0)
         bits[src >> 5] = 1u << (src & 31);
     }
     bool ovf = false;
@@ -132,7 +142,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
             for (uint32_t widx = wave; widx < W; widx += NW) {
                 const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (word == 0) continue;
-                if (lane < 32 && ((word >> lane) & 1u)) m = min(m, key_lat(lab[widx * 32 + lane]));
+                if (lane < 32 && ((word >> lane) & 1u)) m = min(m, key_lat(ld_lab<GLAB>(&lab[widx * 32 + lane])));
             }
             for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
             if (lane == 0 && m != kLat32Inf) atomicMin(&ctl[1], m);
@@ -149,7 +159,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
                 const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (word != 0) {  // wave-uniform
                     bool sel = lane < 32 && ((word >> lane) & 1u);
-                    if (use_delta && sel) sel = key_lat(lab[widx * 32 + lane]) <= thr;
+                    if (use_delta && sel) sel = key_lat(ld_lab<GLAB>(&lab[widx * 32 + lane])) <= thr;
                     const uint32_t mask = (uint32_t)__ballot(sel);
                     if (mask) {
                         // words are owned by one wave; other waves only set bits: clearing is exact
@@ -159,7 +169,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
                     }
                 }
             }
-            if (qn >= QCAP || (!more && qn > 0)) {   // flush: NG nodes per step, G lanes each
+            if (qn >= kQCap || (!more && qn > 0)) {   // flush: NG nodes per step, G lanes each
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -167,7 +177,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
                 for (uint32_t t = 0; t < qn; t += NG) {
                     const uint32_t qi = t + grp;
                     if (qi < qn)
-                        relax_node<G, R, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, ovf, dirty);
+                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, ovf, dirty);
                 }
                 qn = 0;
                 __builtin_amdgcn_wave_barrier();
@@ -190,7 +200,6 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
         atomicAdd(&stats[0], (unsigned long long)expanded);
         if (wave == 0) atomicAdd(&stats[1], (unsigned long long)sweeps);
     }
-    const size_t orow = (size_t)blockIdx.x * n_used;
     for (uint32_t j = tid; j < n_used; j += BLOCK) {
         uint64_t l;
         float p;
@@ -198,7 +207,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
             l = diag_lat[j];
             p = diag_loss[j];
         } else {
-            const uint64_t k = lab[used[j]];
+            const uint64_t k = ld_lab<GLAB>(&lab[used[j]]);
             if (k == kKeyInf) {
                 atomicMin(unreach, (unsigned long long)((uint64_t)row * n_used + j));
                 l = ~0ull;
@@ -210,6 +219,62 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
         }
         out_lat[orow + j] = l;
         out_loss[orow + j] = p;
+    }
+}
+
+// Kernel 1: one workgroup per source row, labels (8 B/node) and the arc ranges in LDS.
+template <int BLOCK, int G, int R, bool CACHE>
+__global__ __launch_bounds__(BLOCK) void sssp_lds_group(
+    const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
+    const uint4* __restrict__ arcs, uint32_t V, const uint32_t* __restrict__ used,
+    uint32_t n_used, uint32_t row_begin, const uint64_t* __restrict__ diag_lat,
+    const float* __restrict__ diag_loss, uint64_t* __restrict__ out_lat,
+    float* __restrict__ out_loss, uint32_t* __restrict__ flags,
+    unsigned long long* __restrict__ unreach, uint32_t delta,
+    unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
+    uint32_t seed_stride) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr uint32_t NW = BLOCK / 64;
+    uint64_t* lab = reinterpret_cast<uint64_t*>(smem);
+    const uint32_t W = (V + 31) >> 5;
+    uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V);
+    uint32_t* ctl = bits + W;            // [0] dirty  [1] min active latency
+    uint32_t* wq = ctl + 4;              // per-wave queue (kQCap + 32 node ids)
+    // [V] arc range {beg, end}, 8-byte aligned after the queues
+    const uint32_t rng_off =
+        (((uint32_t)((wq + NW * (kQCap + 32)) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
+    uint2* rng = reinterpret_cast<uint2*>(smem + rng_off);
+    sssp_row<BLOCK, G, R, CACHE, false>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
+                                        row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
+                                        diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
+                                        delta, stats, seed_lat, seed_stride);
+}
+
+// Kernel 1b: labels in global memory, for graphs whose labels do not fit the LDS (C4: 50k
+// nodes = 400 KB per source).  A persistent grid of slots: slot b owns the label array
+// glab[b*V, (b+1)*V) and walks rows row_begin + b, + gridDim.x, ...; the bitmap and the queues
+// stay in LDS (V/8 bytes).
+template <int BLOCK, int G, int R>
+__global__ __launch_bounds__(BLOCK) void sssp_global_group(
+    const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
+    const uint4* __restrict__ arcs, uint32_t V, const uint32_t* __restrict__ used,
+    uint32_t n_used, uint32_t row_begin, uint32_t row_end, const uint64_t* __restrict__ diag_lat,
+    const float* __restrict__ diag_loss, uint64_t* __restrict__ out_lat,
+    float* __restrict__ out_loss, uint32_t* __restrict__ flags,
+    unsigned long long* __restrict__ unreach, uint32_t delta,
+    unsigned long long* __restrict__ stats, uint64_t* __restrict__ glab) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t W = (V + 31) >> 5;
+    uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* ctl = bits + W;
+    uint32_t* wq = ctl + 4;
+    uint64_t* lab = glab + (size_t)blockIdx.x * V;
+    for (uint32_t row = row_begin + blockIdx.x; row < row_end; row += gridDim.x) {
+        sssp_row<BLOCK, G, R, false, true>(lab, bits, ctl, wq, nullptr, abeg, aend, arcs, V, used,
+                                           n_used, row, (size_t)(row - row_begin) * n_used,
+                                           diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
+                                           delta, stats, nullptr, 0);
+        __syncthreads();   // the next row re-initialises labels and bitmap
     }
 }
 
@@ -810,6 +875,55 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
     return SHD_OK;
 }
 
+template <int BLOCK, int G>
+static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint32_t grid,
+                          size_t lds, uint64_t* d_lat, float* d_loss, uint32_t delta) {
+    PreparedGraph& P = ctx->prep;
+    constexpr int R = G >= 32 ? 2 : 4;
+    sssp_global_group<BLOCK, G, R><<<grid, BLOCK, lds, ctx->stream>>>(
+        A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb, re,
+        ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
+        ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
+        delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
+        ctx->g_glab.as<uint64_t>());
+}
+
+// Kernel 1b driver: labels in global memory (graphs whose labels exceed the LDS).
+static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re,
+                                  uint64_t* d_lat, float* d_loss, uint32_t delta, bool* ovf) {
+    PreparedGraph& P = ctx->prep;
+    hipStream_t s = ctx->stream;
+    constexpr uint32_t BLOCK = 512;
+    const uint32_t W = (P.V + 31) / 32;
+    const size_t lds = (size_t)W * 4 + 16 + (BLOCK / 64) * (kQCap + 32) * 4;
+    if (lds > ctx->max_lds) return SHD_ERR_INVALID;   // bitmap of > ~1.2M nodes
+    const uint32_t per_cu = std::max<uint32_t>(1, env_u32("SHD_SSSP_SLOTS", 2));
+    const uint32_t grid = std::min<uint32_t>(re - rb, (uint32_t)ctx->n_cu * per_cu);
+    SHD_TRY(ctx->g_glab.ensure((size_t)grid * P.V * 8));
+    const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
+    const uint32_t G = env_u32("SHD_SSSP_G", deg >= 64 ? 16 : deg >= 24 ? 8 : 4);
+    SHD_HIP(hipEventRecord(ctx->ev[2], s));
+    switch (G) {
+        case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta); break;
+        case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta); break;
+        default: launch_global<BLOCK, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta); break;
+    }
+    SHD_HIP(hipGetLastError());
+    SHD_HIP(hipEventRecord(ctx->ev[3], s));
+    uint32_t fl = 0;
+    SHD_HIP(hipMemcpyAsync(&fl, ctx->g_flags.p, 4, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    *ovf = fl != 0;
+    if (ctx->stats_on) {
+        unsigned long long st[2];
+        SHD_HIP(hipMemcpy(st, ctx->g_flags.as<char>() + 32, 16, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "shd_sssp_global: rows=%u G=%u slots=%u delta=%u expanded=%llu (%.2f per node) "
+                     "sweeps=%llu (%.1f per row)\n", re - rb, G, grid, delta, st[0],
+                     (double)st[0] / ((double)(re - rb) * P.V), st[1], (double)st[1] / (re - rb));
+    }
+    return SHD_OK;
+}
+
 shd_status fw_latency(shd_ctx* ctx, uint32_t* D, uint32_t Vp, uint32_t T);
 shd_status fw_tight(shd_ctx* ctx, const uint32_t* D, uint32_t Vp, uint32_t* pbeg, uint32_t* pend,
                     uint4* parcs, uint32_t* cursor);
@@ -936,7 +1050,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         SHD_TRY(reset_flags(ctx));
         return run_wide(ctx, rb, re, d_lat, d_loss, err);
     }
-    if (P.narrow_arcs && lds <= ctx->max_lds) {
+    if (P.narrow_arcs && lds <= ctx->max_lds && env_u32("SHD_SSSP_GLOBAL", 0) != 1) {
         const bool dense = P.V <= kPruneMaxV && P.arcs * 8 >= (uint64_t)P.V * P.V;
         const bool prune = (algo == SHD_ALGO_PRUNED ||
                             ((algo == SHD_ALGO_AUTO || algo == SHD_ALGO_DELTA) && dense)) &&
@@ -966,6 +1080,25 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ctx->info.arcs_kept = prune ? P.pruned_arcs : P.arcs;
         if (!ovf) return check_unreach(ctx, err);
         SHD_TRY(reset_flags(ctx));  // some path latency >= 2^32-1 ns: redo with u64 labels
+    }
+    if (P.narrow_arcs && (lds > ctx->max_lds || env_u32("SHD_SSSP_GLOBAL", 0) == 1)) {
+        // labels exceed the LDS: global-label kernel (C4)
+        bool ovf = false;
+        uint32_t delta = kLat32Inf;
+        if (algo == SHD_ALGO_DELTA) delta = env_u32("SHD_SSSP_DELTA", P.mean_arc_lat);
+        ArcView A{ctx->g_off.as<uint32_t>(), ctx->g_off.as<uint32_t>() + 1, ctx->g_arc16.as<uint4>(),
+                  P.arcs};
+        SHD_TRY(run_sssp_global(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
+        ctx->info.algo_used = algo == SHD_ALGO_DELTA ? SHD_ALGO_DELTA : SHD_ALGO_SSSP;
+        SHD_HIP(hipEventRecord(ctx->ev[1], s));
+        SHD_HIP(hipEventSynchronize(ctx->ev[1]));
+        float ms = 0, ms_main = 0;
+        (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
+        (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);
+        ctx->info.ms_total = ms;
+        ctx->info.ms_main = ms_main;
+        if (!ovf) return check_unreach(ctx, err);
+        SHD_TRY(reset_flags(ctx));
     }
     return run_wide(ctx, rb, re, d_lat, d_loss, err);
 }

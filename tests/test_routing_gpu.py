@@ -186,3 +186,33 @@ def test_blocked_closure_padding_and_directed(engine):
         _assert_table(t, lat, loss.view(np.uint32))
         info = engine.last_info()
         assert info["algo_used"] == 4 and info["ms_minplus"] > 0
+
+
+@pytest.mark.parametrize("algo", [1, 3])
+def test_global_label_kernel_large_graph(engine, algo):
+    """V = 25k nodes: 8-byte labels no longer fit the LDS, so the global-label kernel runs.
+    200 used nodes spread over the graph; every pair against the C restatement."""
+    from shadow_amd import synth
+    el = synth.barabasi_albert(25_000, 2, 17)
+    used = np.random.default_rng(5).choice(25_000, size=200, replace=False).astype(np.uint32)
+    code, lat, loss, _ = corc.routing(25_000, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    t = engine_graph_from_edges(el).compute_shortest_paths(used, engine, algo=algo)
+    _assert_table(t, lat, loss.view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_global_label_kernel_forced(engine, seed, monkeypatch):
+    """The global-label kernel on small tie-heavy graphs (forced with SHD_SSSP_GLOBAL=1)."""
+    monkeypatch.setenv("SHD_SSSP_GLOBAL", "1")
+    rng = np.random.default_rng(2000 + seed)
+    n = int(rng.integers(2, 300))
+    ids, s, d, l, p, directed = random_graph(rng, n, float(rng.uniform(0.005, 0.3)), bool(seed % 2),
+                                             max_ms=int(rng.integers(2, 50)))
+    used = rng.permutation(n).astype(np.uint32)
+    code, lat, loss, _ = corc.routing(n, s, d, l, p, directed, used)
+    assert code == "OK"
+    from shadow_amd.routing import NetworkGraph
+    for algo in (1, 3):
+        t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=algo)
+        _assert_table(t, lat, loss.view(np.uint32))
