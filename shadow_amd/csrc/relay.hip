@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void relay_scatter(
 }
 
 // Sort one destination's bucket by (deliver, src, seq) -- bitonic network in LDS.
-constexpr uint32_t kSegCap = 1024;
+constexpr uint32_t kV1Cap = 1024;
 
 struct EvKey {
     uint64_t t;
@@ -188,11 +188,11 @@ __global__ __launch_bounds__(256) void segment_sort(
     uint32_t n_hosts, const uint32_t* __restrict__ ev_off, uint64_t* __restrict__ ev_deliver,
     uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq, uint32_t* __restrict__ ev_pkt,
     uint32_t* __restrict__ big) {
-    __shared__ EvKey s[kSegCap];
+    __shared__ EvKey s[kV1Cap];
     const uint32_t d = blockIdx.x;
     const uint32_t b = ev_off[d], n = ev_off[d + 1] - b;
     if (n <= 1) return;
-    if (n > kSegCap) {
+    if (n > kV1Cap) {
         if (threadIdx.x == 0) big[atomicAdd(&big[0], 1u) + 1] = d;
         return;
     }
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(256) void segment_sort(
     }
 }
 
-// Oversized buckets (> kSegCap events for one destination in one round): bottom-up merge
+// Oversized buckets (> kV1Cap events for one destination in one round): bottom-up merge
 // sort of that bucket by one workgroup through a global scratch area.
 __global__ __launch_bounds__(256) void segment_sort_big(
     const uint32_t* __restrict__ big, const uint32_t* __restrict__ ev_off,
@@ -283,11 +283,10 @@ __global__ __launch_bounds__(256) void segment_sort_big(
 // ==========================================================================================
 // Narrow pipeline (every path latency < 2^32 ns and every deliver - round_end < 2^32): 16-byte
 // event records {deliver - round_end, src host, seq - seq_base[src], packet index}.
-//   K1 relay_stamp_v3   workgroup per kS3Hosts consecutive source hosts; their sends (one
-//                       contiguous range of the batch) stream through LDS in chunks:
-//                       coalesced loads, lane-per-packet path gathers, lane-per-host decisions
-//                       (only the RNG draws and event ids are sequential per host), coalesced
-//                       stores of status / record / destination key
+//   K0 relay_draws      lane per source host: its Xoshiro256++ stream (the only sequential work)
+//   K1 relay_stamp_v5   workgroup per 64 source hosts (in source-node order), lane per send:
+//                       coalesced loads, path lookup (LDS-staged rows), drop rule, deliver
+//                       stamp, scan-based event ids, coalesced stores of status / key / record
 //   K2 rocPRIM onesweep radix sort of the records by destination -- stable: the batch is in
 //      (source host, event id) order, so every destination's run stays in that order
 //   K3 bucket_offsets   lower bound of every destination in the sorted keys
@@ -295,9 +294,6 @@ __global__ __launch_bounds__(256) void segment_sort_big(
 //                       (deliver offset << 32 | position in the run); ties on the deliver time
 //                       fall back to run order = (src host, event id) order
 // ==========================================================================================
-constexpr uint32_t kS3Hosts = 64;      // source hosts per workgroup (one lane each in phase c)
-constexpr uint32_t kS3Chunk = 512;     // packets per LDS chunk (2 per thread)
-
 struct RelayArgs3 {
     uint32_t n_hosts, n_nodes;
     const uint32_t* src_off;
@@ -314,214 +310,249 @@ struct RelayArgs3 {
     uint64_t* next_id_out;
     unsigned long long* counts;
     uint64_t round_end, sim_end, bootstrap_end;
+    uint32_t abs_seq;    // 1: every event id of the round fits 32 bits -> records hold absolute ids
     uint8_t* status;
     uint4* rec;          // per packet (valid when SENT)
     uint32_t* key;       // per packet: destination host if SENT, else n_hosts (sorts last)
     unsigned long long* red;   // [0] min deliver [1] min latency [2] n_sent [3] bad dst [4] wide
-    unsigned long long* prof;  // nullable: phase timings (SHD_RELAY_PROF=1, tuning only)
 };
 
-// K1: a workgroup owns kS3Hosts source hosts, taken in source-node order (R.order: hosts sorted
-// by host_node at setup), so a workgroup's path gathers stay inside a few rows of the table and
-// hit L2.  Chunk k holds the slice [k*S, (k+1)*S) of every host's sends (S = kS3Slice); 8
-// consecutive lanes own the 8 sends of one host in the slice (coalesced loads and stores).
-//   (ab) lane per send: raw loads (prefetched one chunk ahead), path gathers, skip test; a
-//        ballot gives each host its mask of sends that draw (now < sim_end)
-//   (c1) lane per host: the host's Xoshiro256++ stream fills the draws of the masked sends in
-//        send order -- the only sequential work
-//   (c2) lane per send: drop rule, deliver stamp, event id (ballot prefix inside the host's
-//        8-lane group plus the host's running count), stores
-constexpr uint32_t kS3Slice = kS3Chunk / kS3Hosts;   // sends per host per chunk (8)
-constexpr uint32_t kS3Lds = kS3Slice * (kS3Hosts + 1);
+constexpr uint32_t kDrawSlice = 8;
 
-__global__ __launch_bounds__(256) void relay_stamp_v3(RelayArgs3 a) {
-    constexpr uint32_t SPT = kS3Chunk / 256;          // sends per thread per chunk
-    __shared__ uint64_t s_draw[kS3Lds];               // raw generator outputs, slot j*65 + host
-    __shared__ uint32_t s_host[kS3Hosts], s_beg[kS3Hosts], s_len[kS3Hosts], s_node[kS3Hosts];
-    __shared__ uint32_t s_mask[kS3Hosts], s_nsent[kS3Hosts];
-    __shared__ uint32_t s_maxlen;
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t h0 = blockIdx.x * kS3Hosts;
-    const uint32_t nh = min(kS3Hosts, a.n_hosts - h0);
-    if (tid == 0) s_maxlen = 0;
-    __syncthreads();
-    if (tid < nh) {
-        const uint32_t h = a.order[h0 + tid];
-        const uint32_t b = a.src_off[h];
-        s_host[tid] = h;
-        s_beg[tid] = b;
-        s_len[tid] = a.src_off[h + 1] - b;
-        s_node[tid] = a.host_node[h];
-        s_nsent[tid] = 0;
-        atomicMax(&s_maxlen, s_len[tid]);
-    }
-    const bool host_lane = tid < nh;
+// K0 relay_draws: the only sequential part of the relay -- every source host's Xoshiro256++
+// stream (host.rs:218, worker.rs:365) -- as its own kernel: one lane per host (64 consecutive
+// hosts per one-wave workgroup), staged through LDS so the draws leave as 64-byte runs.  A send
+// draws iff now < sim_end (worker.rs:334-341); send times are non-decreasing within a host (a
+// host's sends happen in simulated-time order; the stamp checks it), so the drawing sends are a
+// prefix of the host's range, found from its last send (binary search when it is skipped).
+__global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint64_t* __restrict__ draw) {
+    __shared__ uint64_t s[kDrawSlice][65];
+    __shared__ uint32_t s_beg[64], s_nd[64];
+    const uint32_t lane = threadIdx.x, h = blockIdx.x * 64 + lane;
+    uint32_t nd = 0;
     Xoshiro r{0, 0, 0, 0};
-    if (host_lane && !a.chance) {
-        const size_t h = a.order[h0 + tid];
-        r = Xoshiro{a.rng[4 * h], a.rng[4 * h + 1], a.rng[4 * h + 2], a.rng[4 * h + 3]};
+    if (h < a.n_hosts) {
+        const uint32_t b = a.src_off[h], e = a.src_off[h + 1];
+        nd = e - b;
+        if (nd && !(a.send_time[e - 1] < a.sim_end)) {   // first send with now >= sim_end
+            uint32_t lo = b, hi = e;
+            while (lo < hi) {
+                const uint32_t m = (lo + hi) >> 1;
+                if (a.send_time[m] < a.sim_end) lo = m + 1; else hi = m;
+            }
+            nd = lo - b;
+        }
+        s_beg[lane] = b;
+        r = Xoshiro{a.rng[4 * (size_t)h], a.rng[4 * (size_t)h + 1], a.rng[4 * (size_t)h + 2],
+                    a.rng[4 * (size_t)h + 3]};
+    } else {
+        s_beg[lane] = 0;
+    }
+    s_nd[lane] = nd;
+    uint32_t mx = nd;
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    for (uint32_t j0 = 0; j0 < mx; j0 += kDrawSlice) {
+#pragma unroll
+        for (uint32_t k = 0; k < kDrawSlice; ++k)
+            if (j0 + k < nd) s[k][lane] = r.next();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // 8 lanes per host write its kDrawSlice consecutive draws (64 contiguous bytes)
+#pragma unroll
+        for (uint32_t g = 0; g < 64 * kDrawSlice / 64; ++g) {
+            const uint32_t hl = g * (64 / kDrawSlice) + lane / kDrawSlice, k = lane % kDrawSlice;
+            if (j0 + k < s_nd[hl]) draw[s_beg[hl] + j0 + k] = s[k][hl];
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (h < a.n_hosts) {
+        a.rng_out[4 * (size_t)h] = r.s0;
+        a.rng_out[4 * (size_t)h + 1] = r.s1;
+        a.rng_out[4 * (size_t)h + 2] = r.s2;
+        a.rng_out[4 * (size_t)h + 3] = r.s3;
+    }
+}
+
+// K1 relay_stamp_v5: a workgroup owns kS5Hosts source hosts taken in source-node order
+// (R.order), so its path lookups stay in one or two table rows, staged in LDS when they fit.
+// The hosts' sends (one contiguous range per host) form one list, processed in chunks of
+// kS5Cap positions with consecutive lanes on consecutive positions (coalesced inside every
+// host's range).  No sequential work is left: lane per send, the raw loads, the draw (K0), the
+// destination node and path, the drop rule and deliver stamp (worker.rs:370-402); a block-wide
+// exclusive scan of the sent flags gives every sent packet its event id (host.rs:580-584).
+constexpr uint32_t kS5Hosts = 64;
+constexpr uint32_t kS5Per = 4;                  // sends per thread per chunk
+constexpr uint32_t kS5Cap = 256 * kS5Per;
+constexpr uint32_t kS5RowLds = 2048;            // staged path-table entries (16 KB)
+
+__global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint64_t* __restrict__ draw) {
+    __shared__ uint2 s_rows[kS5RowLds];
+    __shared__ uint16_t s_scan[kS5Cap + 1];
+    __shared__ uint32_t s_host[kS5Hosts], s_beg[kS5Hosts], s_pre[kS5Hosts + 1], s_node[kS5Hosts];
+    __shared__ uint32_t s_rowof[kS5Hosts], s_rownode[kS5Hosts], s_run[kS5Hosts], s_base[kS5Hosts];
+    __shared__ uint32_t s_wsum[4], s_nrows;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t h0 = blockIdx.x * kS5Hosts;
+    const uint32_t nh = min(kS5Hosts, a.n_hosts - h0);
+    if (tid < 64) {   // wave 0: this workgroup's hosts, their ranges (prefix) and staged rows
+        uint32_t len = 0, nd = 0;
+        if (tid < nh) {
+            const uint32_t h = a.order[h0 + tid];
+            const uint32_t b = a.src_off[h];
+            len = a.src_off[h + 1] - b;
+            nd = a.host_node[h];
+            s_host[tid] = h;
+            s_beg[tid] = b;
+            s_node[tid] = nd;
+            s_run[tid] = 0;
+            s_base[tid] = a.abs_seq ? (uint32_t)a.next_id[h] : 0u;
+        }
+        uint32_t incl = len;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        if (tid < nh) s_pre[tid + 1] = incl;
+        if (tid == 0) s_pre[0] = 0;
+        const uint32_t prev = __shfl_up(nd, 1);
+        const bool first = tid < nh && (tid == 0 || nd != prev);
+        const uint64_t fm = __ballot(first);
+        if (tid < nh) {
+            const uint32_t ri = (uint32_t)__popcll(fm & ((2ull << tid) - 1ull)) - 1u;
+            s_rowof[tid] = ri;
+            if (first) s_rownode[ri] = nd;
+        }
+        if (tid == 0) s_nrows = (uint32_t)__popcll(fm);
     }
     __syncthreads();
-    const uint32_t n_chunks = (s_maxlen + kS3Slice - 1) / kS3Slice;
-    uint32_t hl[SPT], jj[SPT], len[SPT], base[SPT], ls[SPT];
-#pragma unroll
-    for (uint32_t q = 0; q < SPT; ++q) {
-        const uint32_t g = tid + 256 * q;
-        hl[q] = g / kS3Slice;
-        jj[q] = g % kS3Slice;
-        ls[q] = jj[q] * (kS3Hosts + 1) + hl[q];
-        const bool hv = hl[q] < nh;
-        base[q] = hv ? s_beg[hl[q]] : 0u;
-        len[q] = hv ? s_len[hl[q]] : 0u;
-    }
-    uint64_t now[SPT];
-    uint32_t dst[SPT], pay[SPT];
-    auto load_raw = [&](uint32_t k) {
-#pragma unroll
-        for (uint32_t q = 0; q < SPT; ++q) {
-            const uint32_t t = k * kS3Slice + jj[q];
-            const bool v = t < len[q];
-            const uint32_t i = base[q] + t;
-            now[q] = v ? a.send_time[i] : ~0ull;
-            dst[q] = v ? a.dst_host[i] : 0u;
-            pay[q] = v ? a.payload[i] : 0u;
+    const bool staged = (uint64_t)s_nrows * a.n_nodes <= kS5RowLds;
+    if (staged) {
+        const uint32_t tot = s_nrows * a.n_nodes;
+        for (uint32_t e = tid; e < tot; e += 256) {
+            const uint32_t rr = e / a.n_nodes, c = e - rr * a.n_nodes;
+            s_rows[e] = a.path[(size_t)s_rownode[rr] * a.n_nodes + c];
         }
-    };
-    // SHD_RELAY_PROF=1: per-phase s_memtime totals of thread 0 (tuning only)
-    uint64_t tp0 = a.prof ? __builtin_amdgcn_s_memtime() : 0, tab = 0, tc = 0, td = 0, tt0 = tp0;
-    if (n_chunks) load_raw(0);
+    }
+    __syncthreads();
+    const uint32_t T = s_pre[nh];
     uint64_t min_d = ~0ull, min_l = ~0ull;
-    bool wide = false;
-    const uint32_t gshift = lane & ~(kS3Slice - 1);    // first lane of this lane's host group
-    for (uint32_t k = 0; k < n_chunks; ++k) {
-        // (ab) path gathers and the draw mask (lane per send)
-        uint2 pp[SPT];
-        size_t pidx[SPT];
-        bool valid[SPT], draws[SPT];
+    bool wide = false, disorder = false;
+    for (uint32_t c0 = 0; c0 < T; c0 += kS5Cap) {
+        const uint32_t cn = min(kS5Cap, T - c0);
+        uint8_t st[kS5Per];
+        uint32_t doff[kS5Per], dst[kS5Per], idx[kS5Per], hl[kS5Per], dn[kS5Per];
 #pragma unroll
-        for (uint32_t q = 0; q < SPT; ++q) {
-            const uint32_t t = k * kS3Slice + jj[q];
-            valid[q] = t < len[q];
-            pidx[q] = 0;
-            pp[q] = make_uint2(0u, 0u);
-            if (valid[q] && dst[q] >= a.n_hosts) {   // "No host ID for dest address" (worker.rs:350-355)
-                atomicMin(&a.red[3], (unsigned long long)(base[q] + t));
-                now[q] = ~0ull;                       // the round fails; no draw
-            } else if (valid[q]) {
-                pidx[q] = (size_t)s_node[hl[q]] * a.n_nodes + a.host_node[dst[q]];
-                pp[q] = a.path[pidx[q]];
-            }
-            draws[q] = valid[q] && now[q] < a.sim_end;
-            const uint32_t gm = (uint32_t)(__ballot(draws[q]) >> gshift) & ((1u << kS3Slice) - 1u);
-            if (jj[q] == 0) s_mask[hl[q]] = gm;
-        }
-        __syncthreads();
-        if (a.prof) {
-            const uint64_t t1 = __builtin_amdgcn_s_memtime();
-            tab += t1 - tp0;
-            tp0 = t1;
-        }
-        // (c1) the host's generator, in send order, for the sends that draw (lane per host)
-        if (host_lane && !a.chance) {
-            uint32_t m = s_mask[tid];
-            while (m) {
-                const uint32_t j = __builtin_ctz(m);
-                m &= m - 1;
-                s_draw[j * (kS3Hosts + 1) + tid] = r.next();
-            }
-        }
-        __syncthreads();
-        if (a.prof) {
-            const uint64_t t1 = __builtin_amdgcn_s_memtime();
-            tc += t1 - tp0;
-            tp0 = t1;
-        }
-        uint64_t now_cur[SPT];
-        uint32_t dst_cur[SPT], pay_cur[SPT];
-#pragma unroll
-        for (uint32_t q = 0; q < SPT; ++q) {
-            now_cur[q] = now[q];
-            dst_cur[q] = dst[q];
-            pay_cur[q] = pay[q];
-        }
-        if (k + 1 < n_chunks) load_raw(k + 1);   // in flight during the decisions and stores
-        // (c2) decisions, event ids, stores (lane per send)
-#pragma unroll
-        for (uint32_t q = 0; q < SPT; ++q) {
-            const uint32_t t = k * kS3Slice + jj[q];
-            const uint32_t i = base[q] + t;
-            uint8_t st = kStSkipped;
-            uint32_t doff = 0;
-            if (draws[q]) {
-                const double reliability = (double)one_minus(__uint_as_float(pp[q].y));
-                const double ch = a.chance ? a.chance[i]
-                                           : (double)(s_draw[ls[q]] >> 11) * (1.0 / 9007199254740992.0);
-                if (!(now_cur[q] < a.bootstrap_end) && ch >= reliability && pay_cur[q] > 0) {
-                    st = kStDropped;
-                } else {
-                    uint64_t tt = now_cur[q] + pp[q].x;
-                    if (tt < a.round_end) tt = a.round_end;
-                    const uint64_t dd = tt - a.round_end;
-                    wide |= (dd >> 32) != 0;
-                    min_d = tt < min_d ? tt : min_d;
-                    min_l = pp[q].x < min_l ? pp[q].x : min_l;
-                    doff = (uint32_t)dd;
-                    st = kStSent;
+        for (uint32_t i = 0; i < kS5Per; ++i) {
+            const uint32_t pos = tid + 256 * i;
+            st[i] = kStSkipped;
+            doff[i] = dst[i] = idx[i] = hl[i] = dn[i] = 0;
+            if (pos < cn) {
+                const uint32_t gp = c0 + pos;
+                uint32_t lo = 0, hi = nh;       // s_pre[lo] <= gp < s_pre[lo + 1]
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_pre[mid] <= gp) lo = mid; else hi = mid;
+                }
+                hl[i] = lo;
+                const uint32_t k = gp - s_pre[lo];
+                idx[i] = s_beg[lo] + k;
+                const uint64_t now = a.send_time[idx[i]];
+                dst[i] = a.dst_host[idx[i]];
+                const uint32_t pay = a.payload[idx[i]];
+                // a drawing send after a skipped one breaks K0's prefix rule
+                if (k > 0 && now < a.sim_end && !(a.send_time[idx[i] - 1] < a.sim_end)) disorder = true;
+                if (dst[i] >= a.n_hosts) {      // "No host ID for dest address" (worker.rs:350-355)
+                    atomicMin(&a.red[3], (unsigned long long)idx[i]);
+                } else if (now < a.sim_end) {
+                    dn[i] = a.host_node[dst[i]];
+                    const uint2 pp = staged ? s_rows[s_rowof[lo] * a.n_nodes + dn[i]]
+                                            : a.path[(size_t)s_node[lo] * a.n_nodes + dn[i]];
+                    const double reliability = (double)one_minus(__uint_as_float(pp.y));
+                    const double ch = a.chance ? a.chance[idx[i]]
+                                               : (double)(draw[idx[i]] >> 11) * (1.0 / 9007199254740992.0);
+                    if (!(now < a.bootstrap_end) && ch >= reliability && pay > 0) {
+                        st[i] = kStDropped;
+                    } else {
+                        uint64_t tt = now + pp.x;
+                        if (tt < a.round_end) tt = a.round_end;
+                        const uint64_t dd = tt - a.round_end;
+                        wide |= (dd >> 32) != 0;
+                        min_d = tt < min_d ? tt : min_d;
+                        min_l = pp.x < min_l ? pp.x : min_l;
+                        doff[i] = (uint32_t)dd;
+                        st[i] = kStSent;
+                    }
                 }
             }
-            // event id: the host's running count + sent sends before this one in its group
-            const uint64_t sm = __ballot(st == kStSent);
-            const uint32_t gm = (uint32_t)(sm >> gshift) & ((1u << kS3Slice) - 1u);
-            const uint32_t below = __popc(gm & ((1u << (lane - gshift)) - 1u));
-            const uint32_t run = hl[q] < nh ? s_nsent[hl[q]] : 0u;
-            if (valid[q]) {
-                a.status[i] = st;
-                a.key[i] = st == kStSent ? dst_cur[q] : a.n_hosts;
-                if (st == kStSent) {
-                    a.rec[i] = make_uint4(doff, s_host[hl[q]], run + below, i);
-                    if (a.counts) atomicAdd(&a.counts[pidx[q]], 1ull);
+            s_scan[pos] = st[i] == kStSent ? 1 : 0;
+        }
+        __syncthreads();
+        {   // block-wide exclusive scan of the sent flags (kS5Per consecutive entries per thread)
+            uint32_t v[kS5Per], sum = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < kS5Per; ++i) {
+                v[i] = s_scan[tid * kS5Per + i];
+                sum += v[i];
+            }
+            uint32_t incl = sum;
+#pragma unroll
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (lane == 63) s_wsum[w] = incl;
+            __syncthreads();
+            uint32_t run = incl - sum;
+            for (uint32_t ww = 0; ww < w; ++ww) run += s_wsum[ww];
+#pragma unroll
+            for (uint32_t i = 0; i < kS5Per; ++i) {
+                s_scan[tid * kS5Per + i] = (uint16_t)run;
+                run += v[i];
+            }
+            if (tid == 255) s_scan[kS5Cap] = (uint16_t)run;
+        }
+        __syncthreads();
+        // stores; event id = host's running count + sent sends before this one in its range
+#pragma unroll
+        for (uint32_t i = 0; i < kS5Per; ++i) {
+            const uint32_t pos = tid + 256 * i;
+            if (pos < cn) {
+                a.status[idx[i]] = st[i];
+                a.key[idx[i]] = st[i] == kStSent ? dst[i] : a.n_hosts;
+                if (st[i] == kStSent) {
+                    const uint32_t first = max(s_pre[hl[i]], c0) - c0;
+                    const uint32_t local = s_base[hl[i]] + s_run[hl[i]] + s_scan[pos] - s_scan[first];
+                    a.rec[idx[i]] = make_uint4(doff[i], s_host[hl[i]], local, idx[i]);
+                    if (a.counts) atomicAdd(&a.counts[(size_t)s_node[hl[i]] * a.n_nodes + dn[i]], 1ull);
                 }
             }
-            if (jj[q] == 0 && hl[q] < nh) s_nsent[hl[q]] = run + __popc(gm);
         }
-        if (a.prof) {
-            const uint64_t t1 = __builtin_amdgcn_s_memtime();
-            td += t1 - tp0;
-            tp0 = t1;
+        __syncthreads();
+        if (tid < nh) {   // running counts for the next chunk
+            const uint32_t pb = max(s_pre[tid], c0), pe = min(s_pre[tid + 1], c0 + cn);
+            if (pe > pb) s_run[tid] += s_scan[pe - c0] - s_scan[pb - c0];
         }
-    }
-    __syncthreads();
-    if (a.prof && tid == 0) {
-        atomicAdd(&a.prof[0], (unsigned long long)tab);
-        atomicAdd(&a.prof[1], (unsigned long long)tc);
-        atomicAdd(&a.prof[2], (unsigned long long)td);
-        atomicAdd(&a.prof[3], (unsigned long long)n_chunks);
-        atomicAdd(&a.prof[4], 1ull);
-        atomicAdd(&a.prof[5], (unsigned long long)(__builtin_amdgcn_s_memtime() - tt0));
+        __syncthreads();
     }
     uint64_t ns = 0;
-    if (host_lane) {
+    if (tid < nh) {
         const size_t h = s_host[tid];
-        if (!a.chance) {
-            a.rng_out[4 * h] = r.s0;
-            a.rng_out[4 * h + 1] = r.s1;
-            a.rng_out[4 * h + 2] = r.s2;
-            a.rng_out[4 * h + 3] = r.s3;
-        } else {
-            for (int w = 0; w < 4; ++w) a.rng_out[4 * h + w] = a.rng[4 * h + w];
-        }
-        ns = s_nsent[tid];
+        if (a.chance)
+            for (int k = 0; k < 4; ++k) a.rng_out[4 * h + k] = a.rng[4 * h + k];
+        ns = s_run[tid];
         a.next_id_out[h] = a.next_id[h] + ns;
     }
     min_d = wave_min_u64(min_d);
     min_l = wave_min_u64(min_l);
     for (int o = 32; o > 0; o >>= 1) ns += __shfl_xor(ns, o);
-    const bool any_wide = __ballot(wide) != 0;
+    const bool any_wide = __ballot(wide) != 0, any_disorder = __ballot(disorder) != 0;
     if (lane == 0) {
         if (min_d != ~0ull) atomicMin(&a.red[0], (unsigned long long)min_d);
         if (min_l != ~0ull) atomicMin(&a.red[1], (unsigned long long)min_l);
         if (ns) atomicAdd(&a.red[2], (unsigned long long)ns);
         if (any_wide) atomicOr(&a.red[4], 1ull);
+        if (any_disorder) atomicOr(&a.red[5], 1ull);
     }
 }
 
@@ -589,32 +620,6 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&k)[NPL], uint32_t lane) 
     }
 }
 
-template <int NPL>
-__device__ __forceinline__ void sort_run(uint32_t n, uint32_t b, uint32_t lane, const uint4* x,
-                                         uint64_t round_end, const uint64_t* __restrict__ seq_base,
-                                         uint64_t* __restrict__ ev_deliver,
-                                         uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq,
-                                         uint32_t* __restrict__ ev_pkt) {
-    uint64_t k[NPL];
-#pragma unroll
-    for (int c = 0; c < NPL; ++c) {
-        const uint32_t e = lane + 64u * c;
-        k[c] = e < n ? (((uint64_t)x[e].x << 32) | e) : ~0ull;
-    }
-    wave_bitonic<NPL>(k, lane);
-#pragma unroll
-    for (int c = 0; c < NPL; ++c) {
-        const uint32_t e = lane + 64u * c;
-        if (e < n) {
-            const uint4 r = x[(uint32_t)k[c]];
-            ev_deliver[b + e] = round_end + r.x;
-            ev_src[b + e] = r.y;
-            ev_seq[b + e] = seq_base[r.y] + r.z;
-            ev_pkt[b + e] = r.w;
-        }
-    }
-}
-
 // xor lane exchange inside a wave for a compile-time distance (the bitonic loops below are fully
 // unrolled, so j folds): DPP quad_perm for 1 and 2, DPP row_ror:8 for 8, ds_swizzle (bitmask
 // mode) for 4, v_permlane16_swap / v_permlane32_swap (gfx950) for 16 and 32.
@@ -676,84 +681,130 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v, uint32_t lane) {
     return v;
 }
 
-// The run's deliver offsets usually span far less than 2^32 ns: then (offset - min) and the
-// position in the run fit one 32-bit key (PB position bits), which halves every exchange.
+// Sort one destination run held in LDS (xs[0..n), n <= kWaveSeg) by one wave; writes the sorted
+// order as LDS positions pm[e] = base + position.  32-bit keys ((offset - min) << PB | position)
+// when the run's deliver offsets leave room for PB position bits, else 64-bit keys.
 template <int NPL, int PB>
-__device__ __forceinline__ void sort_run32(uint32_t n, uint32_t b, uint32_t lane, const uint4* x,
-                                           uint32_t dmin, uint64_t round_end,
-                                           const uint64_t* __restrict__ seq_base,
-                                           uint64_t* __restrict__ ev_deliver,
-                                           uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq,
-                                           uint32_t* __restrict__ ev_pkt) {
-    uint32_t k[NPL];
+__device__ __forceinline__ void wave_sort_perm(uint32_t n, uint32_t lane, const uint4* xs,
+                                               uint32_t lo, uint32_t span, uint16_t* pm,
+                                               uint32_t base) {
+    if (span < (1u << (32 - PB)) - 1u) {
+        uint32_t k[NPL];
 #pragma unroll
-    for (int c = 0; c < NPL; ++c) {
-        const uint32_t e = lane + 64u * c;
-        k[c] = e < n ? ((x[e].x - dmin) << PB) | e : ~0u;
-    }
-    wave_bitonic32<NPL>(k, lane);
+        for (int c = 0; c < NPL; ++c) {
+            const uint32_t e = lane + 64u * c;
+            k[c] = e < n ? ((xs[e].x - lo) << PB) | e : ~0u;
+        }
+        wave_bitonic32<NPL>(k, lane);
 #pragma unroll
-    for (int c = 0; c < NPL; ++c) {
-        const uint32_t e = lane + 64u * c;
-        if (e < n) {
-            const uint4 r = x[k[c] & ((1u << PB) - 1u)];
-            ev_deliver[b + e] = round_end + r.x;
-            ev_src[b + e] = r.y;
-            ev_seq[b + e] = seq_base[r.y] + r.z;
-            ev_pkt[b + e] = r.w;
+        for (int c = 0; c < NPL; ++c) {
+            const uint32_t e = lane + 64u * c;
+            if (e < n) pm[e] = (uint16_t)(base + (k[c] & ((1u << PB) - 1u)));
+        }
+    } else {
+        uint64_t k[NPL];
+#pragma unroll
+        for (int c = 0; c < NPL; ++c) {
+            const uint32_t e = lane + 64u * c;
+            k[c] = e < n ? (((uint64_t)xs[e].x << 32) | e) : ~0ull;
+        }
+        wave_bitonic<NPL>(k, lane);
+#pragma unroll
+        for (int c = 0; c < NPL; ++c) {
+            const uint32_t e = lane + 64u * c;
+            if (e < n) pm[e] = (uint16_t)(base + (uint32_t)k[c]);
         }
     }
 }
 
-// Persistent waves walk the destinations; runs longer than kWaveSeg go to the merge kernel.
-__global__ __launch_bounds__(256) void segment_sort_v4(
+__device__ __forceinline__ void wave_sort_run(uint32_t n, uint32_t lane, const uint4* xs,
+                                              uint16_t* pm, uint32_t base) {
+    uint32_t lo = ~0u, hi = 0;
+    for (uint32_t e = lane; e < n; e += 64) {
+        lo = min(lo, xs[e].x);
+        hi = max(hi, xs[e].x);
+    }
+    lo = wave_min_u32(lo, lane);
+    const uint32_t span = wave_max_u32(hi, lane) - lo;
+    if (n <= 64) wave_sort_perm<1, 6>(n, lane, xs, lo, span, pm, base);
+    else if (n <= 128) wave_sort_perm<2, 7>(n, lane, xs, lo, span, pm, base);
+    else wave_sort_perm<4, 8>(n, lane, xs, lo, span, pm, base);
+}
+
+// K4: a workgroup owns kSegDst consecutive destinations; their runs are one contiguous range of
+// the sorted records, so it is loaded and stored in bulk (coalesced) while each wave sorts whole
+// runs in LDS.  Runs longer than kWaveSeg go to the merge kernel; a range larger than the LDS
+// stage (only with such runs) is handled run by run.
+constexpr uint32_t kSegDst = 8;
+constexpr uint32_t kRunCap = 1536;
+
+__global__ __launch_bounds__(256) void segment_sort_v5(
     uint32_t n_hosts, const uint32_t* __restrict__ ev_off, const uint4* __restrict__ brec,
     uint64_t round_end, const uint64_t* __restrict__ seq_base, uint64_t* __restrict__ ev_deliver,
     uint32_t* __restrict__ ev_src, uint64_t* __restrict__ ev_seq, uint32_t* __restrict__ ev_pkt,
     uint32_t* __restrict__ big) {
-    __shared__ uint4 sr[4][kWaveSeg];
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t nwaves = gridDim.x * 4;
-    uint4* x = sr[w];
-    for (uint32_t d = blockIdx.x * 4 + w; d < n_hosts; d += nwaves) {
-        const uint32_t b = ev_off[d], n = ev_off[d + 1] - b;
+    __shared__ uint4 x[kRunCap];
+    __shared__ uint16_t pm[kRunCap];
+    __shared__ uint32_t off[kSegDst + 1];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t d0 = blockIdx.x * kSegDst;
+    const uint32_t nd = min(kSegDst, n_hosts - d0);
+    if (tid <= nd) off[tid] = ev_off[d0 + tid];
+    __syncthreads();
+    const uint32_t B = off[0], N = off[nd] - B;
+    if (N > kRunCap) {   // run by run through a per-wave stage
+        uint4* xw = x + w * kWaveSeg;
+        uint16_t* pw = pm + w * kWaveSeg;
+        for (uint32_t dl = w; dl < nd; dl += 4) {
+            const uint32_t b = off[dl], n = off[dl + 1] - b;
+            if (n == 0) continue;
+            if (n > kWaveSeg) {
+                if (lane == 0) big[atomicAdd(&big[0], 1u) + 1] = d0 + dl;
+                continue;
+            }
+            for (uint32_t e = lane; e < n; e += 64) xw[e] = brec[b + e];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            wave_sort_run(n, lane, xw, pw, 0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t e = lane; e < n; e += 64) {
+                const uint4 r = xw[pw[e]];
+                ev_deliver[b + e] = round_end + r.x;
+                ev_src[b + e] = r.y;
+                ev_seq[b + e] = seq_base ? seq_base[r.y] + r.z : r.z;
+                ev_pkt[b + e] = r.w;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        return;
+    }
+    for (uint32_t i = tid; i < N; i += 256) x[i] = brec[B + i];
+    __syncthreads();
+    for (uint32_t dl = w; dl < nd; dl += 4) {
+        const uint32_t b = off[dl] - B, n = off[dl + 1] - off[dl];
         if (n == 0) continue;
-        if (n > kWaveSeg) {
-            if (lane == 0) big[atomicAdd(&big[0], 1u) + 1] = d;
+        if (n > kWaveSeg) {   // the merge kernel writes this run; the bulk store skips it
+            if (lane == 0) big[atomicAdd(&big[0], 1u) + 1] = d0 + dl;
+            for (uint32_t e = lane; e < n; e += 64) pm[b + e] = 0xFFFFu;
             continue;
         }
-        uint32_t lo = ~0u, hi = 0;
-        for (uint32_t e = lane; e < n; e += 64) {
-            const uint4 v = brec[b + e];
-            x[e] = v;
-            lo = min(lo, v.x);
-            hi = max(hi, v.x);
-        }
-        lo = wave_min_u32(lo, lane);
-        const uint32_t span = wave_max_u32(hi, lane) - lo;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // 32-bit keys (offset - min) << PB | position when the span leaves room for PB bits
-        if (n <= 64) {
-            if (span < (1u << 26) - 1u)
-                sort_run32<1, 6>(n, b, lane, x, lo, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
-            else
-                sort_run<1>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
-        } else if (n <= 128) {
-            if (span < (1u << 25) - 1u)
-                sort_run32<2, 7>(n, b, lane, x, lo, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
-            else
-                sort_run<2>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
-        } else {
-            if (span < (1u << 24) - 1u)
-                sort_run32<4, 8>(n, b, lane, x, lo, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
-            else
-                sort_run<4>(n, b, lane, x, round_end, seq_base, ev_deliver, ev_src, ev_seq, ev_pkt);
-        }
-        __builtin_amdgcn_wave_barrier();
+        wave_sort_run(n, lane, x + b, pm + b, b);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < N; i += 256) {
+        const uint32_t p = pm[i];
+        if (p == 0xFFFFu) continue;
+        const uint4 r = x[p];
+        ev_deliver[B + i] = round_end + r.x;
+        ev_src[B + i] = r.y;
+        ev_seq[B + i] = seq_base ? seq_base[r.y] + r.z : r.z;
+        ev_pkt[B + i] = r.w;
     }
 }
+
 // Runs longer than kWaveSeg: bottom-up merge passes by one workgroup in a
 // global scratch copy of the bucket (rank by binary search in the sibling run; keys unique).
 __global__ __launch_bounds__(256) void segment_sort_v2_big(
@@ -797,7 +848,7 @@ __global__ __launch_bounds__(256) void segment_sort_v2_big(
             const uint4 e = A[i];
             ev_deliver[b + i] = round_end + e.x;
             ev_src[b + i] = e.y;
-            ev_seq[b + i] = seq_base[e.y] + e.z;
+            ev_seq[b + i] = seq_base ? seq_base[e.y] + e.z : e.z;
             ev_pkt[b + i] = e.w;
         }
         __syncthreads();
@@ -1028,27 +1079,19 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.round_end = rd->round_end;
     a.sim_end = rd->sim_end;
     a.bootstrap_end = rd->bootstrap_end;
+    // event ids below 2^32 for the whole round: records carry absolute ids, no per-event gather
+    a.abs_seq = R.seq_bound + n < (1ull << 32) ? 1u : 0u;
+    const uint64_t* seq_base = a.abs_seq ? nullptr : R.next_id.as<uint64_t>();
     a.status = o->status;
     a.rec = R.rec.as<uint4>();
     a.key = R.ev_val.as<uint32_t>();
     a.red = R.red.as<unsigned long long>();
-    const char* pe = std::getenv("SHD_RELAY_PROF");
-    const bool prof = pe && *pe == '1';
-    if (prof) {
-        SHD_TRY(R.tmp.ensure(64));
-        SHD_HIP(hipMemsetAsync(R.tmp.p, 0, 64, s));
-        a.prof = R.tmp.as<unsigned long long>();
+    if (!b->chance) {   // K0: the per-host generator streams
+        SHD_TRY(R.draws.ensure(nn * 8));
+        relay_draws<<<div_up(H, 64), 64, 0, s>>>(a, R.draws.as<uint64_t>());
     }
-    relay_stamp_v3<<<div_up(H, kS3Hosts), 256, 0, s>>>(a);
+    relay_stamp_v5<<<div_up(H, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint64_t>());
     SHD_HIP(hipGetLastError());
-    if (prof) {
-        unsigned long long p[6];
-        SHD_HIP(hipMemcpyAsync(p, R.tmp.p, 48, hipMemcpyDeviceToHost, s));
-        SHD_HIP(hipStreamSynchronize(s));
-        std::fprintf(stderr, "relay_stamp_v3 prof: WGs=%llu chunks/WG=%.1f  per chunk: ab=%.0f c=%.0f d=%.0f "
-                     "cycles (s_memtime)  per WG total=%.0f\n", p[4], (double)p[3] / p[4],
-                     (double)p[0] / p[3], (double)p[1] / p[3], (double)p[2] / p[3], (double)p[5] / p[4]);
-    }
     // stable LSD radix sort of the records by destination (keys <= H)
     uint32_t bits = 1;
     while (bits < 32 && (H >> bits) != 0) ++bits;
@@ -1062,11 +1105,11 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     uint4* sorted = vb.current();
     uint4* spare = sorted == R.rec.as<uint4>() ? R.brec.as<uint4>() : R.rec.as<uint4>();
     bucket_offsets<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(kb.current(), n, H, o->ev_off);
-    segment_sort_v4<<<std::min<uint32_t>(div_up(H, 4), (uint32_t)ctx->n_cu * 6), 256, 0, s>>>(
-        H, o->ev_off, sorted, rd->round_end, R.next_id.as<uint64_t>(), o->ev_deliver, o->ev_src,
+    segment_sort_v5<<<div_up(H, kSegDst), 256, 0, s>>>(
+        H, o->ev_off, sorted, rd->round_end, seq_base, o->ev_deliver, o->ev_src,
         o->ev_seq, o->ev_pkt, R.ev_val2.as<uint32_t>());
     segment_sort_v2_big<<<64, 256, 0, s>>>(R.ev_val2.as<uint32_t>(), o->ev_off, sorted,
-                                           spare, rd->round_end, R.next_id.as<uint64_t>(),
+                                           spare, rd->round_end, seq_base,
                                            o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt);
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipMemcpyAsync(R.red_host, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -1090,8 +1133,10 @@ static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round
     }
     if (!v2) SHD_TRY(relay_device_v1(ctx, b, rd, o));
     if (R.red_host[3] != ~0ull) return SHD_ERR_NO_HOST;
+    if (v2 && R.red_host[5]) return SHD_ERR_INVALID;   // a host's send times went backwards
     std::swap(R.rng, R.rng2);
     std::swap(R.next_id, R.next_id2);
+    R.seq_bound += R.red_host[2];
     o->min_deliver = R.red_host[0];
     o->min_latency = R.red_host[1];
     o->n_sent = R.red_host[2];
@@ -1145,6 +1190,8 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
     }
     SHD_HIP(hipMemcpyAsync(R.rng.p, rng_state, (size_t)n_hosts * 32, hipMemcpyHostToDevice, s));
     SHD_HIP(hipMemcpyAsync(R.next_id.p, next_event_id, (size_t)n_hosts * 8, hipMemcpyHostToDevice, s));
+    R.seq_bound = 0;   // upper bound of every next event id (grows by n_sent per round)
+    for (uint32_t h = 0; h < n_hosts; h++) R.seq_bound = std::max<uint64_t>(R.seq_bound, next_event_id[h]);
     SHD_HIP(hipMemsetAsync(R.counts.p, 0, (size_t)n_nodes * n_nodes * 8, s));
     SHD_HIP(hipStreamSynchronize(s));
     R.n_hosts = n_hosts;

@@ -179,3 +179,58 @@ def test_bucket_size_classes(engine, n_hosts):
     for k in ("deliver", "src", "seq", "pkt"):
         assert np.array_equal(getattr(r, "ev_" + k), ev[k]), k
     del synth
+
+
+def test_many_source_nodes_per_workgroup(engine):
+    """One host per node on a 3000-node table: a stamp workgroup's source rows do not fit the
+    LDS stage, so the path gathers go to global memory (the other tests use the staged rows)."""
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    NN = 3000
+    el = synth.barabasi_albert(NN, 2, 23)
+    used = np.arange(NN, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(NN, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    H = NN
+    b = synth.packet_batch(H, 300_000, 10**9, 10**9 + 10**6, seed=29)
+    host_node = np.random.default_rng(3).permutation(NN).astype(np.uint32)
+    rng0 = synth.host_rng_states(H, 1)
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss,
+                         rng0.copy(), np.zeros(H, np.uint64), 10**9 + 10**6, 10**12, 0)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, 10**9 + 10**6, 10**12, 0)
+    assert np.array_equal(r.status, o["status"])
+    ev = o["events"]
+    assert np.array_equal(r.ev_off, ev["off"])
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(r, "ev_" + k), ev[k]), k
+
+
+def test_sim_end_inside_round_and_wide_event_ids(engine):
+    """sim_end falls inside the round: every host's sends from sim_end on are skipped (no draw,
+    worker.rs:334-341).  Event ids start above 2^40, so records carry relative ids."""
+    from shadow_amd.relay import Relay
+    from shadow_amd._native import ShdError
+    H, NN = 4000, 100
+    lat, loss, host_node, rng0, b = _c5_like(H, NN, 400_000, 19)
+    nid0 = (np.uint64(1) << np.uint64(40)) + np.arange(H, dtype=np.uint64) * np.uint64(1000)
+    sim_end = 10**9 + 6 * 10**5                      # 60% into the send window
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss,
+                         rng0.copy(), nid0.copy(), 10**9 + 10**6, sim_end, 0)
+    assert 0 < int((o["status"] == 0).sum()) < len(b.send_time)
+    rl = Relay(host_node, rng0, nid0, lat, loss, engine=engine)
+    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, 10**9 + 10**6, sim_end, 0)
+    assert np.array_equal(r.status, o["status"])
+    ev = o["events"]
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(r, "ev_" + k), ev[k]), k
+    st, nid = rl.host_state()
+    # a drawing send after a skipped one (send times going backwards) is rejected, state kept
+    t = b.send_time.copy()
+    h = int(np.argmax(np.diff(b.src_off) > 3))
+    a0 = int(b.src_off[h])
+    t[a0], t[a0 + 1] = np.uint64(sim_end + 5), np.uint64(sim_end - 5)
+    with pytest.raises(ShdError, match="INVALID"):
+        rl.round(b.src_off, t, b.dst_host, b.payload, 10**9 + 10**6, sim_end, 0)
+    st2, nid2 = rl.host_state()
+    assert np.array_equal(st, st2) and np.array_equal(nid, nid2)
