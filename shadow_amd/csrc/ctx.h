@@ -50,8 +50,9 @@ struct RelayState {
     bool count_on = true;       // per-path packet counters (RoutingInfo::increment_packet_count)
     bool last_v2 = false;
     uint64_t seq_bound = 0;     // >= every host's next event id
+    uint32_t hn_bits = 0, hn_words = 0;   // packed host -> node map (0 bits: not used)
     unsigned long long red_host[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    DevBuf host_node, order, lat, loss, path, rng, next_id, rng2, next_id2, counts;
+    DevBuf host_node, order, hn_packed, lat, loss, path, rng, next_id, rng2, next_id2, counts;
     // per-round scratch
     DevBuf pk_off, pk_time, pk_dst, pk_pay, pk_chance, st, ev_key, ev_key2, ev_val, ev_val2,
         ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, scan_tmp, red, rec, brec, tmp, draws;

@@ -556,6 +556,216 @@ __global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint64
     }
 }
 
+// K1 (small node count): relay_stamp_v6 is relay_stamp_v5 with the host -> node map resident in
+// LDS, bit-packed at ceil(log2 n_nodes) bits per host (C5: 100k hosts x 10 bits = 125 KB), so
+// the destination-node lookup -- otherwise one random 64-byte L2 request per send, the stamp's
+// dominant cost -- becomes an LDS read.  One persistent 1024-thread workgroup per CU loads the
+// packed map once and walks the host groups (kS5Hosts hosts each, in source-node order).
+constexpr uint32_t kS6Threads = 1024;
+constexpr uint32_t kS6Per = 4;
+constexpr uint32_t kS6Cap = kS6Threads * kS6Per;
+constexpr uint32_t kS6FixedLds = kS5RowLds * 8 + (kS6Cap + 2) * 2 + 4096;   // rows + scan + small
+
+__device__ __forceinline__ uint32_t packed_get(const uint32_t* t, uint32_t j, uint32_t bits) {
+    const uint32_t o = j * bits, w = o >> 5, sh = o & 31;
+    uint64_t v = t[w];
+    if (sh + bits > 32) v |= (uint64_t)t[w + 1] << 32;
+    return (uint32_t)(v >> sh) & ((1u << bits) - 1u);
+}
+
+__global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const uint64_t* __restrict__ draw,
+                                                             const uint32_t* __restrict__ packed,
+                                                             uint32_t n_words, uint32_t bits) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_tbl[];   // packed host -> node
+    __shared__ uint2 s_rows[kS5RowLds];
+    __shared__ uint16_t s_scan[kS6Cap + 1];
+    __shared__ uint32_t s_host[kS5Hosts], s_beg[kS5Hosts], s_pre[kS5Hosts + 1], s_node[kS5Hosts];
+    __shared__ uint32_t s_rowof[kS5Hosts], s_rownode[kS5Hosts], s_run[kS5Hosts], s_base[kS5Hosts];
+    __shared__ uint32_t s_wsum[kS6Threads / 64], s_nrows;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (uint32_t i = tid; i < n_words; i += kS6Threads) s_tbl[i] = packed[i];
+    const uint32_t n_groups = (a.n_hosts + kS5Hosts - 1) / kS5Hosts;
+    uint64_t min_d = ~0ull, min_l = ~0ull, ns_total = 0;
+    bool wide = false, disorder = false;
+    for (uint32_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
+        const uint32_t h0 = grp * kS5Hosts;
+        const uint32_t nh = min(kS5Hosts, a.n_hosts - h0);
+        __syncthreads();   // the previous group's host arrays / rows are no longer read
+        if (tid < 64) {
+            uint32_t len = 0, nd = 0;
+            if (tid < nh) {
+                const uint32_t h = a.order[h0 + tid];
+                const uint32_t b = a.src_off[h];
+                len = a.src_off[h + 1] - b;
+                nd = a.host_node[h];
+                s_host[tid] = h;
+                s_beg[tid] = b;
+                s_node[tid] = nd;
+                s_run[tid] = 0;
+                s_base[tid] = a.abs_seq ? (uint32_t)a.next_id[h] : 0u;
+            }
+            uint32_t incl = len;
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (tid < nh) s_pre[tid + 1] = incl;
+            if (tid == 0) s_pre[0] = 0;
+            const uint32_t prev = __shfl_up(nd, 1);
+            const bool first = tid < nh && (tid == 0 || nd != prev);
+            const uint64_t fm = __ballot(first);
+            if (tid < nh) {
+                const uint32_t ri = (uint32_t)__popcll(fm & ((2ull << tid) - 1ull)) - 1u;
+                s_rowof[tid] = ri;
+                if (first) s_rownode[ri] = nd;
+            }
+            if (tid == 0) s_nrows = (uint32_t)__popcll(fm);
+        }
+        __syncthreads();
+        const bool staged = (uint64_t)s_nrows * a.n_nodes <= kS5RowLds;
+        if (staged) {
+            const uint32_t tot = s_nrows * a.n_nodes;
+            for (uint32_t e = tid; e < tot; e += kS6Threads) {
+                const uint32_t rr = e / a.n_nodes, c = e - rr * a.n_nodes;
+                s_rows[e] = a.path[(size_t)s_rownode[rr] * a.n_nodes + c];
+            }
+        }
+        __syncthreads();
+        const uint32_t T = s_pre[nh];
+        for (uint32_t c0 = 0; c0 < T; c0 += kS6Cap) {
+            const uint32_t cn = min(kS6Cap, T - c0);
+            uint8_t st[kS6Per];
+            uint32_t doff[kS6Per], dst[kS6Per], idx[kS6Per], hl[kS6Per], dn[kS6Per];
+#pragma unroll
+            for (uint32_t i = 0; i < kS6Per; ++i) {
+                const uint32_t pos = tid + kS6Threads * i;
+                st[i] = kStSkipped;
+                doff[i] = dst[i] = idx[i] = hl[i] = dn[i] = 0;
+                if (pos < cn) {
+                    const uint32_t gp = c0 + pos;
+                    uint32_t lo = 0, hi = nh;       // s_pre[lo] <= gp < s_pre[lo + 1]
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_pre[mid] <= gp) lo = mid; else hi = mid;
+                    }
+                    hl[i] = lo;
+                    const uint32_t k = gp - s_pre[lo];
+                    idx[i] = s_beg[lo] + k;
+                    const uint64_t now = a.send_time[idx[i]];
+                    dst[i] = a.dst_host[idx[i]];
+                    const uint32_t pay = a.payload[idx[i]];
+                    // a drawing send after a skipped one breaks K0's prefix rule
+                    if (k > 0 && now < a.sim_end && !(a.send_time[idx[i] - 1] < a.sim_end)) disorder = true;
+                    if (dst[i] >= a.n_hosts) {      // "No host ID for dest address" (worker.rs:350-355)
+                        atomicMin(&a.red[3], (unsigned long long)idx[i]);
+                    } else if (now < a.sim_end) {
+                        dn[i] = packed_get(s_tbl, dst[i], bits);
+                        const uint2 pp = staged ? s_rows[s_rowof[lo] * a.n_nodes + dn[i]]
+                                                : a.path[(size_t)s_node[lo] * a.n_nodes + dn[i]];
+                        const double reliability = (double)one_minus(__uint_as_float(pp.y));
+                        const double ch = a.chance ? a.chance[idx[i]]
+                                                   : (double)(draw[idx[i]] >> 11) * (1.0 / 9007199254740992.0);
+                        if (!(now < a.bootstrap_end) && ch >= reliability && pay > 0) {
+                            st[i] = kStDropped;
+                        } else {
+                            uint64_t tt = now + pp.x;
+                            if (tt < a.round_end) tt = a.round_end;
+                            const uint64_t dd = tt - a.round_end;
+                            wide |= (dd >> 32) != 0;
+                            min_d = tt < min_d ? tt : min_d;
+                            min_l = pp.x < min_l ? pp.x : min_l;
+                            doff[i] = (uint32_t)dd;
+                            st[i] = kStSent;
+                        }
+                    }
+                }
+                s_scan[pos] = st[i] == kStSent ? 1 : 0;
+            }
+            __syncthreads();
+            {   // block-wide exclusive scan of the sent flags (kS6Per consecutive entries per thread)
+                uint32_t v[kS6Per], sum = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < kS6Per; ++i) {
+                    v[i] = s_scan[tid * kS6Per + i];
+                    sum += v[i];
+                }
+                uint32_t incl = sum;
+#pragma unroll
+                for (uint32_t o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(incl, o);
+                    if (lane >= o) incl += y;
+                }
+                if (lane == 63) s_wsum[w] = incl;
+                __syncthreads();
+                uint32_t run = incl - sum;
+                for (uint32_t ww = 0; ww < w; ++ww) run += s_wsum[ww];
+#pragma unroll
+                for (uint32_t i = 0; i < kS6Per; ++i) {
+                    s_scan[tid * kS6Per + i] = (uint16_t)run;
+                    run += v[i];
+                }
+                if (tid == kS6Threads - 1) s_scan[kS6Cap] = (uint16_t)run;
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t i = 0; i < kS6Per; ++i) {
+                const uint32_t pos = tid + kS6Threads * i;
+                if (pos < cn) {
+                    a.status[idx[i]] = st[i];
+                    a.key[idx[i]] = st[i] == kStSent ? dst[i] : a.n_hosts;
+                    if (st[i] == kStSent) {
+                        const uint32_t first = max(s_pre[hl[i]], c0) - c0;
+                        const uint32_t local = s_base[hl[i]] + s_run[hl[i]] + s_scan[pos] - s_scan[first];
+                        a.rec[idx[i]] = make_uint4(doff[i], s_host[hl[i]], local, idx[i]);
+                        if (a.counts) atomicAdd(&a.counts[(size_t)s_node[hl[i]] * a.n_nodes + dn[i]], 1ull);
+                    }
+                }
+            }
+            __syncthreads();
+            if (tid < nh) {
+                const uint32_t pb = max(s_pre[tid], c0), pe = min(s_pre[tid + 1], c0 + cn);
+                if (pe > pb) s_run[tid] += s_scan[pe - c0] - s_scan[pb - c0];
+            }
+            __syncthreads();
+        }
+        if (tid < nh) {
+            const size_t h = s_host[tid];
+            if (a.chance)
+                for (int k = 0; k < 4; ++k) a.rng_out[4 * h + k] = a.rng[4 * h + k];
+            ns_total += s_run[tid];
+            a.next_id_out[h] = a.next_id[h] + s_run[tid];
+        }
+    }
+    min_d = wave_min_u64(min_d);
+    min_l = wave_min_u64(min_l);
+    for (int o = 32; o > 0; o >>= 1) ns_total += __shfl_xor(ns_total, o);
+    const bool any_wide = __ballot(wide) != 0, any_disorder = __ballot(disorder) != 0;
+    if (lane == 0) {
+        if (min_d != ~0ull) atomicMin(&a.red[0], (unsigned long long)min_d);
+        if (min_l != ~0ull) atomicMin(&a.red[1], (unsigned long long)min_l);
+        if (ns_total) atomicAdd(&a.red[2], (unsigned long long)ns_total);
+        if (any_wide) atomicOr(&a.red[4], 1ull);
+        if (any_disorder) atomicOr(&a.red[5], 1ull);
+    }
+}
+
+// the bit-packed host -> node map for relay_stamp_v6 (built at setup)
+__global__ __launch_bounds__(256) void pack_host_node(const uint32_t* __restrict__ host_node,
+                                                      uint32_t n_hosts, uint32_t bits,
+                                                      uint32_t n_words, uint32_t* __restrict__ out) {
+    const uint32_t wi = blockIdx.x * 256 + threadIdx.x;
+    if (wi >= n_words) return;
+    // word wi holds bits [32 wi, 32 wi + 32) of the concatenated entries
+    const uint64_t b0 = (uint64_t)wi * 32;
+    uint32_t word = 0;
+    for (uint64_t j = b0 / bits; j < n_hosts && j * bits < b0 + 32; ++j) {
+        const int64_t sh = (int64_t)(j * bits) - (int64_t)b0;
+        const uint64_t v = host_node[j];
+        word |= sh >= 0 ? (uint32_t)(v << sh) : (uint32_t)(v >> -sh);
+    }
+    out[wi] = word;
+}
+
 // pack the routing table for the narrow pipeline: one 8-byte gather per packet
 __global__ __launch_bounds__(256) void pack_path(const uint64_t* __restrict__ lat,
                                                  const float* __restrict__ loss, uint64_t nn,
@@ -1090,7 +1300,14 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
         SHD_TRY(R.draws.ensure(nn * 8));
         relay_draws<<<div_up(H, 64), 64, 0, s>>>(a, R.draws.as<uint64_t>());
     }
-    relay_stamp_v5<<<div_up(H, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint64_t>());
+    if (R.hn_bits) {   // host -> node map fits the LDS: persistent stamp, no node gathers
+        const uint32_t groups = div_up(H, kS5Hosts);
+        relay_stamp_v6<<<std::min<uint32_t>(groups, (uint32_t)ctx->n_cu), kS6Threads,
+                         (size_t)R.hn_words * 4, s>>>(a, R.draws.as<uint64_t>(),
+                                                      R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
+    } else {
+        relay_stamp_v5<<<div_up(H, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint64_t>());
+    }
     SHD_HIP(hipGetLastError());
     // stable LSD radix sort of the records by destination (keys <= H)
     uint32_t bits = 1;
@@ -1218,6 +1435,22 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
     {
         const char* v = std::getenv("SHD_RELAY_FORCE_V1");
         R.force_v1 = v && *v == '1';
+    }
+    {   // bit-packed host -> node map for the LDS-resident stamp, when it fits
+        uint32_t bits = 1;
+        while (bits < 32 && (n_nodes - 1) >> bits) ++bits;
+        const uint64_t words = ((uint64_t)n_hosts * bits + 31) / 32 + 1;
+        const char* v = std::getenv("SHD_RELAY_NO_LDS_MAP");   // testing: force the gather path
+        R.hn_bits = 0;
+        if (words * 4 + kS6FixedLds <= ctx->max_lds && !(v && *v == '1')) {
+            SHD_TRY(R.hn_packed.ensure(words * 4));
+            pack_host_node<<<div_up(words, 256), 256, 0, s>>>(R.host_node.as<uint32_t>(), n_hosts, bits,
+                                                              (uint32_t)words, R.hn_packed.as<uint32_t>());
+            SHD_HIP(hipGetLastError());
+            SHD_HIP(hipStreamSynchronize(s));
+            R.hn_bits = bits;
+            R.hn_words = (uint32_t)words;
+        }
     }
     R.ready = true;
     return SHD_OK;

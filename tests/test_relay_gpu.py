@@ -158,12 +158,15 @@ def test_wide_latency_table_and_failed_round_keeps_state(engine):
     del synth
 
 
+@pytest.mark.parametrize("lds_map", [True, False])
 @pytest.mark.parametrize("n_hosts", [300, 2000, 5000])
-def test_bucket_size_classes(engine, n_hosts):
+def test_bucket_size_classes(engine, n_hosts, lds_map, monkeypatch):
     """Destination runs of every size class of the per-run sort (<= 64, <= 128, <= 256 events
-    per destination, and longer runs on the merge path) against the C restatement."""
+    per destination, and longer runs on the merge path) against the C restatement; both stamp
+    kernels (host -> node map resident in LDS, or gathered from global memory)."""
     from shadow_amd import synth
     from shadow_amd.relay import Relay
+    monkeypatch.setenv("SHD_RELAY_NO_LDS_MAP", "0" if lds_map else "1")
     NN = 50
     lat, loss, host_node, rng0, b = _c5_like(n_hosts, NN, 400_000, 13)
     nid0 = np.arange(n_hosts, dtype=np.uint64) * np.uint64(7)
