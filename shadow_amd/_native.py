@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libshd_accel.so")
+LIB_PATH = os.environ.get("SHD_ACCEL_LIB") or os.path.join(HERE, "libshd_accel.so")  # override: tuning builds
 
 SHD_OK = 0
 STATUS_NAMES = {0: "OK", 1: "NO_EDGE", 2: "MULTI_EDGE", 3: "UNREACHABLE", 4: "LATENCY_OVERFLOW",

@@ -573,6 +573,15 @@ __device__ __forceinline__ uint32_t packed_get(const uint32_t* t, uint32_t j, ui
     return (uint32_t)(v >> sh) & ((1u << bits) - 1u);
 }
 
+#ifdef SHD_STAMP_PROF
+// tuning builds only (tools/stamp_prof.sh): shader clocks per phase, summed over workgroups
+__device__ unsigned long long g_stamp_prof[12];
+#define SP_MARK(slot) do { if (threadIdx.x == 0) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    sp_acc[slot] += t_ - sp_t; sp_t = t_; } } while (0)
+#else
+#define SP_MARK(slot) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const uint64_t* __restrict__ draw,
                                                              const uint32_t* __restrict__ packed,
                                                              uint32_t n_words, uint32_t bits) {
@@ -583,27 +592,50 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     __shared__ uint32_t s_rowof[kS5Hosts], s_rownode[kS5Hosts], s_run[kS5Hosts], s_base[kS5Hosts];
     __shared__ uint32_t s_wsum[kS6Threads / 64], s_nrows;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    #ifdef SHD_STAMP_PROF
+    uint64_t sp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, sp_t = __builtin_amdgcn_s_memtime();
+#endif
     for (uint32_t i = tid; i < n_words; i += kS6Threads) s_tbl[i] = packed[i];
     const uint32_t n_groups = (a.n_hosts + kS5Hosts - 1) / kS5Hosts;
     uint64_t min_d = ~0ull, min_l = ~0ull, ns_total = 0;
     bool wide = false, disorder = false;
+    // wave 0 keeps the next group's host descriptors in registers: order[] is fetched when a
+    // group starts and the dependent src_off / host_node / next_id loads are issued once its
+    // path rows are staged, so neither latency sits on the critical path of the next group
+    uint32_t p_h = 0, p_b = 0, p_len = 0, p_nd = 0, p_base = 0;
+    auto fetch_hosts = [&](uint32_t g) {
+        const uint32_t hh0 = g * kS5Hosts;
+        if (g < n_groups && tid < min(kS5Hosts, a.n_hosts - hh0)) {
+            p_b = a.src_off[p_h];
+            p_len = a.src_off[p_h + 1] - p_b;
+            p_nd = a.host_node[p_h];
+            p_base = a.abs_seq ? (uint32_t)a.next_id[p_h] : 0u;
+        }
+    };
+    if (tid < 64 && blockIdx.x < n_groups && tid < min(kS5Hosts, a.n_hosts - blockIdx.x * kS5Hosts)) {
+        p_h = a.order[blockIdx.x * kS5Hosts + tid];
+    }
+    if (tid < 64) fetch_hosts(blockIdx.x);
+    const uint64_t* __restrict__ rsrc = a.chance ? reinterpret_cast<const uint64_t*>(a.chance) : draw;
     for (uint32_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
         const uint32_t h0 = grp * kS5Hosts;
         const uint32_t nh = min(kS5Hosts, a.n_hosts - h0);
+        const uint32_t nxt = grp + gridDim.x;
         __syncthreads();   // the previous group's host arrays / rows are no longer read
+        SP_MARK(0);
         if (tid < 64) {
             uint32_t len = 0, nd = 0;
             if (tid < nh) {
-                const uint32_t h = a.order[h0 + tid];
-                const uint32_t b = a.src_off[h];
-                len = a.src_off[h + 1] - b;
-                nd = a.host_node[h];
-                s_host[tid] = h;
-                s_beg[tid] = b;
+                len = p_len;
+                nd = p_nd;
+                s_host[tid] = p_h;
+                s_beg[tid] = p_b;
                 s_node[tid] = nd;
                 s_run[tid] = 0;
-                s_base[tid] = a.abs_seq ? (uint32_t)a.next_id[h] : 0u;
+                s_base[tid] = p_base;
             }
+            if (nxt < n_groups && tid < min(kS5Hosts, a.n_hosts - nxt * kS5Hosts))
+                p_h = a.order[nxt * kS5Hosts + tid];
             uint32_t incl = len;
             for (uint32_t o = 1; o < 64; o <<= 1) {
                 const uint32_t y = __shfl_up(incl, o);
@@ -622,6 +654,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
             if (tid == 0) s_nrows = (uint32_t)__popcll(fm);
         }
         __syncthreads();
+        SP_MARK(1);
         const bool staged = (uint64_t)s_nrows * a.n_nodes <= kS5RowLds;
         if (staged) {
             const uint32_t tot = s_nrows * a.n_nodes;
@@ -630,45 +663,64 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 s_rows[e] = a.path[(size_t)s_rownode[rr] * a.n_nodes + c];
             }
         }
+        if (tid < 64) fetch_hosts(nxt);
         __syncthreads();
+        SP_MARK(2);
         const uint32_t T = s_pre[nh];
         for (uint32_t c0 = 0; c0 < T; c0 += kS6Cap) {
             const uint32_t cn = min(kS6Cap, T - c0);
+            // (a) positions -> packet indices (positions past the chunk end are clamped onto its
+            // last packet so that every load below is in bounds and issued unconditionally)
+            uint32_t idx[kS6Per], hl[kS6Per], kk[kS6Per];
+#pragma unroll
+            for (uint32_t i = 0; i < kS6Per; ++i) {
+                const uint32_t gp = c0 + min(tid + kS6Threads * i, cn - 1);
+                uint32_t lo = 0, hi = nh;           // s_pre[lo] <= gp < s_pre[lo + 1]
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_pre[mid] <= gp) lo = mid; else hi = mid;
+                }
+                hl[i] = lo;
+                kk[i] = gp - s_pre[lo];
+                idx[i] = s_beg[lo] + kk[i];
+            }
+            SP_MARK(8);
+            // (b) all loads of the chunk in flight together
+            uint64_t now[kS6Per], prv[kS6Per], rv[kS6Per];
+            uint32_t dst[kS6Per], pay[kS6Per];
+#pragma unroll
+            for (uint32_t i = 0; i < kS6Per; ++i) {
+                now[i] = a.send_time[idx[i]];
+                prv[i] = a.send_time[idx[i] - (kk[i] > 0 ? 1u : 0u)];
+                dst[i] = a.dst_host[idx[i]];
+                pay[i] = a.payload[idx[i]];
+                rv[i] = rsrc[idx[i]];
+            }
+            SP_MARK(9);
+            // (c) decisions
             uint8_t st[kS6Per];
-            uint32_t doff[kS6Per], dst[kS6Per], idx[kS6Per], hl[kS6Per], dn[kS6Per];
+            uint32_t doff[kS6Per], dn[kS6Per];
 #pragma unroll
             for (uint32_t i = 0; i < kS6Per; ++i) {
                 const uint32_t pos = tid + kS6Threads * i;
                 st[i] = kStSkipped;
-                doff[i] = dst[i] = idx[i] = hl[i] = dn[i] = 0;
+                doff[i] = dn[i] = 0;
                 if (pos < cn) {
-                    const uint32_t gp = c0 + pos;
-                    uint32_t lo = 0, hi = nh;       // s_pre[lo] <= gp < s_pre[lo + 1]
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (s_pre[mid] <= gp) lo = mid; else hi = mid;
-                    }
-                    hl[i] = lo;
-                    const uint32_t k = gp - s_pre[lo];
-                    idx[i] = s_beg[lo] + k;
-                    const uint64_t now = a.send_time[idx[i]];
-                    dst[i] = a.dst_host[idx[i]];
-                    const uint32_t pay = a.payload[idx[i]];
                     // a drawing send after a skipped one breaks K0's prefix rule
-                    if (k > 0 && now < a.sim_end && !(a.send_time[idx[i] - 1] < a.sim_end)) disorder = true;
+                    if (kk[i] > 0 && now[i] < a.sim_end && !(prv[i] < a.sim_end)) disorder = true;
                     if (dst[i] >= a.n_hosts) {      // "No host ID for dest address" (worker.rs:350-355)
                         atomicMin(&a.red[3], (unsigned long long)idx[i]);
-                    } else if (now < a.sim_end) {
+                    } else if (now[i] < a.sim_end) {
                         dn[i] = packed_get(s_tbl, dst[i], bits);
-                        const uint2 pp = staged ? s_rows[s_rowof[lo] * a.n_nodes + dn[i]]
-                                                : a.path[(size_t)s_node[lo] * a.n_nodes + dn[i]];
+                        const uint2 pp = staged ? s_rows[s_rowof[hl[i]] * a.n_nodes + dn[i]]
+                                                : a.path[(size_t)s_node[hl[i]] * a.n_nodes + dn[i]];
                         const double reliability = (double)one_minus(__uint_as_float(pp.y));
-                        const double ch = a.chance ? a.chance[idx[i]]
-                                                   : (double)(draw[idx[i]] >> 11) * (1.0 / 9007199254740992.0);
-                        if (!(now < a.bootstrap_end) && ch >= reliability && pay > 0) {
+                        const double ch = a.chance ? __longlong_as_double((long long)rv[i])
+                                                   : (double)(rv[i] >> 11) * (1.0 / 9007199254740992.0);
+                        if (!(now[i] < a.bootstrap_end) && ch >= reliability && pay[i] > 0) {
                             st[i] = kStDropped;
                         } else {
-                            uint64_t tt = now + pp.x;
+                            uint64_t tt = now[i] + pp.x;
                             if (tt < a.round_end) tt = a.round_end;
                             const uint64_t dd = tt - a.round_end;
                             wide |= (dd >> 32) != 0;
@@ -681,7 +733,9 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 }
                 s_scan[pos] = st[i] == kStSent ? 1 : 0;
             }
+            SP_MARK(10);
             __syncthreads();
+            SP_MARK(3);
             {   // block-wide exclusive scan of the sent flags (kS6Per consecutive entries per thread)
                 uint32_t v[kS6Per], sum = 0;
 #pragma unroll
@@ -707,6 +761,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 if (tid == kS6Threads - 1) s_scan[kS6Cap] = (uint16_t)run;
             }
             __syncthreads();
+            SP_MARK(4);
 #pragma unroll
             for (uint32_t i = 0; i < kS6Per; ++i) {
                 const uint32_t pos = tid + kS6Threads * i;
@@ -722,11 +777,13 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 }
             }
             __syncthreads();
+            SP_MARK(5);
             if (tid < nh) {
                 const uint32_t pb = max(s_pre[tid], c0), pe = min(s_pre[tid + 1], c0 + cn);
                 if (pe > pb) s_run[tid] += s_scan[pe - c0] - s_scan[pb - c0];
             }
             __syncthreads();
+            SP_MARK(6);
         }
         if (tid < nh) {
             const size_t h = s_host[tid];
@@ -736,6 +793,11 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
             a.next_id_out[h] = a.next_id[h] + s_run[tid];
         }
     }
+#ifdef SHD_STAMP_PROF
+    SP_MARK(7);
+    if (tid == 0)
+        for (int q = 0; q < 12; ++q) atomicAdd(&g_stamp_prof[q], (unsigned long long)sp_acc[q]);
+#endif
     min_d = wave_min_u64(min_d);
     min_l = wave_min_u64(min_l);
     for (int o = 32; o > 0; o >>= 1) ns_total += __shfl_xor(ns_total, o);
@@ -1584,3 +1646,14 @@ shd_status shd_path_packet_counts(shd_ctx* ctx, uint64_t* counts) {
 }
 
 }  // extern "C"
+
+#ifdef SHD_STAMP_PROF
+extern "C" int shd_debug_stamp_prof(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(shd::g_stamp_prof), sizeof(unsigned long long) * 12) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[12] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(shd::g_stamp_prof), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif

@@ -71,6 +71,71 @@ __global__ __launch_bounds__(256) void kB(Buf b, const uint32_t* order, const ui
     }
 }
 
+
+// P: persistent workgroup per CU (1024 threads, 4 positions each per chunk) over host groups
+__global__ __launch_bounds__(1024) void kP(Buf b, const uint32_t* order, const uint32_t* off,
+                                           uint32_t H, int gather) {
+    __shared__ uint32_t s_beg[64], s_pre[65];
+    __shared__ uint16_t s_flag[4096];
+    const uint32_t tid = threadIdx.x, ng = (H + 63) / 64;
+    for (uint32_t g = blockIdx.x; g < ng; g += gridDim.x) {
+        const uint32_t h0 = g * 64, nh = min(64u, H - h0);
+        __syncthreads();
+        if (tid < 64) {
+            uint32_t len = 0;
+            if (tid < nh) {
+                const uint32_t h = order[h0 + tid];
+                s_beg[tid] = off[h];
+                len = off[h + 1] - off[h];
+            }
+            uint32_t incl = len;
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (tid >= o) incl += y;
+            }
+            if (tid < nh) s_pre[tid + 1] = incl;
+            if (tid == 0) s_pre[0] = 0;
+        }
+        __syncthreads();
+        const uint32_t T = s_pre[nh];
+        for (uint32_t c0 = 0; c0 < T; c0 += 4096) {
+            const uint32_t cn = min(4096u, T - c0);
+            uint32_t idx[4];
+            uint64_t t[4], r[4];
+            uint32_t d[4], p[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t gp = c0 + min(tid + 1024u * i, cn - 1);
+                uint32_t lo = 0, hi = nh;
+                while (hi - lo > 1) {
+                    const uint32_t m = (lo + hi) >> 1;
+                    if (s_pre[m] <= gp) lo = m; else hi = m;
+                }
+                idx[i] = s_beg[lo] + gp - s_pre[lo];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                t[i] = b.t[idx[i]]; d[i] = b.d[idx[i]]; p[i] = b.p[idx[i]]; r[i] = b.r[idx[i]];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (gather) d[i] = b.hn[d[i]];
+                s_flag[tid + 1024 * i] = (uint16_t)(t[i] ^ r[i]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (tid + 1024u * i < cn) {
+                    b.st[idx[i]] = (uint8_t)s_flag[tid ^ 1];
+                    b.key[idx[i]] = d[i] + p[i];
+                    b.rec[idx[i]] = make_uint4((uint32_t)t[i], d[i], p[i], (uint32_t)r[i]);
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 int main() {
     const uint32_t H = 100000, N = 10000000;
     std::mt19937_64 g(4);
@@ -110,5 +175,15 @@ int main() {
     run("B node-ordered host groups", [&] { kB<<<(H + 63) / 64, 256>>>(b, o_ord, o_off, H, 0); });
     run("C node-ordered + node gather", [&] { kB<<<(H + 63) / 64, 256>>>(b, o_ord, o_off, H, 1); });
     run("D batch order + node gather", [&] { kA<<<2048, 256>>>(b, N, 1); });
+    std::vector<uint32_t> ident(H);
+    for (uint32_t h = 0; h < H; ++h) ident[h] = h;
+    uint32_t* o_id;
+    CK(hipMalloc(&o_id, H * 4));
+    CK(hipMemcpy(o_id, ident.data(), H * 4, hipMemcpyHostToDevice));
+    run("B batch-ordered host groups", [&] { kB<<<(H + 63) / 64, 256>>>(b, o_id, o_off, H, 0); });
+    run("P persistent, node-ordered", [&] { kP<<<256, 1024>>>(b, o_ord, o_off, H, 0); });
+    run("P persistent, batch-ordered", [&] { kP<<<256, 1024>>>(b, o_id, o_off, H, 0); });
+    run("P persistent x2/CU, node-ordered", [&] { kP<<<512, 1024>>>(b, o_ord, o_off, H, 0); });
+    run("P non-persistent, node-ordered", [&] { kP<<<(H + 63) / 64, 1024>>>(b, o_ord, o_off, H, 0); });
     return 0;
 }
