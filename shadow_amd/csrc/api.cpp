@@ -65,6 +65,12 @@ shd_ctx* shd_open(int device_ordinal, shd_status* st) {
         return fail(SHD_ERR_HIP);
     }
     ctx->own_stream = true;
+    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pin), 64 * sizeof(unsigned long long),
+                      hipHostMallocDefault) != hipSuccess) {
+        ctx->h_pin = nullptr;
+        shd_close(ctx);
+        return fail(SHD_ERR_HIP);
+    }
     for (auto& e : ctx->ev)
         if (hipEventCreate(&e) != hipSuccess) {
             shd_close(ctx);
@@ -80,6 +86,7 @@ void shd_close(shd_ctx* ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (auto& e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
+    if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;  // DevBuf destructors free device memory
 }

@@ -88,6 +88,7 @@ struct shd_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     hipEvent_t ev[8] = {};
+    unsigned long long* h_pin = nullptr;   // 64 pinned host words: flag / reduction read-backs
     int n_cu = 0;
     size_t max_lds = 0;
 

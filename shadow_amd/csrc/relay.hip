@@ -374,6 +374,15 @@ __global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint64_t* __rest
     }
 }
 
+// A path-table entry from global memory through an explicit global (addrspace 1) pointer.  Next
+// to an LDS-staged alternative a plain `cond ? s_rows[i] : path[j]` lets the compiler select the
+// pointer and issue a flat load, and a flat load makes every later s_waitcnt wait for the
+// wave's outstanding stores as well -- which serialised the stamp's record stores.
+__device__ __forceinline__ uint2 path_global(const uint2* p, size_t i) {
+    const unsigned long long v = ((const __attribute__((address_space(1))) unsigned long long*)p)[i];
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+
 // K1 relay_stamp_v5: a workgroup owns kS5Hosts source hosts taken in source-node order
 // (R.order), so its path lookups stay in one or two table rows, staged in LDS when they fit.
 // The hosts' sends (one contiguous range per host) form one list, processed in chunks of
@@ -467,7 +476,7 @@ __global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint64
                 } else if (now < a.sim_end) {
                     dn[i] = a.host_node[dst[i]];
                     const uint2 pp = staged ? s_rows[s_rowof[lo] * a.n_nodes + dn[i]]
-                                            : a.path[(size_t)s_node[lo] * a.n_nodes + dn[i]];
+                                            : path_global(a.path, (size_t)s_node[lo] * a.n_nodes + dn[i]);
                     const double reliability = (double)one_minus(__uint_as_float(pp.y));
                     const double ch = a.chance ? a.chance[idx[i]]
                                                : (double)(draw[idx[i]] >> 11) * (1.0 / 9007199254740992.0);
@@ -564,7 +573,7 @@ __global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint64
 constexpr uint32_t kS6Threads = 1024;
 constexpr uint32_t kS6Per = 4;
 constexpr uint32_t kS6Cap = kS6Threads * kS6Per;
-constexpr uint32_t kS6FixedLds = kS5RowLds * 8 + (kS6Cap + 2) * 2 + 4096;   // rows + scan + small
+constexpr uint32_t kS6FixedLds = kS5RowLds * 8 + (kS6Cap + 2) * 2 + kS6Cap + 4096;   // rows + scan + owners + small
 
 __device__ __forceinline__ uint32_t packed_get(const uint32_t* t, uint32_t j, uint32_t bits) {
     const uint32_t o = j * bits, w = o >> 5, sh = o & 31;
@@ -591,8 +600,9 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     __shared__ uint32_t s_host[kS5Hosts], s_beg[kS5Hosts], s_pre[kS5Hosts + 1], s_node[kS5Hosts];
     __shared__ uint32_t s_rowof[kS5Hosts], s_rownode[kS5Hosts], s_run[kS5Hosts], s_base[kS5Hosts];
     __shared__ uint32_t s_wsum[kS6Threads / 64], s_nrows;
+    __shared__ uint8_t s_own[kS6Cap];   // chunk position -> host slot in the group
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    #ifdef SHD_STAMP_PROF
+#ifdef SHD_STAMP_PROF
     uint64_t sp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, sp_t = __builtin_amdgcn_s_memtime();
 #endif
     for (uint32_t i = tid; i < n_words; i += kS6Threads) s_tbl[i] = packed[i];
@@ -616,6 +626,15 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
         p_h = a.order[blockIdx.x * kS5Hosts + tid];
     }
     if (tid < 64) fetch_hosts(blockIdx.x);
+    // 16 threads per host slot fill the owner map of the chunk starting at position cb
+    static_assert(kS6Threads == kS5Hosts * 16, "owner fill: 16 threads per host slot");
+    auto fill_owner = [&](uint32_t cb, uint32_t nh) {
+        const uint32_t hh = tid >> 4, sub = tid & 15;
+        if (hh < nh) {
+            const uint32_t pb = max(s_pre[hh], cb), pe = min(s_pre[hh + 1], cb + kS6Cap);
+            for (uint32_t p = pb + sub; p < pe; p += 16) s_own[p - cb] = (uint8_t)hh;
+        }
+    };
     const uint64_t* __restrict__ rsrc = a.chance ? reinterpret_cast<const uint64_t*>(a.chance) : draw;
     for (uint32_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
         const uint32_t h0 = grp * kS5Hosts;
@@ -663,23 +682,21 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 s_rows[e] = a.path[(size_t)s_rownode[rr] * a.n_nodes + c];
             }
         }
+        fill_owner(0, nh);
         if (tid < 64) fetch_hosts(nxt);
         __syncthreads();
         SP_MARK(2);
         const uint32_t T = s_pre[nh];
         for (uint32_t c0 = 0; c0 < T; c0 += kS6Cap) {
             const uint32_t cn = min(kS6Cap, T - c0);
-            // (a) positions -> packet indices (positions past the chunk end are clamped onto its
-            // last packet so that every load below is in bounds and issued unconditionally)
+            // (a) positions -> packet indices through the owner map (positions past the chunk end
+            // are clamped onto its last packet so every load below is in bounds and unconditional)
             uint32_t idx[kS6Per], hl[kS6Per], kk[kS6Per];
 #pragma unroll
             for (uint32_t i = 0; i < kS6Per; ++i) {
-                const uint32_t gp = c0 + min(tid + kS6Threads * i, cn - 1);
-                uint32_t lo = 0, hi = nh;           // s_pre[lo] <= gp < s_pre[lo + 1]
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_pre[mid] <= gp) lo = mid; else hi = mid;
-                }
+                const uint32_t q = min(tid + kS6Threads * i, cn - 1);
+                const uint32_t gp = c0 + q;
+                const uint32_t lo = s_own[q];       // s_pre[lo] <= gp < s_pre[lo + 1]
                 hl[i] = lo;
                 kk[i] = gp - s_pre[lo];
                 idx[i] = s_beg[lo] + kk[i];
@@ -713,7 +730,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                     } else if (now[i] < a.sim_end) {
                         dn[i] = packed_get(s_tbl, dst[i], bits);
                         const uint2 pp = staged ? s_rows[s_rowof[hl[i]] * a.n_nodes + dn[i]]
-                                                : a.path[(size_t)s_node[hl[i]] * a.n_nodes + dn[i]];
+                                                : path_global(a.path, (size_t)s_node[hl[i]] * a.n_nodes + dn[i]);
                         const double reliability = (double)one_minus(__uint_as_float(pp.y));
                         const double ch = a.chance ? __longlong_as_double((long long)rv[i])
                                                    : (double)(rv[i] >> 11) * (1.0 / 9007199254740992.0);
@@ -776,6 +793,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                     }
                 }
             }
+            if (c0 + kS6Cap < T) fill_owner(c0 + kS6Cap, nh);   // s_own of this chunk is consumed
             __syncthreads();
             SP_MARK(5);
             if (tid < nh) {
@@ -1317,6 +1335,14 @@ static shd_status sort_by_dst(RelayState& R, rocprim::double_buffer<uint32_t>& k
 
 // Narrow pipeline: K1 stamp, K2 radix sort by destination, K3 offsets, K4 per-run sort; one
 // host sync (for the round reductions).
+// the round's reductions: [0] min deliver, [1] min latency, [2] sent, [3] first bad index,
+// [4] wide offset, [5] send-order violation; plus the big-run counter of K4
+__global__ __launch_bounds__(64) void red_init(unsigned long long* __restrict__ red, uint32_t* __restrict__ n_big) {
+    const uint32_t t = threadIdx.x;
+    if (t < 8) red[t] = (t <= 1 || t == 3) ? ~0ull : 0ull;
+    if (t == 0) *n_big = 0;
+}
+
 static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
                                   shd_relay_out* o) {
     RelayState& R = ctx->relay;
@@ -1329,9 +1355,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     SHD_TRY(R.ev_val.ensure(nn * 4));    // keys
     SHD_TRY(R.ev_key.ensure(nn * 4));    // keys (second buffer)
     SHD_TRY(R.ev_val2.ensure((size_t)(H + 2) * 4));
-    unsigned long long init[8] = {~0ull, ~0ull, 0ull, ~0ull, 0ull, 0ull, 0ull, 0ull};
-    SHD_HIP(hipMemcpyAsync(R.red.p, init, sizeof(init), hipMemcpyHostToDevice, s));
-    SHD_HIP(hipMemsetAsync(R.ev_val2.p, 0, 4, s));
+    red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.ev_val2.as<uint32_t>());
     RelayArgs3 a{};
     a.n_hosts = H;
     a.n_nodes = R.n_nodes;
@@ -1391,8 +1415,9 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
                                            spare, rd->round_end, seq_base,
                                            o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt);
     SHD_HIP(hipGetLastError());
-    SHD_HIP(hipMemcpyAsync(R.red_host, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 8, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
+    std::memcpy(R.red_host, ctx->h_pin + 8, sizeof(R.red_host));
     return SHD_OK;
 }
 

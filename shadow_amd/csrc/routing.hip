@@ -294,9 +294,18 @@ __global__ __launch_bounds__(256) void arcs_pack(const uint32_t* __restrict__ ds
 // over the K lowest-latency neighbours of u (any subset is sound; the nearest catch almost
 // all: C2 keeps ~49 of 999 arcs per node with K = 32).  Ties (detour == arc) are kept.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void dense_init(uint64_t* __restrict__ Wk, uint64_t nn) {
+__global__ __launch_bounds__(256) void dense_init(uint64_t* __restrict__ Wk, uint64_t nn,
+                                                  uint32_t* __restrict__ cursor) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < nn) Wk[i] = kKeyInf;
+    if (i == 0) *cursor = 0;   // prune_rows' output cursor
+}
+
+// per-build flags (one launch instead of three memsets): [0,16) overflow / misc = 0,
+// [16,24) first unreachable pair = ~0, [24,64) = 0 (stats counters at 32)
+__global__ __launch_bounds__(64) void flags_init(uint32_t* __restrict__ f) {
+    const uint32_t t = threadIdx.x;
+    if (t < 16) f[t] = (t == 4 || t == 5) ? 0xFFFFFFFFu : 0u;
 }
 
 // one workgroup per row u: lexicographic min over parallel arcs into the dense key matrix
@@ -609,11 +618,18 @@ static shd_status upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
     return SHD_OK;
 }
 
+// one pinned read-back of the build flags (overflow word, first unreachable pair) and one sync
+static shd_status read_flags(shd_ctx* ctx) {
+    SHD_HIP(hipMemcpyAsync(ctx->h_pin, ctx->g_flags.p, 24, hipMemcpyDeviceToHost, ctx->stream));
+    SHD_HIP(hipStreamSynchronize(ctx->stream));
+    return SHD_OK;
+}
+static bool flag_ovf(const shd_ctx* ctx) { return (uint32_t)ctx->h_pin[0] != 0; }
+
+// the first unreachable pair of the last read_flags (the reference panics there, graph/mod.rs:221)
 static shd_status check_unreach(shd_ctx* ctx, shd_error* err) {
     PreparedGraph& P = ctx->prep;
-    unsigned long long bad = 0;
-    SHD_HIP(hipMemcpyAsync(&bad, ctx->g_flags.as<char>() + 16, 8, hipMemcpyDeviceToHost, ctx->stream));
-    SHD_HIP(hipStreamSynchronize(ctx->stream));
+    const unsigned long long bad = ctx->h_pin[2];
     if (bad != ~0ull) {
         const uint32_t r = (uint32_t)(bad / P.n_used), c = (uint32_t)(bad % P.n_used);
         return set_err(err, SHD_ERR_UNREACHABLE, P.node_ids[P.used[r]], P.node_ids[P.used[c]]);
@@ -623,9 +639,8 @@ static shd_status check_unreach(shd_ctx* ctx, shd_error* err) {
 
 static shd_status reset_flags(shd_ctx* ctx) {
     SHD_TRY(ctx->g_flags.ensure(64));
-    SHD_HIP(hipMemsetAsync(ctx->g_flags.p, 0, 16, ctx->stream));
-    SHD_HIP(hipMemsetAsync(ctx->g_flags.as<char>() + 16, 0xFF, 8, ctx->stream));
-    SHD_HIP(hipMemsetAsync(ctx->g_flags.as<char>() + 32, 0, 16, ctx->stream));
+    flags_init<<<1, 64, 0, ctx->stream>>>(ctx->g_flags.as<uint32_t>());
+    SHD_HIP(hipGetLastError());
     return SHD_OK;
 }
 
@@ -677,10 +692,8 @@ static shd_status run_wide(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d_l
                                      ctx->g_diag_loss.as<float>(), d_lat, d_loss,
                                      reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16));
     }
-    uint32_t fl[2] = {0, 0};
-    SHD_HIP(hipMemcpyAsync(fl, ctx->g_flags.p, 8, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    if (fl[1]) return set_err(err, SHD_ERR_LATENCY_OVERFLOW, 0, 0);
+    SHD_TRY(read_flags(ctx));
+    if ((uint32_t)(ctx->h_pin[0] >> 32)) return set_err(err, SHD_ERR_LATENCY_OVERFLOW, 0, 0);
     ctx->info.wide_latency = 1;
     return check_unreach(ctx, err);
 }
@@ -860,10 +873,7 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
     }
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(ctx->ev[3], s));
-    uint32_t fl = 0;
-    SHD_HIP(hipMemcpyAsync(&fl, ctx->g_flags.p, 4, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    *ovf = fl != 0;
+    (void)ovf;   // the caller reads the overflow flag with read_flags()
     if (ctx->stats_on) {
         unsigned long long st[2];
         SHD_HIP(hipMemcpy(st, ctx->g_flags.as<char>() + 32, 16, hipMemcpyDeviceToHost));
@@ -910,10 +920,7 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     }
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(ctx->ev[3], s));
-    uint32_t fl = 0;
-    SHD_HIP(hipMemcpyAsync(&fl, ctx->g_flags.p, 4, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    *ovf = fl != 0;
+    (void)ovf;   // the caller reads the overflow flag with read_flags()
     if (ctx->stats_on) {
         unsigned long long st[2];
         SHD_HIP(hipMemcpy(st, ctx->g_flags.as<char>() + 32, 16, hipMemcpyDeviceToHost));
@@ -985,8 +992,7 @@ static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
     uint32_t* pbeg = ctx->g_prune_cnt.as<uint32_t>();
     uint32_t* pend = pbeg + V;
     uint32_t* cursor = pend + V;
-    SHD_HIP(hipMemsetAsync(cursor, 0, 4, s));
-    dense_init<<<div_up(nn, 256), 256, 0, s>>>(Wk, nn);
+    dense_init<<<div_up(nn, 256), 256, 0, s>>>(Wk, nn, cursor);
     dense_scatter<<<V, 256, 0, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
                                     ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wk);
     dense_lat<<<div_up(nn, 256), 256, 0, s>>>(Wk, Wl, nn);
@@ -1035,7 +1041,8 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         SHD_TRY(run_blocked(ctx, rb, re, d_lat, d_loss, &ovf));
         ctx->info.algo_used = SHD_ALGO_BLOCKED;
         SHD_HIP(hipEventRecord(ctx->ev[1], s));
-        SHD_HIP(hipEventSynchronize(ctx->ev[1]));
+        SHD_TRY(read_flags(ctx));
+        ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;
         (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
         (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);
@@ -1070,7 +1077,8 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ctx->info.algo_used = algo == SHD_ALGO_DELTA ? SHD_ALGO_DELTA
                               : prune ? SHD_ALGO_PRUNED : SHD_ALGO_SSSP;
         SHD_HIP(hipEventRecord(ctx->ev[1], s));
-        SHD_HIP(hipEventSynchronize(ctx->ev[1]));
+        SHD_TRY(read_flags(ctx));
+        ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;
         (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
         (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);
@@ -1091,7 +1099,8 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         SHD_TRY(run_sssp_global(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
         ctx->info.algo_used = algo == SHD_ALGO_DELTA ? SHD_ALGO_DELTA : SHD_ALGO_SSSP;
         SHD_HIP(hipEventRecord(ctx->ev[1], s));
-        SHD_HIP(hipEventSynchronize(ctx->ev[1]));
+        SHD_TRY(read_flags(ctx));
+        ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;
         (void)hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]);
         (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);

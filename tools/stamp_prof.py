@@ -19,7 +19,7 @@ lib = C.CDLL(_native.LIB_PATH)
 out = (C.c_ulonglong * 12)()
 assert lib.shd_debug_stamp_prof(out, 0) == 0
 names = ["group setup", "rows issue+wait", "rows stage", "chunk barrier", "scan", "stores",
-         "run update", "tail", "idx search", "load issue", "decide(wait)", "-"]
+         "run update", "tail", "idx (owner map)", "load issue", "decide(wait)", "-"]
 tot = sum(out)
 for n, v in zip(names, out):
     print(f"{n:18s} {v:16d}  {100.0 * v / max(tot, 1):5.1f}%")
