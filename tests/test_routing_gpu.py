@@ -216,3 +216,4 @@ def test_global_label_kernel_forced(engine, seed, monkeypatch):
     for algo in (1, 3):
         t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=algo)
         _assert_table(t, lat, loss.view(np.uint32))
+
