@@ -234,6 +234,27 @@ shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t*
 shd_status shd_relay_set_counters(shd_ctx* ctx, int32_t enabled);
 shd_status shd_path_packet_counts(shd_ctx* ctx, uint64_t* counts);
 
+/* ---------------------------------------------------------------------------------------
+ * GML loader (host code, no GPU needed).  Replaces the reference's
+ * gml_parser::parse (src/lib/gml-parser/src/lib.rs:52-57) + NetworkGraph::parse
+ * (src/main/network/graph/mod.rs:136-183): GML text -> the shd_graph arrays the routing build
+ * takes.  Node index = order of the node in the text (petgraph add_node order); a repeated GML
+ * id maps to its later node, as the reference's HashMap insert does.  On failure `msg` holds the
+ * reference's message (e.g. "Edge 'latency' must not be 0", "Edge source 7 doesn't exist").
+ * ------------------------------------------------------------------------------------- */
+typedef struct shd_gml shd_gml;
+
+/* Parse `len` bytes of GML.  SHD_ERR_INVALID: grammar or validation error;
+ * SHD_ERR_LATENCY_OVERFLOW: an edge latency does not fit u64 ns (the reference panics in
+ * convert(Nano).unwrap(), graph/mod.rs:338). */
+shd_status shd_gml_parse(const char* text, size_t len, shd_gml** out, char* msg, size_t msg_len);
+/* View of the parsed graph; the arrays stay owned by `g` until shd_gml_free. */
+shd_status shd_gml_graph(const shd_gml* g, shd_graph* view);
+/* host_bandwidth_down / _up per node in bits/s (UINT64_MAX = attribute absent; values beyond
+ * u64 saturate at UINT64_MAX - 1).  Either pointer may be NULL; arrays are [n_nodes]. */
+shd_status shd_gml_node_bandwidth(const shd_gml* g, uint64_t* down_bps, uint64_t* up_bps);
+void shd_gml_free(shd_gml* g);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,8 +3,9 @@
 Restates:
   * ``src/lib/gml-parser/src/parser.rs:44-262`` (nom grammar: key/item/gml/node/edge/value/
     int/float/string/newline/int_as_bool) and ``src/lib/gml-parser/src/lib.rs:52-57``;
-  * ``src/main/core/support/units.rs:214-280`` (TimePrefix), ``:377-388`` (convert with
-    checked_mul), ``:405-438`` (FromStr: regex ``^([+-]?[0-9\\.]*)\\s*(.*)$``);
+  * ``src/main/core/support/units.rs:214-280`` (TimePrefix), ``:142-178`` (SiPrefixUpper),
+    ``:377-388`` (convert with checked_mul), ``:405-438`` (FromStr: regex
+    ``^([+-]?[0-9\\.]*)\\s*(.*)$``, suffix stripping, ``ParseIntError`` texts);
   * ``src/main/network/graph/mod.rs:30-113`` (ShadowNode / ShadowEdge ``try_from``),
     ``:136-183`` (NetworkGraph::parse) and ``:335-342`` (edge -> PathProperties).
 
@@ -110,7 +111,8 @@ class _Cursor:
 
 
 _FLOAT_RE = re.compile(r"[+-]?(?:[0-9]+(?:\.[0-9]*)?|\.[0-9]+)(?:[eE][+-]?[0-9]+)?")
-_FLOAT_BAD_EXP = re.compile(r"[+-]?(?:[0-9]+(?:\.[0-9]*)?|\.[0-9]+)[eE][+-]?(?![0-9])")
+# an exponent marker with no digits after its optional sign (no backtracking over the sign)
+_FLOAT_BAD_EXP = re.compile(r"[+-]?(?:[0-9]+(?:\.[0-9]*)?|\.[0-9]+)[eE](?:[+-](?![0-9])|(?![+\-0-9]))")
 
 
 def _value(c: _Cursor):
@@ -243,7 +245,7 @@ for _names, _ns in (
     for _n in _names:
         _TIME_PREFIX_NS[_n] = _ns
 
-_UNIT_RE = re.compile(r"^([+-]?[0-9.]*)\s*(.*)$")
+_UNIT_RE = re.compile(r"^([+-]?[0-9.]*)\s*(.*)\Z")   # Rust `$`: end of text only
 
 
 def parse_time(text: str):
@@ -257,15 +259,51 @@ def parse_time(text: str):
     elif unit in _TIME_PREFIX_NS:
         mag = _TIME_PREFIX_NS[unit]
     else:
-        raise GmlError("Unit was not one of (ns|...)")
-    # Rust u64::from_str: optional '+', digits only
-    v = value[1:] if value.startswith("+") else value
-    if not v.isdigit() or not v.isascii():
-        raise GmlError(f"invalid digit in {value!r}")
+        raise GmlError("Unit was not one of (ns|nanosecond|nanoseconds|us|μs|microsecond|microseconds"
+                       "|ms|millisecond|milliseconds|s|sec|secs|second|seconds|m|min|mins|minute"
+                       "|minutes|h|hr|hrs|hour|hours)")
+    return _parse_u64(value), mag
+
+
+def _parse_u64(value: str) -> int:
+    """Rust ``u64::from_str`` with its ``ParseIntError`` messages: an optional '+', then
+    ASCII digits only."""
+    if value == "":
+        raise GmlError("cannot parse integer from empty string")
+    v = value[1:] if value[0] == "+" and len(value) > 1 else value
+    if not (v.isascii() and v.isdigit()):
+        raise GmlError("invalid digit found in string")
     iv = int(v)
     if iv > U64_MAX:
         raise GmlError("number too large to fit in target type")
-    return iv, mag
+    return iv
+
+
+_SI_UPPER = {"K": 1000, "kilo": 1000, "Ki": 1024, "kibi": 1024, "M": 10**6, "mega": 10**6,
+             "Mi": 2**20, "mebi": 2**20, "G": 10**9, "giga": 10**9, "Gi": 2**30, "gibi": 2**30,
+             "T": 10**12, "tera": 10**12, "Ti": 2**40, "tebi": 2**40}
+
+
+def parse_bits_per_sec(text: str) -> int:
+    """``BitsPerSec::<SiPrefixUpper>::from_str`` (units.rs:142-178, 405-438, 578): the unit
+    minus a "bit"/"bits" suffix is the SI prefix ("" = base).  Returns bits/s (unbounded)."""
+    m = _UNIT_RE.match(text)
+    if m is None:
+        raise GmlError("Unable to identify value and unit")
+    value, unit = m.group(1).strip(), m.group(2).strip()
+    prefix = unit
+    for suf in ("bit", "bits"):
+        if unit.endswith(suf):
+            prefix = unit[: len(unit) - len(suf)]
+            break
+    if prefix == "":
+        mag = 1
+    elif prefix in _SI_UPPER:
+        mag = _SI_UPPER[prefix]
+    else:
+        raise GmlError("Unit prefix was not one of (K|kilo|Ki|kibi|M|mega|Mi|mebi|G|giga|Gi|gibi"
+                       "|T|tera|Ti|tebi)")
+    return _parse_u64(value) * mag
 
 
 def time_to_ns(value: int, mag: int) -> int:
@@ -306,12 +344,18 @@ def _edge_from_gml(kv: dict):
         raise GmlError("Edge 'latency' was not provided")
     if lat[0] != "str":
         raise GmlError("Edge 'latency' is not a string")
-    lat_v, lat_mag = parse_time(lat[1])
+    try:
+        lat_v, lat_mag = parse_time(lat[1])
+    except GmlError as e:
+        raise GmlError(f"Edge 'latency' is not a valid unit: {e}") from None
     jit = kv.pop("jitter", None)
     if jit is not None:
         if jit[0] != "str":
             raise GmlError("Edge 'jitter' is not a string")
-        parse_time(jit[1])                       # parsed and ignored
+        try:
+            parse_time(jit[1])                   # parsed and ignored
+        except GmlError as e:
+            raise GmlError(f"Edge 'jitter' is not a valid unit: {e}") from None
     pl = kv.pop("packet_loss", None)
     if pl is None:
         loss = np.float32(0.0)
@@ -333,9 +377,14 @@ def parse_network_graph(text: str) -> NetworkGraph:
     for kv in g.nodes:
         if kv["id"] is None:
             raise GmlError("Node 'id' was not provided")
-        for bw in ("host_bandwidth_down", "host_bandwidth_up"):
-            if bw in kv and kv[bw][0] != "str":
-                raise GmlError(f"Node '{bw}' is not a string")
+        for bw in ("host_bandwidth_down", "host_bandwidth_up"):   # ShadowNode (:30-62)
+            if bw in kv:
+                if kv[bw][0] != "str":
+                    raise GmlError(f"Node '{bw}' is not a string")
+                try:
+                    parse_bits_per_sec(kv[bw][1])
+                except GmlError as e:
+                    raise GmlError(f"Node '{bw}' is not a valid unit: {e}") from None
         id_map[kv["id"]] = len(node_ids)
         node_ids.append(kv["id"])
     edges = []

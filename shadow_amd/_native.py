@@ -28,6 +28,7 @@ EXPORTED = [
     "shd_relay_round_device", "shd_events_merge_device", "shd_relay_get_host_state",
     "shd_relay_set_counters",
     "shd_path_packet_counts",
+    "shd_gml_parse", "shd_gml_graph", "shd_gml_node_bandwidth", "shd_gml_free",
 ]
 
 
@@ -111,6 +112,10 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_relay_set_counters": (I32, [P, I32]),
         "shd_events_merge_device": (I32, [P, U32, U32, P, P, P, P, P, P, U64, P]),
         "shd_path_packet_counts": (I32, [P, P]),
+        "shd_gml_parse": (I32, [P, C.c_size_t, P, P, C.c_size_t]),
+        "shd_gml_graph": (I32, [P, P]),
+        "shd_gml_node_bandwidth": (I32, [P, P, P]),
+        "shd_gml_free": (None, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

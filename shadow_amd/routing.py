@@ -6,7 +6,9 @@ Mirrors (FlyearthR/shadow ``src/main/network/graph/mod.rs``):
   * ``PathProperties`` as a ``(latency_ns, packet_loss)`` pair (:298-342);
   * ``RoutingInfo`` (:430-479): ``path``, ``increment_packet_count`` (device counters),
     ``get_smallest_latency_ns``;
-  * ``generate_routing_info`` (``src/main/core/sim_config.rs:424-461``).
+  * ``generate_routing_info`` (``src/main/core/sim_config.rs:424-461``);
+  * ``NetworkGraph.parse`` (:136-183) and ``load_network_graph`` (:481-520) over the native
+    GML loader (``shd_gml_parse``; host code, no GPU).
 Errors keep the reference's messages: ``Err(..)`` results raise :class:`NetGraphError`; the
 reference's ``assert_eq!`` panic on an unreachable pair raises :class:`RoutingPanic`.
 """
@@ -118,6 +120,44 @@ class NetworkGraph:
         self.directed = bool(directed)
         self._id_to_index = {int(v): i for i, v in enumerate(self.node_ids)}
 
+    @classmethod
+    def parse(cls, graph_text) -> "NetworkGraph":
+        """``NetworkGraph::parse`` (graph/mod.rs:136-183) through the native loader.
+
+        Raises :class:`NetGraphError` with the reference's message on any GML or validation
+        error, :class:`RoutingPanic` for an edge latency beyond u64 ns (the reference's
+        ``convert(Nano).unwrap()``, :338)."""
+        lib = N.load()
+        data = graph_text.encode() if isinstance(graph_text, str) else bytes(graph_text)
+        h = C.c_void_p()
+        msg = C.create_string_buffer(1024)
+        st = lib.shd_gml_parse(data, len(data), C.byref(h), msg, len(msg))
+        if st != N.SHD_OK:
+            text = msg.value.decode("utf-8", "replace")
+            if N.STATUS_NAMES.get(st) == "LATENCY_OVERFLOW":
+                raise RoutingPanic(text)
+            raise NetGraphError(text)
+        try:
+            v = N.Graph()
+            N.check(lib.shd_gml_graph(h, C.byref(v)), "shd_gml_graph")
+
+            def arr(p, n, ct, dt):
+                if n == 0:
+                    return np.zeros(0, dt)
+                return np.ctypeslib.as_array(C.cast(p, C.POINTER(ct)), shape=(n,)).astype(dt, copy=True)
+            g = cls(arr(v.node_ids, v.n_nodes, C.c_uint32, np.uint32),
+                    arr(v.edge_src, v.n_edges, C.c_uint32, np.uint32),
+                    arr(v.edge_dst, v.n_edges, C.c_uint32, np.uint32),
+                    arr(v.edge_latency_ns, v.n_edges, C.c_uint64, np.uint64),
+                    arr(v.edge_packet_loss, v.n_edges, C.c_float, np.float32), bool(v.directed))
+            down = np.empty(v.n_nodes, np.uint64)
+            up = np.empty(v.n_nodes, np.uint64)
+            N.check(lib.shd_gml_node_bandwidth(h, N.ptr(down), N.ptr(up)), "shd_gml_node_bandwidth")
+            g.bandwidth_down_bps, g.bandwidth_up_bps = down, up   # UINT64_MAX = not given
+            return g
+        finally:
+            lib.shd_gml_free(h)
+
     @property
     def n_nodes(self) -> int:
         return len(self.node_ids)
@@ -194,3 +234,20 @@ def generate_routing_info(graph: NetworkGraph, nodes, use_shortest_paths: bool =
     table = (graph.compute_shortest_paths(idx, engine) if use_shortest_paths
              else graph.get_direct_paths(idx, engine))
     return RoutingInfo(table)
+
+
+def load_network_graph(path: str) -> str:
+    """``load_network_graph`` (graph/mod.rs:481-520) for a GML file source: the text of `path`,
+    xz-decompressed when it ends in ``.xz`` (the reference's ``compression: xz``; Python's
+    lzma stands in for lzma-rs), decoded as strict UTF-8 like ``String::from_utf8``."""
+    import lzma
+    if path.endswith(".xz"):
+        with lzma.open(path, "rb") as f:
+            raw = f.read()
+    else:
+        with open(path, "rb") as f:
+            raw = f.read()
+    try:
+        return raw.decode("utf-8")
+    except UnicodeDecodeError as e:
+        raise NetGraphError(f"invalid utf-8: {e}") from None
