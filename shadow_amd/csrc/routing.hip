@@ -331,39 +331,115 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
     const uint32_t* __restrict__ Wl, const uint64_t* __restrict__ Wk, uint32_t V, uint32_t P,
     uint32_t* __restrict__ pbeg, uint32_t* __restrict__ pend, uint4* __restrict__ parcs,
     uint32_t* __restrict__ cursor) {
+    // Detour nodes x: ~K of u's lowest-latency neighbours, chosen by a 256-bin latency histogram
+    // (every node in the bins below the K-th smallest latency's bin, then nodes of that bin in
+    // index order up to K).  Any set of detour nodes is sound -- it only decides how many arcs
+    // are dropped -- so this replaces a full bitonic sort of the row (55 barrier stages) by
+    // three passes over it.
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t* s = reinterpret_cast<uint64_t*>(smem);  // P entries (lat << 32 | x)
-    uint4* kept = reinterpret_cast<uint4*>(s + P);     // V staged arcs
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(kept + V);
-    const uint32_t u = blockIdx.x, tid = threadIdx.x;
+    uint4* kept = reinterpret_cast<uint4*>(smem);      // V staged arcs
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(kept + V);   // [0] kept [1] base [2] max [3] below-bin
+    uint32_t* hist = cnt + 8;                          // 256 bins
+    uint32_t* selx = hist + 256;                       // K detour nodes
+    uint32_t* sela = selx + K;                         // their latencies
+    uint16_t* binv = reinterpret_cast<uint16_t*>(sela + K);   // bin per node (0xFFFF: no arc)
+    const uint32_t u = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const uint32_t* row = Wl + (size_t)u * V;
-    for (uint32_t i = tid; i < P; i += BLOCK)
-        s[i] = i < V ? (((uint64_t)row[i] << 32) | i) : ~0ull;
-    if (tid == 0) cnt[0] = 0;
+    (void)P;
+    for (uint32_t i = tid; i < 256; i += BLOCK) hist[i] = 0;
+    if (tid < 8) cnt[tid] = 0;
+    uint32_t mx = 0;
+    for (uint32_t v = tid; v < V; v += BLOCK) {
+        const uint32_t w = row[v];
+        if (w != kLat32Inf) mx = max(mx, w);
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
     __syncthreads();
-    // bitonic sort ascending (only the first K entries are used)
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = tid; i < P; i += BLOCK) {
-                const uint32_t l = i ^ j;
-                if (l > i) {
-                    const uint64_t a = s[i], b = s[l];
-                    if ((a > b) == ((i & k) == 0)) {
-                        s[i] = b;
-                        s[l] = a;
-                    }
-                }
+    if (lane == 0) atomicMax(&cnt[2], mx);
+    __syncthreads();
+    const uint32_t bits = 32u - (uint32_t)__clz((int)max(cnt[2], 1u));
+    const uint32_t sh = bits > 8 ? bits - 8 : 0;
+    for (uint32_t v = tid; v < V; v += BLOCK) {
+        const uint32_t w = row[v];
+        binv[v] = w != kLat32Inf ? (uint16_t)(w >> sh) : (uint16_t)0xFFFF;
+        if (w != kLat32Inf) atomicAdd(&hist[w >> sh], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {   // wave 0: the bin holding the K-th smallest latency
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            c[i] = hist[tid * 4 + i];
+            sum += c[i];
+        }
+        uint32_t incl = sum;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        uint32_t run = incl - sum, bsel = 256, below = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (bsel == 256 && run + c[i] >= (uint32_t)K) {
+                bsel = tid * 4 + i;
+                below = run;
             }
-            __syncthreads();
+            run += c[i];
+        }
+        const uint64_t m = __ballot(bsel != 256);
+        if (m) {
+            const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+            const uint32_t b = __shfl((int)bsel, first), bl = __shfl((int)below, first);
+            if (tid == 0) {
+                cnt[4] = b;
+                cnt[3] = bl;
+            }
+        } else if (tid == 0) {
+            cnt[4] = 256;      // fewer than K finite entries: take them all
+            cnt[3] = 0;
+        }
+        if (tid == 0) {
+            cnt[5] = 0;        // slots below the bin
+            cnt[6] = 0;        // slots in the bin
         }
     }
+    __syncthreads();
+    {   // every node of the bins below; then wave 0 takes the boundary bin in index order, so
+        // the detour set (and with it the kept-arc count) is the same on every run
+        const uint32_t bsel = cnt[4], below = cnt[3];
+        for (uint32_t v = tid; v < V; v += BLOCK) {
+            if (binv[v] < bsel) {
+                const uint32_t sl = atomicAdd(&cnt[5], 1u);
+                selx[sl] = v;
+                sela[sl] = row[v];
+            }
+        }
+        if (tid < 64 && bsel < 256) {
+            uint32_t taken = 0;
+            for (uint32_t v0 = 0; v0 < V && below + taken < (uint32_t)K; v0 += 64) {
+                const uint32_t v = v0 + lane;
+                const bool hit = v < V && binv[v] == bsel;
+                const uint64_t m = __ballot(hit);
+                const uint32_t sl = below + taken + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (hit && sl < (uint32_t)K) {
+                    selx[sl] = v;
+                    sela[sl] = row[v];
+                }
+                taken += (uint32_t)__popcll(m);
+            }
+            if (tid == 0) cnt[6] = taken;
+        }
+    }
+    __syncthreads();
+    const uint32_t nsel = min((uint32_t)K, cnt[5] + cnt[6]);
     uint32_t xs[K], as[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-        const uint64_t e = j < (int)P ? s[j] : ~0ull;
-        as[j] = (uint32_t)(e >> 32);
-        xs[j] = (uint32_t)e;
+        xs[j] = (uint32_t)j < nsel ? selx[j] : 0u;
+        as[j] = (uint32_t)j < nsel ? sela[j] : kLat32Inf;
     }
+    if (tid == 0) cnt[0] = 0;
+    __syncthreads();
     const size_t base = (size_t)u * V;
     for (uint32_t v = tid; v < V; v += BLOCK) {  // 2-hop test of every arc of u
         const uint32_t w = row[v];
@@ -996,7 +1072,7 @@ static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
     dense_scatter<<<V, 256, 0, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
                                     ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wk);
     dense_lat<<<div_up(nn, 256), 256, 0, s>>>(Wk, Wl, nn);
-    prune_rows<256, kPruneK><<<V, 256, (size_t)Pw * 8 + (size_t)V * 16 + 16, s>>>(
+    prune_rows<256, kPruneK><<<V, 256, (size_t)V * 18 + (8 + 256 + 2 * kPruneK) * 4, s>>>(
         Wl, Wk, V, Pw, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor);
     SHD_HIP(hipGetLastError());
     *out = ArcView{pbeg, pend, ctx->g_prune_dst.as<uint4>(), 0};
