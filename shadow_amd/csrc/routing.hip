@@ -928,11 +928,15 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
     // per node) at G = 8 and on C3 (BA, ~6 arcs per node) at G = 4
     uint32_t G = deg >= 64 ? 16 : deg >= 24 ? 8 : 4;
     G = env_u32("SHD_SSSP_G", G);          // tuning overrides (results are identical)
-    // Workgroup shape: while two workgroups fit a CU's LDS keep 256 threads (several sources per
-    // CU); once a source's labels need most of the LDS, one 1024-thread workgroup per CU.  The
-    // LDS arc-range cache is dropped when it no longer fits.
+    // Workgroup shape: once a source's labels need most of the LDS, one 1024-thread workgroup
+    // per CU (the LDS arc-range cache is dropped when it no longer fits).  Otherwise rows per CU
+    // decide: with one row or fewer per CU the row's sweeps are the critical path and 16 waves
+    // shorten them (C2, 125 rows: 71 us at 1024 threads vs 151 at 256); with ~4 rows per CU
+    // the CU is full either way and 256 is best (196 vs 252 us).
     const size_t half = ctx->max_lds / 2;
-    uint32_t block = sssp_lds_bytes(P.V, 256, true) <= half ? 256 : 1024;
+    const uint32_t rows_per_cu = div_up(re - rb, (uint32_t)ctx->n_cu);
+    uint32_t block = sssp_lds_bytes(P.V, 256, true) > half ? 1024
+                     : rows_per_cu <= 1 ? 1024 : rows_per_cu <= 2 ? 512 : 256;
     block = env_u32("SHD_SSSP_BLOCK", block);
     if (block != 256 && block != 512 && block != 1024) block = 256;
     const bool cache = sssp_lds_bytes(P.V, block, true) <= ctx->max_lds;
