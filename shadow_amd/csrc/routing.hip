@@ -43,7 +43,7 @@ __device__ __forceinline__ uint64_t ld_lab(const uint64_t* p) {
 
 template <int G, int R, bool CACHE, bool GLAB>
 __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* lab, uint32_t* bits,
-                                           const uint2* rng, const uint32_t* __restrict__ abeg,
+                                           uint32_t scratch, const uint2* rng, const uint32_t* __restrict__ abeg,
                                            const uint32_t* __restrict__ aend,
                                            const uint4* __restrict__ arcs, bool& ovf, bool& dirty) {
     const uint64_t ku = ld_lab<GLAB>(&lab[u]);
@@ -51,32 +51,49 @@ __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* la
     const float qu = one_minus(key_loss(ku));
     const uint2 r = CACHE ? rng[u] : make_uint2(abeg[u], aend[u]);
     for (uint32_t k0 = r.x + gl; k0 < r.y; k0 += G * R) {
-        // issue R independent arc loads, then R relaxations: R arcs in flight per lane
+        // R arc loads, then R label atomics, all issued back to back: the loads are clamped into
+        // the node's range and the atomics are unconditional (a dead slot carries the +inf key,
+        // which min leaves unchanged, aimed at the lane's own scratch label so no two lanes
+        // collide), so no branch splits them and each group waits for one load and one LDS
+        // round trip per R arcs instead of R of each
         uint4 a[R];
+        bool live[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const uint32_t k = k0 + i * G;
-            a[i] = k < r.y ? arcs[k] : make_uint4(0u, kLat32Inf, 0u, 0u);
+            live[i] = k < r.y;
+            a[i] = arcs[live[i] ? k : r.y - 1];
         }
         uint64_t cand[R], old[R];
+        uint32_t tgt[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const uint32_t cl = lu + a[i].y;
-            const bool ok = a[i].y != kLat32Inf && cl >= lu && cl != kLat32Inf;
-            if (a[i].y != kLat32Inf && !ok) ovf = true;   // path latency leaves u32: wide rerun
+            const bool ok = live[i] && a[i].y != kLat32Inf && cl >= lu && cl != kLat32Inf;
+            if (live[i] && a[i].y != kLat32Inf && !ok) ovf = true;   // leaves u32: wide rerun
             cand[i] = ok ? pack_key(cl, fold_q(qu, __uint_as_float(a[i].z))) : kKeyInf;
+            tgt[i] = ok ? a[i].x : scratch;
         }
+        if constexpr (GLAB) {   // global labels: no scratch slots, skip dead slots instead
 #pragma unroll
-        for (int i = 0; i < R; ++i)
-            old[i] = cand[i] != kKeyInf ? atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[i].x]),
-                                                    (unsigned long long)cand[i])
-                                        : 0ull;
+            for (int i = 0; i < R; ++i)
+                old[i] = cand[i] != kKeyInf
+                             ? atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[i].x]), (unsigned long long)cand[i])
+                             : 0ull;
+        } else {
 #pragma unroll
-        for (int i = 0; i < R; ++i)
-            if (cand[i] < old[i]) {
-                atomicOr(&bits[a[i].x >> 5], 1u << (a[i].x & 31));
-                dirty = true;
-            }
+            for (int i = 0; i < R; ++i)
+                old[i] = atomicMin(reinterpret_cast<unsigned long long*>(&lab[tgt[i]]), (unsigned long long)cand[i]);
+        }
+        uint32_t imp = 0;
+#pragma unroll
+        for (int i = 0; i < R; ++i) imp |= (cand[i] < old[i] ? 1u : 0u) << i;
+        if (imp) {
+            dirty = true;
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+                if ((imp >> i) & 1u) atomicOr(&bits[a[i].x >> 5], 1u << (a[i].x & 31));
+        }
     }
 }
 
@@ -177,7 +194,7 @@ __device__ __forceinline__ void sssp_row(
                 for (uint32_t t = 0; t < qn; t += NG) {
                     const uint32_t qi = t + grp;
                     if (qi < qn)
-                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, ovf, dirty);
+                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs, ovf, dirty);
                 }
                 qn = 0;
                 __builtin_amdgcn_wave_barrier();
@@ -235,9 +252,9 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     uint32_t seed_stride) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr uint32_t NW = BLOCK / 64;
-    uint64_t* lab = reinterpret_cast<uint64_t*>(smem);
+    uint64_t* lab = reinterpret_cast<uint64_t*>(smem);   // V labels + 64 per-lane scratch labels
     const uint32_t W = (V + 31) >> 5;
-    uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V);
+    uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V + 64);
     uint32_t* ctl = bits + W;            // [0] dirty  [1] min active latency
     uint32_t* wq = ctl + 4;              // per-wave queue (kQCap + 32 node ids)
     // [V] arc range {beg, end}, 8-byte aligned after the queues
@@ -884,7 +901,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
                          uint64_t* d_lat, float* d_loss, uint32_t delta, const uint32_t* seed,
                          uint32_t seed_stride) {
     PreparedGraph& P = ctx->prep;
-    constexpr int R = G >= 32 ? 2 : 4;   // arcs in flight per lane
+    constexpr int R = G >= 32 ? 2 : G == 4 ? 2 : 4;   // arcs in flight per lane (sparse rows: 2)
     sssp_lds_group<BLOCK, G, R, CACHE><<<re - rb, BLOCK, lds, ctx->stream>>>(
         A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
         ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
@@ -895,7 +912,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
 
 static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
     // labels + bitmap + control + per-wave queues (+ arc ranges, 8-byte aligned)
-    const size_t head = (size_t)V * 8 + (size_t)((V + 31) / 32) * 4 + 16 + (block / 64) * 96 * 4;
+    const size_t head = (size_t)(V + 64) * 8 + (size_t)((V + 31) / 32) * 4 + 16 + (block / 64) * 96 * 4;
     return cache ? ((head + 7) & ~(size_t)7) + (size_t)V * 8 : head;
 }
 
