@@ -901,7 +901,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
                          uint64_t* d_lat, float* d_loss, uint32_t delta, const uint32_t* seed,
                          uint32_t seed_stride) {
     PreparedGraph& P = ctx->prep;
-    constexpr int R = G >= 32 ? 2 : G == 4 ? 2 : 4;   // arcs in flight per lane (sparse rows: 2)
+    constexpr int R = G >= 32 ? 2 : G == 4 ? 2 : 4;   // arcs in flight per lane (R = 6, 8 at G = 8 measured slower on C2)
     sssp_lds_group<BLOCK, G, R, CACHE><<<re - rb, BLOCK, lds, ctx->stream>>>(
         A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
         ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
