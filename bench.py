@@ -313,6 +313,63 @@ def cpu_baseline_relay(rl, lat_table, loss_table, budget_s=8.0):
                        f"mutex + binary-heap push, OpenMP over source hosts)")
 
 
+
+def codel_leg(eng, steps=5, cpu=True):
+    """the destination side of C5 -- 100k CoDel router queues, each fed the
+    ~100 packets a C5 round delivers to it and drained by as many pops (interface reads 2 ms
+    apart, so standing delays cross TARGET for longer than INTERVAL and the drop path runs),
+    one batch per step."""
+    import torch
+    from shadow_amd import _native as N
+    from shadow_amd.codel import CoDelQueues, POP
+    H, per = 100_000, 100
+    rng = np.random.default_rng(6)
+    t0 = 946684800 * 10**9 + 10**9
+    n = H * 2 * per
+    # per host: 100 pushes at arrival times, then 100 pops; arrivals bunched so queues build up
+    arr = np.sort(rng.integers(0, 5 * 10**6, size=(H, per)), axis=1).astype(np.uint64) + np.uint64(t0)
+    pops = arr[:, -1:] + np.arange(1, per + 1, dtype=np.uint64)[None, :] * np.uint64(2_000_000)
+    tarr = np.concatenate([arr, pops], axis=1).reshape(-1)
+    size = np.concatenate([np.full((H, per), 1500, np.uint32), np.full((H, per), POP, np.uint32)], axis=1).reshape(-1)
+    pkt = np.concatenate([np.arange(H * per, dtype=np.uint32).reshape(H, per), np.zeros((H, per), np.uint32)],
+                         axis=1).reshape(-1)
+    off = (np.arange(H + 1, dtype=np.uint64) * (2 * per)).astype(np.uint32)
+    q = CoDelQueues(eng, H, 2 * per)
+    dev = lambda a, dt: torch.from_numpy(a.view(dt)).cuda()  # noqa: E731
+    d_off, d_time, d_size, d_pkt = dev(off, np.int32), dev(tarr, np.int64), dev(size, np.int32), dev(pkt, np.int32)
+    pop_out = torch.empty(n, dtype=torch.int32, device="cuda")
+    fate = torch.zeros(H * per, dtype=torch.int64, device="cuda")
+    ops = N.CodelOps(n, N.ptr(d_off).value, N.ptr(d_time).value, N.ptr(d_size).value, N.ptr(d_pkt).value)
+
+    def step():
+        eng.lib.shd_codel_setup(eng.ctx, H, 2 * per)
+        N.check(eng.lib.shd_codel_run_device(eng.ctx, C.byref(ops), N.ptr(pop_out), N.ptr(fate), H * per),
+                "codel_run")
+    step()
+    torch.cuda.synchronize()
+    s0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - s0) * 1e3 / steps
+    f = fate.cpu().numpy().view(np.uint64)
+    dropped = int(np.count_nonzero((f & np.uint64(3)) == 2))
+    out = {"workload": "C5 destinations: 100k CoDel queues x (100 pushes + 100 pops) per batch",
+           "ops": n, "ms_per_batch": ms, "value": n / (ms * 1e-3), "unit": "queue ops/s",
+           "dropped": dropped, "work": "one lane per host replays its ops in order (sequential state machine)"}
+    if cpu:   # oracle restatement (pure Python, one core) on 2,000 of the hosts
+        from oracle import codel as O
+        k = 2000
+        s1 = time.perf_counter()
+        O.run_ops(k, off[: k + 1], tarr[: 2 * per * k], size[: 2 * per * k], pkt[: 2 * per * k])
+        dt = time.perf_counter() - s1
+        out["cpu_baseline"] = {"value": 2 * per * k / dt, "unit": "queue ops/s", "cores": 1, "kind": "port",
+                               "sample": "oracle/codel.py on 2,000 hosts of the same batch (400k ops)"}
+        _, pop_ref, _ = O.run_ops(k, off[: k + 1], tarr[: 2 * per * k], size[: 2 * per * k], pkt[: 2 * per * k])
+        out["cpu_baseline"]["bit_exact_vs_gpu"] = bool(
+            np.array_equal(np.asarray(pop_ref, np.uint32), pop_out.cpu().numpy().view(np.uint32)[: 2 * per * k]))
+    return out
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -324,6 +381,7 @@ def main():
     ap.add_argument("--no-relay", action="store_true")
     ap.add_argument("--no-c3", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--no-codel", action="store_true")
     args = ap.parse_args()
     world, rank, local = dist_setup(args.gpus)
     from shadow_amd.routing import Engine
@@ -382,6 +440,8 @@ def main():
         res["c3"] = c3_leg(eng)
     if not args.no_c4:
         res["c4"] = c4_leg(eng, world, rank, args.c4_steps)
+    if world == 1 and not args.no_codel:
+        res["codel"] = codel_leg(eng, cpu=not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(res), flush=True)
     eng.close()

@@ -235,6 +235,40 @@ shd_status shd_relay_set_counters(shd_ctx* ctx, int32_t enabled);
 shd_status shd_path_packet_counts(shd_ctx* ctx, uint64_t* counts);
 
 /* ---------------------------------------------------------------------------------------
+ * CoDel inbound router queues.  Replaces CoDelQueue::push / pop
+ * (src/main/network/router/codel_queue.rs:125-306) for every host at once: one queue per host
+ * stays on the device; a call replays a batch of operations, grouped by host, each host's in
+ * time order.  A push carries (time, total size, packet id); a pop (size == SHD_CODEL_POP)
+ * returns the next conforming packet or none, dropping per RFC 8289 as the reference does.
+ * ------------------------------------------------------------------------------------- */
+#define SHD_CODEL_POP 0xFFFFFFFFu
+
+typedef struct shd_codel_ops {   /* device pointers */
+    uint64_t n_ops;
+    const uint32_t* host_off;    /* [n_hosts + 1] */
+    const uint64_t* time;        /* [n_ops] emulated ns (the `now` argument) */
+    const uint32_t* size;        /* [n_ops] packet total size for a push, SHD_CODEL_POP for a pop */
+    const uint32_t* pkt;         /* [n_ops] packet id for a push (ignored for a pop) */
+} shd_codel_ops;
+
+typedef struct shd_codel_state {   /* one host's queue, for inspection (the reference's fields) */
+    uint32_t len, mode;            /* mode: 0 Store, 1 Drop */
+    uint32_t has_interval_end, has_drop_next;
+    uint64_t interval_end, drop_next;
+    uint64_t current_drop_count, previous_drop_count, total_bytes_stored;
+} shd_codel_state;
+
+/* (Re)create n_hosts empty queues holding up to `capacity` packets each. */
+shd_status shd_codel_setup(shd_ctx* ctx, uint32_t n_hosts, uint32_t capacity);
+/* Run a batch.  pop_out[k] = packet id a pop returned (SHD_CODEL_POP for none or for a push);
+ * fate[id] = (op index << 2) | 1 (dequeued) or | 2 (dropped) for every packet this batch
+ * dequeued or dropped (other entries untouched).  SHD_ERR_INVALID: a queue exceeded its
+ * capacity or a packet id >= n_ids (the batch ran; the affected pushes/marks were skipped). */
+shd_status shd_codel_run_device(shd_ctx* ctx, const shd_codel_ops* ops, uint32_t* pop_out,
+                                uint64_t* fate, uint32_t n_ids);
+shd_status shd_codel_get_state(shd_ctx* ctx, uint32_t host, shd_codel_state* out);
+
+/* ---------------------------------------------------------------------------------------
  * GML loader (host code, no GPU needed).  Replaces the reference's
  * gml_parser::parse (src/lib/gml-parser/src/lib.rs:52-57) + NetworkGraph::parse
  * (src/main/network/graph/mod.rs:136-183): GML text -> the shd_graph arrays the routing build

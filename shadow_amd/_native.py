@@ -29,6 +29,7 @@ EXPORTED = [
     "shd_relay_set_counters",
     "shd_path_packet_counts",
     "shd_gml_parse", "shd_gml_graph", "shd_gml_node_bandwidth", "shd_gml_free",
+    "shd_codel_setup", "shd_codel_run_device", "shd_codel_get_state",
 ]
 
 
@@ -71,6 +72,18 @@ class RelayOut(C.Structure):
     _fields_ = [("status", C.c_void_p), ("ev_off", C.c_void_p), ("ev_deliver", C.c_void_p),
                 ("ev_src", C.c_void_p), ("ev_seq", C.c_void_p), ("ev_pkt", C.c_void_p),
                 ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64)]
+
+
+class CodelOps(C.Structure):
+    _fields_ = [("n_ops", C.c_uint64), ("host_off", C.c_void_p), ("time", C.c_void_p),
+                ("size", C.c_void_p), ("pkt", C.c_void_p)]
+
+
+class CodelState(C.Structure):
+    _fields_ = [("len", C.c_uint32), ("mode", C.c_uint32), ("has_interval_end", C.c_uint32),
+                ("has_drop_next", C.c_uint32), ("interval_end", C.c_uint64), ("drop_next", C.c_uint64),
+                ("current_drop_count", C.c_uint64), ("previous_drop_count", C.c_uint64),
+                ("total_bytes_stored", C.c_uint64)]
 
 
 _lib = None
@@ -116,6 +129,9 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_gml_graph": (I32, [P, P]),
         "shd_gml_node_bandwidth": (I32, [P, P, P]),
         "shd_gml_free": (None, [P]),
+        "shd_codel_setup": (I32, [P, U32, U32]),
+        "shd_codel_run_device": (I32, [P, P, P, P, U32]),
+        "shd_codel_get_state": (I32, [P, U32, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

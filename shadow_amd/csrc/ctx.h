@@ -40,6 +40,12 @@ struct DevBuf {
     }
 };
 
+struct CodelState {   // CoDel router queues (codel.hip)
+    DevBuf st, flags, ring, status;
+    uint32_t n_hosts = 0, cap = 0;
+    bool ready = false;
+};
+
 struct RelayState {
     bool ready = false;
     uint32_t n_hosts = 0;
@@ -106,4 +112,5 @@ struct shd_ctx {
         g_dense, g_prune_dst, g_prune_cnt, g_labels, g_aux, g_arc16, g_fw, g_glab;
 
     shd::RelayState relay;
+    shd::CodelState codel;
 };
