@@ -272,7 +272,10 @@ def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=F
         n_sent = step()
     barrier_sync(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
+    pipe = C.c_int32(0)
+    N.check(eng.lib.shd_relay_last_pipeline(eng.ctx, C.byref(pipe)), "last_pipeline")
     return dict(H=H, P=P, dt=dt, ms_per_step=dt / steps * 1e3, n_sent=int(n_sent), batch=b,
+                pipeline=int(pipe.value),
                 host_node=host_node, rng0=rng0, start=start)
 
 
@@ -419,6 +422,7 @@ def main():
         ach = bytes_round / (ms * 1e-3) / 1e9
         rel = {"metric": "packets relayed/s per round", "value": pv, "unit": "packets/s",
                "steps": ks, "ms_per_round": ms, "n_sent_last_round": int(rl["n_sent"]),
+               "pipeline": rl["pipeline"],
                "scaling": "strong",
                "path_counters": "off (reference reads them only in the never-called "
                                 "log_packet_counts; CPU baseline keeps none)",

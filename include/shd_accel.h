@@ -234,6 +234,10 @@ shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t*
 shd_status shd_relay_set_counters(shd_ctx* ctx, int32_t enabled);
 shd_status shd_path_packet_counts(shd_ctx* ctx, uint64_t* counts);
 
+/* Which device pipeline ran the last successful round (diagnostics; no reference counterpart):
+ * 7 = destination-bin placement, 3 = radix sort by destination, 1 = 64-bit records. */
+shd_status shd_relay_last_pipeline(const shd_ctx* ctx, int32_t* pipeline);
+
 /* ---------------------------------------------------------------------------------------
  * CoDel inbound router queues.  Replaces CoDelQueue::push / pop
  * (src/main/network/router/codel_queue.rs:125-306) for every host at once: one queue per host

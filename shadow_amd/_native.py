@@ -26,7 +26,7 @@ EXPORTED = [
     "shd_routing_last_info",
     "shd_routing_lookup", "shd_routing_smallest_latency", "shd_relay_setup", "shd_relay_round",
     "shd_relay_round_device", "shd_events_merge_device", "shd_relay_get_host_state",
-    "shd_relay_set_counters",
+    "shd_relay_set_counters", "shd_relay_last_pipeline",
     "shd_path_packet_counts",
     "shd_gml_parse", "shd_gml_graph", "shd_gml_node_bandwidth", "shd_gml_free",
     "shd_codel_setup", "shd_codel_run_device", "shd_codel_get_state",
@@ -123,6 +123,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_relay_round_device": (I32, [P, P, P, P]),
         "shd_relay_get_host_state": (I32, [P, P, P]),
         "shd_relay_set_counters": (I32, [P, I32]),
+        "shd_relay_last_pipeline": (I32, [P, P]),
         "shd_events_merge_device": (I32, [P, U32, U32, P, P, P, P, P, P, U64, P]),
         "shd_path_packet_counts": (I32, [P, P]),
         "shd_gml_parse": (I32, [P, C.c_size_t, P, P, C.c_size_t]),

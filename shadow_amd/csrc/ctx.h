@@ -53,6 +53,8 @@ struct RelayState {
     bool own_table = false;   // table copied by shd_relay_setup (else: routing resident table)
     bool table_narrow = false;  // every path latency < 2^32 ns -> 16-byte event records (v2)
     bool force_v1 = false;      // SHD_RELAY_FORCE_V1=1 (testing)
+    bool force_v3 = false;      // SHD_RELAY_FORCE_V3=1 (testing): radix pipeline, not v7
+    int last_pipe = 0;          // pipeline of the last round: 1, 3 or 7
     bool count_on = true;       // per-path packet counters (RoutingInfo::increment_packet_count)
     bool last_v2 = false;
     uint64_t seq_bound = 0;     // >= every host's next event id
@@ -61,7 +63,8 @@ struct RelayState {
     DevBuf host_node, order, hn_packed, lat, loss, path, rng, next_id, rng2, next_id2, counts;
     // per-round scratch
     DevBuf pk_off, pk_time, pk_dst, pk_pay, pk_chance, st, ev_key, ev_key2, ev_val, ev_val2,
-        ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, scan_tmp, red, rec, brec, tmp, draws;
+        ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, scan_tmp, red, rec, brec, tmp, draws,
+        bin_cnt, bin_base, bin_lb;
 };
 
 struct PreparedGraph {

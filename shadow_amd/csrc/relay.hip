@@ -315,6 +315,12 @@ struct RelayArgs3 {
     uint4* rec;          // per packet (valid when SENT)
     uint32_t* key;       // per packet: destination host if SENT, else n_hosts (sorts last)
     unsigned long long* red;   // [0] min deliver [1] min latency [2] n_sent [3] bad dst [4] wide
+                               // [5] send-order violation [6] v7 bin overflow
+    // v7 (destination-bin placement): the records of bin b written by stamp workgroup g start at
+    // bin_base[b] + seg_pre[g * n_bins + b]
+    const uint32_t* bin_base;
+    const uint32_t* seg_pre;
+    uint32_t n_bins;
 };
 
 constexpr uint32_t kDrawSlice = 16;   // draws per host per LDS transpose (16: 43 us vs 47 at 8 on C5)
@@ -591,10 +597,22 @@ __device__ unsigned long long g_stamp_prof[12];
 #define SP_MARK(slot) do { } while (0)
 #endif
 
+// BIN (pipeline v7): every packet with a valid destination is also placed, sent or not, into
+// its destination bin (kBinDst consecutive destinations): the workgroup's slots of bin b are
+// the segment bin_base[b] + seg_pre[g][b] counted by relay_bin_hist; the slot inside the
+// segment comes from an LDS counter (four 8-bit counters per word).  The records carry the
+// status and the destination's low bits so bin_sort_v7 can filter and split them.
+constexpr uint32_t kBinShift = 5;
+constexpr uint32_t kBinDst = 1u << kBinShift;
+constexpr uint32_t kHistSplit = 8;   // histogram rows per stamp workgroup (relay_bin_hist)
+
+template <bool BIN>
 __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const uint64_t* __restrict__ draw,
                                                              const uint32_t* __restrict__ packed,
                                                              uint32_t n_words, uint32_t bits) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tbl[];   // packed host -> node
+    uint32_t* s_cur = s_tbl + n_words;                                 // BIN: slot counters
+    if (BIN && a.red[6]) return;   // a bin overflowed its 8-bit counters or LDS stage: the host reruns v3
     __shared__ uint2 s_rows[kS5RowLds];
     __shared__ uint16_t s_scan[kS6Cap + 1];
     __shared__ uint32_t s_host[kS5Hosts], s_beg[kS5Hosts], s_pre[kS5Hosts + 1], s_node[kS5Hosts];
@@ -606,6 +624,8 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     uint64_t sp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, sp_t = __builtin_amdgcn_s_memtime();
 #endif
     for (uint32_t i = tid; i < n_words; i += kS6Threads) s_tbl[i] = packed[i];
+    if (BIN)
+        for (uint32_t i = tid; i < (a.n_bins + 3) / 4; i += kS6Threads) s_cur[i] = 0;
     const uint32_t n_groups = (a.n_hosts + kS5Hosts - 1) / kS5Hosts;
     uint64_t min_d = ~0ull, min_l = ~0ull, ns_total = 0;
     bool wide = false, disorder = false;
@@ -784,12 +804,24 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 const uint32_t pos = tid + kS6Threads * i;
                 if (pos < cn) {
                     a.status[idx[i]] = st[i];
-                    a.key[idx[i]] = st[i] == kStSent ? dst[i] : a.n_hosts;
+                    uint32_t local = 0;
                     if (st[i] == kStSent) {
                         const uint32_t first = max(s_pre[hl[i]], c0) - c0;
-                        const uint32_t local = s_base[hl[i]] + s_run[hl[i]] + s_scan[pos] - s_scan[first];
-                        a.rec[idx[i]] = make_uint4(doff[i], s_host[hl[i]], local, idx[i]);
+                        local = s_base[hl[i]] + s_run[hl[i]] + s_scan[pos] - s_scan[first];
                         if (a.counts) atomicAdd(&a.counts[(size_t)s_node[hl[i]] * a.n_nodes + dn[i]], 1ull);
+                    }
+                    if (!BIN) {
+                        a.key[idx[i]] = st[i] == kStSent ? dst[i] : a.n_hosts;
+                        if (st[i] == kStSent) a.rec[idx[i]] = make_uint4(doff[i], s_host[hl[i]], local, idx[i]);
+                    } else if (dst[i] < a.n_hosts) {
+                        const uint32_t bin = dst[i] >> kBinShift, sh = (bin & 3u) * 8u;
+                        const uint32_t old = atomicAdd(&s_cur[bin >> 2], 1u << sh);
+                        const uint32_t slot = a.bin_base[bin] + a.seg_pre[(size_t)blockIdx.x * a.n_bins + bin] +
+                                              ((old >> sh) & 0xFFu);
+                        a.rec[slot] = make_uint4(doff[i],
+                                                 s_host[hl[i]] | ((dst[i] & (kBinDst - 1)) << 18) |
+                                                     ((uint32_t)st[i] << 24),
+                                                 local, idx[i]);
                     }
                 }
             }
@@ -1316,6 +1348,359 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
 
 // rocPRIM onesweep by destination: RB bits per pass (the default for this key/value pair on
 // gfx950 is 8 -> three passes for 100k hosts; 9 bits covers 2^18 hosts in two passes)
+
+// ==========================================================================================
+// Pipeline v7: destination-bin placement instead of a radix sort.  The stamp writes every
+// packet's record straight into its destination bin (kBinDst destinations); the slots of a
+// (stamp workgroup, bin) pair are counted beforehand by relay_bin_hist, which walks exactly the
+// packets that workgroup will stamp.  bin_sort_v7 then loads one bin into LDS, drops the unsent
+// records, splits the rest by destination and sorts each destination's run by
+// (deliver, packet index) -- packet-index order is (src host, event id) order, the EventQueue
+// tie-break -- so the slot order inside a bin never shows in the output.  Global traffic: the
+// stamp's 16-byte record write plus one coalesced read of it, instead of two radix passes.
+// ==========================================================================================
+constexpr uint32_t kV7MaxHosts = 1u << 18;      // src host bits in the record
+constexpr uint32_t kV7MaxPackets = 1u << 24;    // packet-index bits in bin_sort_v7's key
+constexpr uint32_t kB7Threads = 512;
+constexpr uint32_t kB7Cap = 3584;               // records per bin staged in LDS (C5: ~3200)
+constexpr uint32_t kB7Per = kB7Cap / kB7Threads;
+constexpr unsigned long long kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbMask = (1ull << 62) - 1;
+
+// Histogram row r = g * kHistSplit + k counts, per destination bin, the packets of the host
+// groups g + (k + j * kHistSplit) * G (j = 0, 1, ...) -- together the rows g * kHistSplit + k
+// cover exactly the groups the stamp's workgroup g walks, every packet with a valid
+// destination.  The rows' exclusive prefix at row g * kHistSplit is that workgroup's segment
+// start.  A group's packet positions are flattened over the workgroup (owner by binary search
+// in the 64-entry prefix) with kHistUnroll independent loads in flight per thread.
+constexpr uint32_t kHistUnroll = 8;
+
+__global__ __launch_bounds__(256) void relay_bin_hist(RelayArgs3 a, uint32_t G, uint32_t* __restrict__ cnt) {
+    extern __shared__ uint32_t s_cnt[];
+    __shared__ uint32_t s_beg[kS5Hosts], s_pre[kS5Hosts + 1];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t g = blockIdx.x / kHistSplit, k = blockIdx.x % kHistSplit;
+    for (uint32_t i = tid; i < a.n_bins; i += 256) s_cnt[i] = 0;
+    const uint32_t n_groups = (a.n_hosts + kS5Hosts - 1) / kS5Hosts;
+    for (uint32_t grp = g + k * G; grp < n_groups; grp += kHistSplit * G) {
+        const uint32_t h0 = grp * kS5Hosts, nh = min(kS5Hosts, a.n_hosts - h0);
+        __syncthreads();
+        if (tid < 64) {
+            uint32_t len = 0;
+            if (tid < nh) {
+                const uint32_t h = a.order[h0 + tid];
+                s_beg[tid] = a.src_off[h];
+                len = a.src_off[h + 1] - s_beg[tid];
+            }
+            uint32_t incl = len;
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o);
+                if (lane >= o) incl += y;
+            }
+            if (tid < nh) s_pre[tid + 1] = incl;
+            if (tid == 0) s_pre[0] = 0;
+        }
+        __syncthreads();
+        const uint32_t T = s_pre[nh];
+        for (uint32_t base = 0; base < T; base += 256 * kHistUnroll) {
+            uint32_t d[kHistUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kHistUnroll; ++u) {
+                const uint32_t p = base + u * 256 + tid;
+                d[u] = ~0u;
+                if (p < T) {
+                    uint32_t lo = 0, hi = nh;   // s_pre[lo] <= p < s_pre[lo + 1]
+                    while (hi - lo > 1) {
+                        const uint32_t m = (lo + hi) >> 1;
+                        if (s_pre[m] <= p) lo = m; else hi = m;
+                    }
+                    d[u] = a.dst_host[s_beg[lo] + (p - s_pre[lo])];
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kHistUnroll; ++u)
+                if (d[u] < a.n_hosts) atomicAdd(&s_cnt[d[u] >> kBinShift], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < a.n_bins; i += 256) cnt[(size_t)blockIdx.x * a.n_bins + i] = s_cnt[i];
+}
+
+// seg[g][b] = number of bin-b slots of stamp workgroups before g (the sum of kHistSplit
+// histogram rows per workgroup, exclusive prefix over g); tot[b] = all of bin b.  Lane = bin,
+// wave = a slice of workgroups; every row load of a slice is independent.  A workgroup count
+// that does not fit the stamp's 8-bit slot counters flags red[6].
+constexpr uint32_t kColMaxG = 256;   // stamp workgroups (one per CU)
+
+__global__ __launch_bounds__(1024) void bin_col_scan(uint32_t G, uint32_t n_bins, const uint32_t* __restrict__ cnt,
+                                                     uint32_t* __restrict__ seg, uint32_t* __restrict__ tot,
+                                                     unsigned long long* __restrict__ red) {
+    __shared__ uint32_t s[16][64];
+    constexpr uint32_t kPer = kColMaxG / 16;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, b = blockIdx.x * 64 + lane;
+    const uint32_t g0 = min(G, w * kPer), g1 = min(G, g0 + kPer);
+    uint32_t c[kPer];
+    uint32_t sum = 0;
+    bool over = false;
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+        const uint32_t g = g0 + i;
+        c[i] = 0;
+        if (g < g1 && b < n_bins) {
+#pragma unroll
+            for (uint32_t k = 0; k < kHistSplit; ++k) c[i] += cnt[((size_t)g * kHistSplit + k) * n_bins + b];
+        }
+        over |= c[i] > 0xFFu;
+        sum += c[i];
+    }
+    if (over) atomicOr(&red[6], 1ull);
+    s[w][lane] = sum;
+    __syncthreads();
+    uint32_t run = 0;
+    for (uint32_t u = 0; u < w; ++u) run += s[u][lane];
+    if (b < n_bins) {
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const uint32_t g = g0 + i;
+            if (g < g1) seg[(size_t)g * n_bins + b] = run;
+            run += c[i];
+        }
+        if (w == 15) tot[b] = run;
+    }
+}
+
+// one workgroup: bin_base = exclusive scan of tot (bin_base[n_bins] = total); clears the
+// look-back states and the ticket of bin_sort_v7; a bin larger than its LDS stage flags red[6]
+__global__ __launch_bounds__(1024) void bin_base_scan(uint32_t n_bins, const uint32_t* __restrict__ tot,
+                                                      uint32_t* __restrict__ base,
+                                                      unsigned long long* __restrict__ lb,
+                                                      unsigned long long* __restrict__ red) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t per = (n_bins + 1023) / 1024, b0 = min(n_bins, tid * per), b1 = min(n_bins, b0 + per);
+    uint32_t sum = 0;
+    bool over = false;
+    for (uint32_t b = b0; b < b1; ++b) {
+        sum += tot[b];
+        over |= tot[b] > kB7Cap;
+    }
+    if (over) atomicOr(&red[6], 1ull);
+    uint32_t incl = sum;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (uint32_t u = 0; u < w; ++u) run += s_w[u];
+    for (uint32_t b = b0; b < b1; ++b) {
+        base[b] = run;
+        run += tot[b];
+    }
+    if (tid == 1023) base[n_bins] = run;
+    for (uint32_t b = tid; b <= n_bins; b += 1024) lb[b] = 0;   // lb[n_bins]: the ticket
+}
+
+// 64-bit wave bitonic (element e = lane + 64 c), lane exchanges through xor_lane on both halves
+template <int NPL>
+__device__ __forceinline__ void wave_bitonic64(uint64_t (&k)[NPL], uint32_t lane) {
+#pragma unroll
+    for (uint32_t kk = 2; kk <= 64u * NPL; kk <<= 1) {
+#pragma unroll
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            if (j >= 64) {
+                const uint32_t cj = j / 64;
+#pragma unroll
+                for (int c = 0; c < NPL; ++c) {
+                    if ((c & cj) == 0) {
+                        const bool asc = ((lane + 64u * c) & kk) == 0;
+                        const uint64_t x = k[c], y = k[c | cj];
+                        const bool sw = asc ? (y < x) : (x < y);
+                        k[c] = sw ? y : x;
+                        k[c | cj] = sw ? x : y;
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < NPL; ++c) {
+                    const uint32_t lo = xor_lane((uint32_t)k[c], j, lane);
+                    const uint32_t hi = xor_lane((uint32_t)(k[c] >> 32), j, lane);
+                    const uint64_t o = ((uint64_t)hi << 32) | lo;
+                    const bool take_min = ((lane & j) == 0) == (((lane + 64u * c) & kk) == 0);
+                    k[c] = take_min ? (o < k[c] ? o : k[c]) : (o > k[c] ? o : k[c]);
+                }
+            }
+        }
+    }
+}
+
+struct V7Out {
+    uint64_t* deliver;
+    uint32_t* src;
+    uint64_t* seq;
+    uint32_t* pkt;
+    const uint64_t* seq_base;
+    uint64_t round_end;
+};
+
+__device__ __forceinline__ void v7_emit(const V7Out& o, size_t at, const uint4& r) {
+    const uint32_t src = r.y & (kV7MaxHosts - 1);
+    o.deliver[at] = o.round_end + r.x;
+    o.src[at] = src;
+    o.seq[at] = o.seq_base ? o.seq_base[src] + r.z : r.z;
+    o.pkt[at] = r.w;
+}
+
+// one destination run (bin slots ls[0..n), n <= 256) sorted by (deliver offset, packet index),
+// key = (x - lo) << 32 | (pkt - pmin) << 8 | e  (pkt - pmin < 2^24, e < 256: unique); writes
+// the run's order as slots: pm[rank] = slot
+template <int NPL>
+__device__ __forceinline__ void v7_sort_run(uint32_t n, uint32_t lane, const uint4* x, const uint16_t* ls,
+                                            uint16_t* pm) {
+    uint2 v[NPL];
+    uint32_t lo = ~0u, pmin = ~0u;
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t e = lane + 64u * c;
+        if (e < n) {
+            const uint4 r = x[ls[e]];
+            v[c] = make_uint2(r.x, r.w);
+        } else {
+            v[c] = make_uint2(~0u, ~0u);
+        }
+        lo = min(lo, v[c].x);
+        pmin = min(pmin, v[c].y);
+    }
+    lo = wave_min_u32(lo, lane);
+    pmin = wave_min_u32(pmin, lane);
+    uint64_t k[NPL];
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t e = lane + 64u * c;
+        k[c] = e < n ? ((uint64_t)(v[c].x - lo) << 32) | ((uint64_t)(v[c].y - pmin) << 8) | e : ~0ull;
+    }
+    wave_bitonic64<NPL>(k, lane);
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t rank = lane + 64u * c;
+        if (rank < n) pm[rank] = ls[(uint32_t)k[c] & 0xFFu];
+    }
+}
+
+// K4 (v7): one workgroup per bin, bins taken in ticket order so the event offsets can use a
+// decoupled look-back (publish the bin's sent count, add the predecessors' counts).  The bin's
+// records are staged in LDS, grouped by destination, each run sorted by one wave into the
+// bin's output order, and the bin's events stored in that order (coalesced).
+__global__ __launch_bounds__(kB7Threads) void bin_sort_v7(uint32_t n_hosts, uint32_t n_bins,
+                                                          const uint32_t* __restrict__ bin_base,
+                                                          const uint4* __restrict__ rec,
+                                                          unsigned long long* __restrict__ lb,
+                                                          uint32_t* __restrict__ ev_off, V7Out o,
+                                                          const unsigned long long* __restrict__ red,
+                                                          uint32_t stop) {   // tuning: stop after phase
+    __shared__ uint4 x[kB7Cap];
+    __shared__ uint16_t ls[kB7Cap], pm[kB7Cap];
+    __shared__ uint32_t s_cnt[kBinDst], s_off[kBinDst + 1], s_cur[kBinDst], s_bin, s_excl;
+    if (red[6]) return;   // overflow: the host reruns the round on v3
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_bin = atomicAdd(reinterpret_cast<unsigned int*>(&lb[n_bins]), 1u);
+    if (tid < kBinDst) s_cnt[tid] = s_cur[tid] = 0;
+    __syncthreads();
+    const uint32_t bin = s_bin;
+    const uint32_t B = bin_base[bin], N = bin_base[bin + 1] - B;
+    {   // every load of the bin in flight at once (N <= kB7Cap)
+        uint4 r[kB7Per];
+#pragma unroll
+        for (uint32_t u = 0; u < kB7Per; ++u) {
+            const uint32_t i = tid + u * kB7Threads;
+            if (i < N) r[u] = rec[B + i];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kB7Per; ++u) {
+            const uint32_t i = tid + u * kB7Threads;
+            if (i < N) {
+                x[i] = r[u];
+                if ((r[u].y >> 24) == kStSent) atomicAdd(&s_cnt[(r[u].y >> 18) & (kBinDst - 1)], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    if (stop == 1) return;
+    if (w == 0) {
+        const uint32_t c = lane < kBinDst ? s_cnt[lane] : 0u;
+        uint32_t incl = c;
+        for (uint32_t q = 1; q < 64; q <<= 1) {
+            const uint32_t y = __shfl_up(incl, q);
+            if (lane >= q) incl += y;
+        }
+        if (lane <= kBinDst) s_off[lane] = incl - c;
+        const uint32_t agg = __shfl(incl, 63);
+        unsigned long long excl = 0;
+        if (bin == 0) {
+            if (lane == 0) __hip_atomic_store(&lb[0], kLbIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0) __hip_atomic_store(&lb[bin], kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // look-back 64 predecessors at a time: lane l reads bin hi - l; the nearest inclusive
+            // state ends the walk once every state up to it has been published (bin 0 always is)
+            for (int32_t hi = (int32_t)bin - 1;;) {
+                const int32_t j = hi - (int32_t)lane;
+                const unsigned long long v =
+                    j >= 0 ? __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+                const uint64_t incl_m = __ballot((v & kLbIncl) != 0), zero_m = __ballot(v == 0);
+                const uint32_t fi = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;
+                const uint64_t upto = fi == 64 ? ~0ull : ((2ull << fi) - 1ull);
+                if (zero_m & upto) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                unsigned long long add = lane <= fi ? (v & kLbMask) : 0ull;
+                for (int q = 32; q > 0; q >>= 1) add += __shfl_xor(add, q);
+                excl += add;
+                if (fi < 64) break;
+                hi -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(&lb[bin], kLbIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) s_excl = (uint32_t)excl;
+    }
+    __syncthreads();
+    const uint32_t excl = s_excl, d0 = bin * kBinDst, S = s_off[kBinDst];
+    if (tid < kBinDst && d0 + tid < n_hosts) ev_off[d0 + tid] = excl + s_off[tid];
+    if (tid == 0 && bin == n_bins - 1) ev_off[n_hosts] = excl + S;
+    if (stop == 2) return;
+    for (uint32_t i = tid; i < N; i += kB7Threads) {
+        const uint32_t y = x[i].y;
+        if ((y >> 24) == kStSent) {
+            const uint32_t dl = (y >> 18) & (kBinDst - 1);
+            ls[s_off[dl] + atomicAdd(&s_cur[dl], 1u)] = (uint16_t)i;
+        }
+    }
+    __syncthreads();
+    if (stop == 3) return;
+    for (uint32_t dl = w; dl < kBinDst; dl += kB7Threads / 64) {
+        const uint32_t b = s_off[dl], n = s_off[dl + 1] - b;
+        if (n == 0) continue;
+        if (n <= 64) v7_sort_run<1>(n, lane, x, ls + b, pm + b);
+        else if (n <= 128) v7_sort_run<2>(n, lane, x, ls + b, pm + b);
+        else if (n <= 256) v7_sort_run<4>(n, lane, x, ls + b, pm + b);
+        else {   // long run (rare): rank = number of smaller (deliver, packet) keys
+            for (uint32_t e = lane; e < n; e += 64) {
+                const uint4 q0 = x[ls[b + e]];
+                uint32_t rank = 0;
+                for (uint32_t f = 0; f < n; ++f) {
+                    const uint4 q = x[ls[b + f]];
+                    rank += (q.x < q0.x || (q.x == q0.x && q.w < q0.w)) ? 1u : 0u;
+                }
+                pm[b + rank] = ls[b + e];
+            }
+        }
+    }
+    __syncthreads();
+    if (stop == 4) return;
+    for (uint32_t p = tid; p < S; p += kB7Threads) v7_emit(o, (size_t)excl + p, x[pm[p]]);
+}
+
 template <unsigned RB>
 using DstSortCfg = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
@@ -1343,19 +1728,10 @@ __global__ __launch_bounds__(64) void red_init(unsigned long long* __restrict__ 
     if (t == 0) *n_big = 0;
 }
 
-static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
-                                  shd_relay_out* o) {
+static RelayArgs3 relay_args3(shd_ctx* ctx, const shd_batch* b, const shd_round* rd, shd_relay_out* o) {
     RelayState& R = ctx->relay;
-    hipStream_t s = ctx->stream;
     const uint64_t n = b->n_packets;
     const uint32_t H = R.n_hosts;
-    const size_t nn = std::max<uint64_t>(n, 1);
-    SHD_TRY(R.rec.ensure(nn * 16));
-    SHD_TRY(R.brec.ensure(nn * 16));
-    SHD_TRY(R.ev_val.ensure(nn * 4));    // keys
-    SHD_TRY(R.ev_key.ensure(nn * 4));    // keys (second buffer)
-    SHD_TRY(R.ev_val2.ensure((size_t)(H + 2) * 4));
-    red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.ev_val2.as<uint32_t>());
     RelayArgs3 a{};
     a.n_hosts = H;
     a.n_nodes = R.n_nodes;
@@ -1377,18 +1753,34 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.bootstrap_end = rd->bootstrap_end;
     // event ids below 2^32 for the whole round: records carry absolute ids, no per-event gather
     a.abs_seq = R.seq_bound + n < (1ull << 32) ? 1u : 0u;
-    const uint64_t* seq_base = a.abs_seq ? nullptr : R.next_id.as<uint64_t>();
     a.status = o->status;
     a.rec = R.rec.as<uint4>();
     a.key = R.ev_val.as<uint32_t>();
     a.red = R.red.as<unsigned long long>();
-    if (!b->chance) {   // K0: the per-host generator streams
-        SHD_TRY(R.draws.ensure(nn * 8));
+    return a;
+}
+
+static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                                  shd_relay_out* o) {
+    RelayState& R = ctx->relay;
+    hipStream_t s = ctx->stream;
+    const uint64_t n = b->n_packets;
+    const uint32_t H = R.n_hosts;
+    const size_t nn = std::max<uint64_t>(n, 1);
+    SHD_TRY(R.rec.ensure(nn * 16));
+    SHD_TRY(R.brec.ensure(nn * 16));
+    SHD_TRY(R.ev_val.ensure(nn * 4));    // keys
+    SHD_TRY(R.ev_key.ensure(nn * 4));    // keys (second buffer)
+    SHD_TRY(R.ev_val2.ensure((size_t)(H + 2) * 4));
+    SHD_TRY(R.draws.ensure(nn * 8));
+    red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.ev_val2.as<uint32_t>());
+    RelayArgs3 a = relay_args3(ctx, b, rd, o);
+    const uint64_t* seq_base = a.abs_seq ? nullptr : R.next_id.as<uint64_t>();
+    if (!b->chance)   // K0: the per-host generator streams
         relay_draws<<<div_up(H, 64), 64, 0, s>>>(a, R.draws.as<uint64_t>());
-    }
     if (R.hn_bits) {   // host -> node map fits the LDS: persistent stamp, no node gathers
         const uint32_t groups = div_up(H, kS5Hosts);
-        relay_stamp_v6<<<std::min<uint32_t>(groups, (uint32_t)ctx->n_cu), kS6Threads,
+        relay_stamp_v6<false><<<std::min<uint32_t>(groups, (uint32_t)ctx->n_cu), kS6Threads,
                          (size_t)R.hn_words * 4, s>>>(a, R.draws.as<uint64_t>(),
                                                       R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     } else {
@@ -1421,6 +1813,64 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     return SHD_OK;
 }
 
+
+// v7 eligibility: narrow table, LDS host map, src ids and packet indices within the record /
+// key fields, and the stamp's LDS (map + slot counters) within the CU's 160 KB
+static bool relay_v7_ok(shd_ctx* ctx, uint64_t n) {
+    RelayState& R = ctx->relay;
+    if (!R.hn_bits || R.force_v3 || R.n_hosts > kV7MaxHosts || n > kV7MaxPackets) return false;
+    if (std::min<uint32_t>(div_up(R.n_hosts, kS5Hosts), (uint32_t)ctx->n_cu) > kColMaxG) return false;
+    static size_t stat_lds = 0;
+    if (!stat_lds) {
+        hipFuncAttributes at{};
+        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&relay_stamp_v6<true>)) != hipSuccess) return false;
+        stat_lds = at.sharedSizeBytes;
+    }
+    const uint32_t n_bins = div_up(R.n_hosts, kBinDst);
+    return stat_lds + (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4 <= 160 * 1024;
+}
+
+static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                                  shd_relay_out* o) {
+    RelayState& R = ctx->relay;
+    hipStream_t s = ctx->stream;
+    const uint64_t n = b->n_packets;
+    const uint32_t H = R.n_hosts;
+    const size_t nn = std::max<uint64_t>(n, 1);
+    const uint32_t n_bins = div_up(H, kBinDst);
+    const uint32_t G = std::min<uint32_t>(div_up(H, kS5Hosts), (uint32_t)ctx->n_cu);
+    SHD_TRY(R.rec.ensure(nn * 16));
+    SHD_TRY(R.draws.ensure(nn * 8));
+    SHD_TRY(R.bin_cnt.ensure((size_t)G * (kHistSplit + 1) * n_bins * 4));
+    SHD_TRY(R.bin_base.ensure((size_t)(2 * n_bins + 1) * 4));
+    SHD_TRY(R.bin_lb.ensure((size_t)(n_bins + 1) * 8));
+    red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.bin_base.as<uint32_t>());
+    RelayArgs3 a = relay_args3(ctx, b, rd, o);
+    uint32_t* tot = R.bin_base.as<uint32_t>() + n_bins + 1;
+    a.bin_base = R.bin_base.as<uint32_t>();
+    a.n_bins = n_bins;
+    uint32_t* seg = R.bin_cnt.as<uint32_t>() + (size_t)G * kHistSplit * n_bins;
+    a.seg_pre = seg;
+    relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
+    bin_col_scan<<<div_up(n_bins, 64), 1024, 0, s>>>(G, n_bins, R.bin_cnt.as<uint32_t>(), seg, tot, a.red);
+    bin_base_scan<<<1, 1024, 0, s>>>(n_bins, tot, R.bin_base.as<uint32_t>(), R.bin_lb.as<unsigned long long>(), a.red);
+    if (!b->chance)   // K0: the per-host generator streams
+        relay_draws<<<div_up(H, 64), 64, 0, s>>>(a, R.draws.as<uint64_t>());
+    relay_stamp_v6<true><<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4, s>>>(
+        a, R.draws.as<uint64_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
+    V7Out vo{o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt,
+             a.abs_seq ? nullptr : R.next_id.as<uint64_t>(), rd->round_end};
+    const char* stop = std::getenv("SHD_B7_STOP");   // tuning only: partial K4 (wrong output)
+    bin_sort_v7<<<n_bins, kB7Threads, 0, s>>>(H, n_bins, R.bin_base.as<uint32_t>(), R.rec.as<uint4>(),
+                                             R.bin_lb.as<unsigned long long>(), o->ev_off, vo, a.red,
+                                             stop && *stop ? (uint32_t)std::atoi(stop) : 0u);
+    SHD_HIP(hipGetLastError());
+    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 8, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    std::memcpy(R.red_host, ctx->h_pin + 8, sizeof(R.red_host));
+    return SHD_OK;
+}
+
 // One round: the new host state (RNG streams, event ids) is written to the second buffer and
 // committed only when the round succeeds, so a failed round leaves the hosts untouched.
 static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
@@ -1431,10 +1881,21 @@ static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round
     SHD_TRY(R.dst_cnt.ensure((size_t)(H + 1) * 4));
     SHD_TRY(R.scan_tmp.ensure(64));
     bool v2 = R.table_narrow && !R.force_v1;
+    R.last_pipe = 1;
     if (v2) {
-        SHD_TRY(relay_device_v3(ctx, b, rd, o));
+        bool done = false;
+        if (relay_v7_ok(ctx, b->n_packets)) {
+            SHD_TRY(relay_device_v7(ctx, b, rd, o));
+            done = !R.red_host[6];   // else a bin overflowed: redo with the radix pipeline
+            R.last_pipe = 7;
+        }
+        if (!done) {
+            SHD_TRY(relay_device_v3(ctx, b, rd, o));
+            R.last_pipe = 3;
+        }
         if (R.red_host[4]) v2 = false;   // a deliver offset needs 64 bits: redo with v1
     }
+    if (!v2) R.last_pipe = 1;
     if (!v2) SHD_TRY(relay_device_v1(ctx, b, rd, o));
     if (R.red_host[3] != ~0ull) return SHD_ERR_NO_HOST;
     if (v2 && R.red_host[5]) return SHD_ERR_INVALID;   // a host's send times went backwards
@@ -1522,6 +1983,8 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
     {
         const char* v = std::getenv("SHD_RELAY_FORCE_V1");
         R.force_v1 = v && *v == '1';
+        const char* v3 = std::getenv("SHD_RELAY_FORCE_V3");   // testing: radix pipeline instead of v7
+        R.force_v3 = v3 && *v3 == '1';
     }
     {   // bit-packed host -> node map for the LDS-resident stamp, when it fits
         uint32_t bits = 1;
@@ -1651,6 +2114,12 @@ shd_status shd_events_merge_device(shd_ctx* ctx, uint32_t n_runs, uint32_t n_dst
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipStreamSynchronize(s));
     d_out->n_sent = n_events;
+    return SHD_OK;
+}
+
+shd_status shd_relay_last_pipeline(const shd_ctx* ctx, int32_t* pipeline) {
+    if (!ctx || !pipeline) return SHD_ERR_INVALID;
+    *pipeline = ctx->relay.last_pipe;
     return SHD_OK;
 }
 

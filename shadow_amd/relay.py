@@ -103,6 +103,12 @@ class Relay:
                 "shd_relay_get_host_state")
         return rng, nid
 
+    def last_pipeline(self) -> int:
+        """Device pipeline of the last round: 7 bin placement, 3 radix sort, 1 64-bit records."""
+        v = C.c_int32(0)
+        N.check(self.eng.lib.shd_relay_last_pipeline(self.eng.ctx, C.byref(v)), "last_pipeline")
+        return v.value
+
     def packet_counts(self):
         c = np.zeros((self.n_nodes, self.n_nodes), np.uint64)
         N.check(self.eng.lib.shd_path_packet_counts(self.eng.ctx, N.ptr(c)), "packet_counts")

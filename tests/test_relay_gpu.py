@@ -46,13 +46,14 @@ def _c5_like(n_hosts, n_nodes, n_packets, seed, start=10**9, runahead=10**6):
     return lat, loss, synth.c5_host_nodes(n_hosts, n_nodes), synth.host_rng_states(n_hosts, 1), b
 
 
-@pytest.mark.parametrize("force_v1", [False, True])
+@pytest.mark.parametrize("pipe", [7, 3, 1])
 @pytest.mark.parametrize("chance_mode", [False, True])
-def test_multi_round_vs_c_oracle(engine, chance_mode, force_v1, monkeypatch):
+def test_multi_round_vs_c_oracle(engine, chance_mode, pipe, monkeypatch):
     """Three consecutive rounds on 20k hosts / 1M packets: streams and ids carry across rounds
-    (both the 16-byte-record pipeline and the 64-bit fallback pipeline)."""
+    (bin-placement pipeline, radix-sort pipeline and the 64-bit fallback pipeline)."""
     from shadow_amd.relay import Relay
-    monkeypatch.setenv("SHD_RELAY_FORCE_V1", "1" if force_v1 else "0")
+    monkeypatch.setenv("SHD_RELAY_FORCE_V1", "1" if pipe == 1 else "0")
+    monkeypatch.setenv("SHD_RELAY_FORCE_V3", "1" if pipe == 3 else "0")
     H, NN = 20_000, 200
     lat, loss, host_node, rng0, _ = _c5_like(H, NN, 1000, 11)
     nid0 = np.zeros(H, np.uint64)
@@ -78,7 +79,38 @@ def test_multi_round_vs_c_oracle(engine, chance_mode, force_v1, monkeypatch):
         assert (r.min_deliver, r.min_latency, r.n_sent) == (o["min_deliver"], o["min_latency"], o["n_sent"])
         st, nid = rl.host_state()
         assert np.array_equal(st, orng) and np.array_equal(nid, onid)
+        assert rl.last_pipeline() == pipe
         start += ra
+
+
+@pytest.mark.parametrize("rel_ids", [False, True])
+def test_bin_pipeline_long_runs(engine, rel_ids):
+    """Pipeline 7 with destination runs in every class of its per-destination sort: wave
+    bitonic (<= 64, <= 128, <= 256 events) and the rank sort of longer runs, inside bins that
+    still fit the LDS stage; event ids absolute (32-bit) or relative to a base above 2^40."""
+    from shadow_amd.relay import Relay
+    H, NN = 3000, 40
+    lat, loss, host_node, rng0, b = _c5_like(H, NN, 150_000, 17)
+    dst = b.dst_host.copy()
+    dst[::300] = 7        # ~500 extra events: rank-sort run
+    dst[1::1000] = 70     # ~150 extra: 256-wide bitonic
+    dst[2::2000] = 130    # ~75 extra: 128-wide bitonic
+    src = np.repeat(np.arange(H), np.diff(b.src_off)).astype(np.uint32)
+    dst[(dst == src)] = (dst[(dst == src)] + 1) % H
+    nid0 = (np.arange(H, dtype=np.uint64) + np.uint64(2**41)) if rel_ids else np.zeros(H, np.uint64)
+    o = corc.relay_round(b.src_off, b.send_time, dst, b.payload, host_node, lat, loss, rng0.copy(),
+                         nid0.copy(), 10**9 + 10**6, 10**12, 0)
+    rl = Relay(host_node, rng0, nid0, lat, loss, engine=engine)
+    r = rl.round(b.src_off, b.send_time, dst, b.payload, 10**9 + 10**6, 10**12, 0)
+    assert rl.last_pipeline() == 7
+    ev = o["events"]
+    sizes = np.diff(ev["off"].astype(np.int64))
+    assert sizes[7] > 256 and 128 < sizes[70] <= 256 and 64 < sizes[130] <= 128
+    assert np.array_equal(r.status, o["status"])
+    assert np.array_equal(r.ev_off, ev["off"])
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(r, "ev_" + k), ev[k]), k
+    assert (r.min_deliver, r.min_latency, r.n_sent) == (o["min_deliver"], o["min_latency"], o["n_sent"])
 
 
 def test_hot_destination_bucket(engine):
@@ -98,6 +130,7 @@ def test_hot_destination_bucket(engine):
     r = rl.round(b.src_off, b.send_time, dst, b.payload, 10**9 + 10**6, 10**12, 0)
     ev = o["events"]
     assert int(ev["off"][8] - ev["off"][7]) > 1024
+    assert rl.last_pipeline() == 3   # the hot bin overflows pipeline 7's LDS stage: radix rerun
     assert np.array_equal(r.ev_off, ev["off"])
     for k in ("deliver", "src", "seq", "pkt"):
         assert np.array_equal(getattr(r, "ev_" + k), ev[k]), k
