@@ -76,6 +76,16 @@ shd_ctx* shd_open(int device_ordinal, shd_status* st) {
             shd_close(ctx);
             return fail(SHD_ERR_HIP);
         }
+    for (auto& e : ctx->sev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+            shd_close(ctx);
+            return fail(SHD_ERR_HIP);
+        }
+    if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess) {
+        ctx->side = nullptr;
+        shd_close(ctx);
+        return fail(SHD_ERR_HIP);
+    }
     if (st) *st = SHD_OK;
     return ctx;
 }
@@ -84,8 +94,12 @@ void shd_close(shd_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->side) (void)hipStreamSynchronize(ctx->side);
     for (auto& e : ctx->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : ctx->sev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;  // DevBuf destructors free device memory

@@ -97,6 +97,8 @@ struct shd_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     hipEvent_t ev[8] = {};
+    hipStream_t side = nullptr;        // second stream: work that overlaps the main stream's
+    hipEvent_t sev[2] = {};            // fork / join events (no timing)
     unsigned long long* h_pin = nullptr;   // 64 pinned host words: flag / reduction read-backs
     int n_cu = 0;
     size_t max_lds = 0;

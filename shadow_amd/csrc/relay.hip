@@ -11,14 +11,13 @@
 // then src event id.  Every event of round r has deliver >= round_end, so batching the whole
 // round to the barrier (core/manager.rs:455-464) is exact.
 //
-// Pipeline (one stream, no host sync inside):
-//   K1 relay_stamp     one lane per source host walks its sends in order (the RNG stream and
-//                      the event-id counter are sequential per host); gathers the path, draws,
-//                      decides, stamps; claims a slot in the destination bucket (atomic count).
-//   K2 scan            exclusive scan of per-destination counts -> event offsets.
-//   K3 relay_scatter   one lane per packet scatters its event into the destination bucket.
-//   K4 segment_sort    one workgroup per destination sorts its bucket by the full event key
-//                      (unique), so the atomic slot order never shows in the output.
+// Pipelines (one stream plus a side stream for K0, one host sync per round):
+//   7  K0 draws || bin histogram + scans; K1 stamp places every record into its destination
+//      bin (32 destinations); K4 bin_sort_v7 sorts each bin in LDS (decoupled look-back for
+//      the event offsets) and stores the events in order
+//   3  K0; K1 stamp writes records by packet; K2 radix sort by destination; K3 offsets; K4
+//      per-destination wave sort (fallback when a bin overflows pipeline 7's limits)
+//   1  64-bit records (path latencies >= 2^32 ns)
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -1851,11 +1850,16 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.n_bins = n_bins;
     uint32_t* seg = R.bin_cnt.as<uint32_t>() + (size_t)G * kHistSplit * n_bins;
     a.seg_pre = seg;
+    if (!b->chance) {   // K0: the per-host generator streams, on the side stream next to the bins
+        SHD_HIP(hipEventRecord(ctx->sev[0], s));
+        SHD_HIP(hipStreamWaitEvent(ctx->side, ctx->sev[0], 0));
+        relay_draws<<<div_up(H, 64), 64, 0, ctx->side>>>(a, R.draws.as<uint64_t>());
+        SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));
+    }
     relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
     bin_col_scan<<<div_up(n_bins, 64), 1024, 0, s>>>(G, n_bins, R.bin_cnt.as<uint32_t>(), seg, tot, a.red);
     bin_base_scan<<<1, 1024, 0, s>>>(n_bins, tot, R.bin_base.as<uint32_t>(), R.bin_lb.as<unsigned long long>(), a.red);
-    if (!b->chance)   // K0: the per-host generator streams
-        relay_draws<<<div_up(H, 64), 64, 0, s>>>(a, R.draws.as<uint64_t>());
+    if (!b->chance) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
     relay_stamp_v6<true><<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4, s>>>(
         a, R.draws.as<uint64_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     V7Out vo{o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt,

@@ -5,8 +5,9 @@ FETCH_SIZE / WRITE_SIZE are in KB.  The read counter is calibrated on tools/bw_p
 applied to every kernel's FETCH_SIZE (MI355X guide: gfx950 tallies wide reads at half), the
 write counter is taken as is (kA's writes come out within a few percent of the byte count).
   routing: sssp_lds_group, one launch (the C2 build's dominant kernel)
-  relay:   every relay kernel of one round (K0 draws, K1 stamp, K2 radix passes, K3 offsets,
-           K4 segment sorts), summed and divided by the number of rounds
+  relay:   every relay kernel of one round (pipeline 7: K0 draws, bin histogram + scans, K1
+           stamp, K4 bin sort; pipeline 3: K0, K1, K2 radix passes, K3 offsets, K4 segment
+           sorts), summed and divided by the number of rounds
 """
 import csv
 import json
@@ -44,7 +45,8 @@ def per_launch(sel):
 sssp = per_launch(lambda k: "sssp_lds_group" in k)
 r_read = sum(v[0] * v[2] for v in sssp.values()) / sum(v[2] for v in sssp.values())
 r_write = sum(v[1] * v[2] for v in sssp.values()) / sum(v[2] for v in sssp.values())
-relay_sel = ("relay_draws", "relay_stamp", "rocprim", "bucket_offsets", "segment_sort")
+relay_sel = ("relay_draws", "relay_stamp", "rocprim", "bucket_offsets", "segment_sort", "relay_bin_hist",
+             "bin_col_scan", "bin_base_scan", "bin_sort_v7")
 relay = per_launch(lambda k: any(s in k for s in relay_sel))
 rounds = sum(v[2] for k, v in relay.items() if "relay_stamp" in k)
 rel_read = sum(v[0] * v[2] for v in relay.values()) / rounds
@@ -64,3 +66,13 @@ doc = {
 os.makedirs(os.path.dirname(dst), exist_ok=True)
 json.dump(doc, open(dst, "w"), indent=1)
 print(json.dumps({k: doc[k] for k in ("read_factor", "write_factor_measured", "routing", "relay")}))
+
+# the raw per-kernel means behind the numbers above (KB per launch, uncalibrated)
+if len(sys.argv) > 3:
+    with open(sys.argv[3], "w", newline="") as f:
+        wr = csv.writer(f)
+        wr.writerow(["run", "counter", "kernel", "launches", "mean_KB"])
+        for run in ("probe", "bench"):
+            for c in ("FETCH_SIZE", "WRITE_SIZE"):
+                for k, v in sorted(load(run, c).items()):
+                    wr.writerow([run, c, k.split("(")[0], len(v), round(sum(v) / len(v) / 1e3, 1)])
