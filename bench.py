@@ -373,6 +373,64 @@ def codel_leg(eng, steps=5, cpu=True):
             np.array_equal(np.asarray(pop_ref, np.uint32), pop_out.cpu().numpy().view(np.uint32)[: 2 * per * k]))
     return out
 
+
+def tbucket_leg(eng, steps=5, cpu=True):
+    """the source side of C5 -- 100k upstream relays, each with the token
+    bucket of a 10 Mbit/s interface (create_token_bucket: 1,250 B per 1 ms refill, capacity
+    2,750 B) and ~100 forwarding attempts of C5 sizes spread over 20 ms, so buckets run dry,
+    block and skip.  The buckets are re-created each step (identical work per step)."""
+    import torch
+    from shadow_amd import _native as N
+    from shadow_amd.tbucket import SIM_START, create_token_bucket
+    H, per = 100_000, 100
+    rng = np.random.default_rng(7)
+    t0 = SIM_START + 10**9
+    n = H * per
+    tarr = (np.sort(rng.integers(0, 20 * 10**6, size=(H, per)), axis=1).astype(np.uint64)
+            + np.uint64(t0)).reshape(-1)
+    u = rng.random(n)
+    size = np.where(u < 0.2, 66, np.where(u < 0.8, 1514, rng.integers(67, 1515, n))).astype(np.uint32)
+    flags = np.zeros(n, np.uint8)
+    off = (np.arange(H + 1, dtype=np.uint64) * per).astype(np.uint32)
+    c, i, v = create_token_bucket(10_000_000 // 8)
+    caps, incs, itvs, last = (np.full(H, x, np.uint64) for x in (c, i, v, t0))
+    dev = lambda a, dt: torch.from_numpy(a.view(dt)).cuda()  # noqa: E731
+    d_off, d_time, d_size, d_flags = dev(off, np.int32), dev(tarr, np.int64), dev(size, np.int32), dev(flags, np.uint8)
+    status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    value = torch.empty(n, dtype=torch.int64, device="cuda")
+    ops = N.TbOps(n, N.ptr(d_off).value, N.ptr(d_time).value, N.ptr(d_size).value, N.ptr(d_flags).value)
+
+    def step():
+        N.check(eng.lib.shd_tb_setup(eng.ctx, H, N.ptr(caps), N.ptr(incs), N.ptr(itvs), N.ptr(last)), "tb_setup")
+        N.check(eng.lib.shd_tb_run_device(eng.ctx, C.byref(ops), N.ptr(status), N.ptr(value)), "tb_run")
+    step()
+    torch.cuda.synchronize()
+    s0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - s0) * 1e3 / steps
+    st = status.cpu().numpy()
+    out = {"workload": "C5 sources: 100k token-bucket relays (10 Mbit/s) x 100 forwarding attempts per batch",
+           "ops": n, "ms_per_batch": ms, "value": n / (ms * 1e-3), "unit": "relay attempts/s",
+           "forwarded": int(np.count_nonzero(st == 0)), "blocked": int(np.count_nonzero(st == 1)),
+           "skipped": int(np.count_nonzero(st == 2)),
+           "work": "one lane per relay replays its attempts in order (sequential state machine); "
+                   "step includes shd_tb_setup (host -> device copy of 100k buckets)"}
+    if cpu:   # oracle restatement (pure Python, one core) on 2,000 of the relays
+        from oracle import token_bucket as O
+        k = 2000
+        bk = [O.TokenBucket(c, i, v, t0) for _ in range(k)]
+        s1 = time.perf_counter()
+        ost, oval = O.relay_run(bk, [0] * k, off[: k + 1], tarr[: per * k], size[: per * k], flags[: per * k])
+        dt = time.perf_counter() - s1
+        out["cpu_baseline"] = {"value": per * k / dt, "unit": "relay attempts/s", "cores": 1, "kind": "port",
+                               "sample": "oracle/token_bucket.py on 2,000 relays of the same batch (200k attempts)",
+                               "bit_exact_vs_gpu": bool(
+                                   np.array_equal(np.asarray(ost, np.uint8), st[: per * k]) and np.array_equal(
+                                       np.asarray(oval, np.uint64), value.cpu().numpy().view(np.uint64)[: per * k]))}
+    return out
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -385,6 +443,7 @@ def main():
     ap.add_argument("--no-c3", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--no-codel", action="store_true")
+    ap.add_argument("--no-tbucket", action="store_true")
     args = ap.parse_args()
     world, rank, local = dist_setup(args.gpus)
     from shadow_amd.routing import Engine
@@ -446,6 +505,8 @@ def main():
         res["c4"] = c4_leg(eng, world, rank, args.c4_steps)
     if world == 1 and not args.no_codel:
         res["codel"] = codel_leg(eng, cpu=not args.no_cpu_baseline)
+    if world == 1 and not args.no_tbucket:
+        res["tbucket"] = tbucket_leg(eng, cpu=not args.no_cpu_baseline)
     if rank == 0:
         print(json.dumps(res), flush=True)
     eng.close()

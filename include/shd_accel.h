@@ -273,6 +273,48 @@ shd_status shd_codel_run_device(shd_ctx* ctx, const shd_codel_ops* ops, uint32_t
 shd_status shd_codel_get_state(shd_ctx* ctx, uint32_t host, shd_codel_state* out);
 
 /* ---------------------------------------------------------------------------------------
+ * Token-bucket relays.  Replaces TokenBucket::conforming_remove
+ * (src/main/network/relay/token_bucket.rs:68-157) as Relay::forward_until_blocked calls it
+ * (src/main/network/relay/mod.rs:200-287), for every relay at once: one bucket per relay stays
+ * on the device; a call replays a batch of forwarding attempts, grouped by relay, each relay's
+ * in time order.  An attempt is FORWARDED (value = the balance after it; UINT64_MAX for a relay
+ * without a bucket), BLOCKED (value = the duration until it would conform; the relay is then
+ * Pending until now + value, as forward_later schedules it) or SKIPPED (made while the relay
+ * was Pending; value = the pending deadline).  Flag SHD_TB_EXEMPT: a local packet or one sent
+ * while bootstrapping, forwarded without tokens (relay/mod.rs:224-229).
+ * ------------------------------------------------------------------------------------- */
+#define SHD_TB_FORWARDED 0
+#define SHD_TB_BLOCKED 1
+#define SHD_TB_SKIPPED 2
+#define SHD_TB_EXEMPT 1u
+
+typedef struct shd_tb_ops {     /* device pointers */
+    uint64_t n_ops;
+    const uint32_t* relay_off;  /* [n_relays + 1] */
+    const uint64_t* time;       /* [n_ops] emulated ns (Worker::current_time) */
+    const uint32_t* size;       /* [n_ops] packet total size (tokens to remove) */
+    const uint8_t* flags;       /* [n_ops] SHD_TB_EXEMPT or 0 */
+} shd_tb_ops;
+
+typedef struct shd_tb_state {   /* one relay's bucket, for inspection (the reference's fields) */
+    uint64_t capacity, balance, refill_increment, refill_interval, last_refill, pending_until;
+} shd_tb_state;
+
+/* (Re)create n_relays buckets (TokenBucket::new_inner, token_bucket.rs:37-60; full at start).
+ * All three parameters 0 = no bucket (RateLimit::Unlimited); some but not all 0 is
+ * SHD_ERR_INVALID (the reference's new() returns None and its caller unwraps).  Host arrays;
+ * create_token_bucket (relay/mod.rs:291-302) is capacity = max(1, Bps/1000) + 1500,
+ * increment = max(1, Bps/1000), interval = 1 ms. */
+shd_status shd_tb_setup(shd_ctx* ctx, uint32_t n_relays, const uint64_t* capacity,
+                        const uint64_t* refill_increment, const uint64_t* refill_interval_ns,
+                        const uint64_t* last_refill);
+/* Run a batch (device pointers); status[k] / value[k] per attempt.  SHD_ERR_INVALID where the
+ * reference panics (a time before the bucket's last refill, a SimulationTime past SIMTIME_MAX);
+ * the batch still ran. */
+shd_status shd_tb_run_device(shd_ctx* ctx, const shd_tb_ops* ops, uint8_t* status, uint64_t* value);
+shd_status shd_tb_get_state(shd_ctx* ctx, uint32_t relay, shd_tb_state* out);
+
+/* ---------------------------------------------------------------------------------------
  * GML loader (host code, no GPU needed).  Replaces the reference's
  * gml_parser::parse (src/lib/gml-parser/src/lib.rs:52-57) + NetworkGraph::parse
  * (src/main/network/graph/mod.rs:136-183): GML text -> the shd_graph arrays the routing build

@@ -30,6 +30,7 @@ EXPORTED = [
     "shd_path_packet_counts",
     "shd_gml_parse", "shd_gml_graph", "shd_gml_node_bandwidth", "shd_gml_free",
     "shd_codel_setup", "shd_codel_run_device", "shd_codel_get_state",
+    "shd_tb_setup", "shd_tb_run_device", "shd_tb_get_state",
 ]
 
 
@@ -77,6 +78,16 @@ class RelayOut(C.Structure):
 class CodelOps(C.Structure):
     _fields_ = [("n_ops", C.c_uint64), ("host_off", C.c_void_p), ("time", C.c_void_p),
                 ("size", C.c_void_p), ("pkt", C.c_void_p)]
+
+
+class TbOps(C.Structure):
+    _fields_ = [("n_ops", C.c_uint64), ("relay_off", C.c_void_p), ("time", C.c_void_p),
+                ("size", C.c_void_p), ("flags", C.c_void_p)]
+
+
+class TbState(C.Structure):
+    _fields_ = [("capacity", C.c_uint64), ("balance", C.c_uint64), ("refill_increment", C.c_uint64),
+                ("refill_interval", C.c_uint64), ("last_refill", C.c_uint64), ("pending_until", C.c_uint64)]
 
 
 class CodelState(C.Structure):
@@ -133,6 +144,9 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_codel_setup": (I32, [P, U32, U32]),
         "shd_codel_run_device": (I32, [P, P, P, P, U32]),
         "shd_codel_get_state": (I32, [P, U32, P]),
+        "shd_tb_setup": (I32, [P, U32, P, P, P, P]),
+        "shd_tb_run_device": (I32, [P, P, P, P]),
+        "shd_tb_get_state": (I32, [P, U32, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -7,7 +7,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = [os.path.join(HERE, "csrc", f) for f in ("routing.hip", "blocked.hip", "relay.hip", "api.cpp", "gml.cpp", "codel.hip")]
+SRC = [os.path.join(HERE, "csrc", f) for f in ("routing.hip", "blocked.hip", "relay.hip", "api.cpp", "gml.cpp", "codel.hip", "tbucket.hip")]
 OUT = os.path.join(HERE, "libshd_accel.so")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          # Rust never contracts 1-(1-p)*(1-e) into an FMA: keep every f32 op separately rounded

@@ -46,6 +46,12 @@ struct CodelState {   // CoDel router queues (codel.hip)
     bool ready = false;
 };
 
+struct TbState {   // token-bucket relays (tbucket.hip)
+    DevBuf st, err;
+    uint32_t n_relays = 0;
+    bool ready = false;
+};
+
 struct RelayState {
     bool ready = false;
     uint32_t n_hosts = 0;
@@ -118,4 +124,5 @@ struct shd_ctx {
 
     shd::RelayState relay;
     shd::CodelState codel;
+    shd::TbState tb;
 };
