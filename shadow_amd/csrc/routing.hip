@@ -449,27 +449,30 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
     }
     __syncthreads();
     const uint32_t nsel = min((uint32_t)K, cnt[5] + cnt[6]);
-    uint32_t xs[K], as[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        xs[j] = (uint32_t)j < nsel ? selx[j] : 0u;
-        as[j] = (uint32_t)j < nsel ? sela[j] : kLat32Inf;
+    for (uint32_t j = nsel + tid; j < (uint32_t)K; j += BLOCK) {   // unused slots: no detour
+        selx[j] = 0u;
+        sela[j] = kLat32Inf;
     }
     if (tid == 0) cnt[0] = 0;
     __syncthreads();
     const size_t base = (size_t)u * V;
+    constexpr int KC = K < 32 ? K : 32;   // detours per batch of loads in flight
     for (uint32_t v = tid; v < V; v += BLOCK) {  // 2-hop test of every arc of u
         const uint32_t w = row[v];
         if (w == kLat32Inf) continue;
         uint32_t z = kLat32Inf;
-        uint32_t bv[K];
+        for (int j0 = 0; j0 < K && w <= z; j0 += KC) {   // stop once a strict detour is found
+            uint32_t bv[KC], as[KC];
 #pragma unroll
-        for (int j = 0; j < K; ++j)   // all K detour loads in flight together
-            bv[j] = as[j] != kLat32Inf ? Wl[(size_t)xs[j] * V + v] : kLat32Inf;
+            for (int j = 0; j < KC; ++j) {   // the batch's detour loads in flight together
+                as[j] = sela[j0 + j];
+                bv[j] = as[j] != kLat32Inf ? Wl[(size_t)selx[j0 + j] * V + v] : kLat32Inf;
+            }
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const uint32_t t = as[j] + bv[j];
-            if (as[j] != kLat32Inf && bv[j] != kLat32Inf && t >= as[j]) z = min(z, t);
+            for (int j = 0; j < KC; ++j) {
+                const uint32_t t = as[j] + bv[j];
+                if (as[j] != kLat32Inf && bv[j] != kLat32Inf && t >= as[j]) z = min(z, t);
+            }
         }
         if (w <= z) {
             const uint32_t slot = atomicAdd(&cnt[0], 1u);
@@ -1093,8 +1096,16 @@ static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
     dense_scatter<<<V, 256, 0, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
                                     ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wk);
     dense_lat<<<div_up(nn, 256), 256, 0, s>>>(Wk, Wl, nn);
-    prune_rows<256, kPruneK><<<V, 256, (size_t)V * 18 + (8 + 256 + 2 * kPruneK) * 4, s>>>(
-        Wl, Wk, V, Pw, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor);
+    const char* pk = std::getenv("SHD_PRUNE_K");   // tuning: detour nodes per row (same output tables)
+    const uint32_t Kr = pk && *pk ? (uint32_t)std::atoi(pk) : kPruneK;
+    const uint32_t K = Kr >= 128 ? 128u : Kr >= 64 ? 64u : 32u;
+    const size_t plds = (size_t)V * 18 + (8 + 256 + 2 * (size_t)K) * 4;
+    if (K >= 128)
+        prune_rows<256, 128><<<V, 256, plds, s>>>(Wl, Wk, V, Pw, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor);
+    else if (K >= 64)
+        prune_rows<256, 64><<<V, 256, plds, s>>>(Wl, Wk, V, Pw, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor);
+    else
+        prune_rows<256, 32><<<V, 256, plds, s>>>(Wl, Wk, V, Pw, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor);
     SHD_HIP(hipGetLastError());
     *out = ArcView{pbeg, pend, ctx->g_prune_dst.as<uint4>(), 0};
     return SHD_OK;
