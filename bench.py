@@ -103,16 +103,22 @@ def prepare(eng, el):
     return n
 
 
-def sharded_build(eng, world, rank, n, algo, steps, warmup, keep=False):
-    """Rows [rb, re) of an n x n build on this rank + all-gather; returns timings."""
+def sharded_build(eng, world, rank, n, algo, steps, warmup, keep=False, gather=True):
+    """Rows [rb, re) of an n x n build on this rank + all-gather (gather=False: the row shards
+    stay resident, SURVEY 8(e) "keep shards and gather on demand"); returns timings."""
     import torch
     from shadow_amd import _native as N
     per = (n + world - 1) // world
     rb, re = min(rank * per, n), min((rank + 1) * per, n)
-    full_lat = torch.empty((world * per, n), dtype=torch.int64, device="cuda")
-    full_loss = torch.empty((world * per, n), dtype=torch.float32, device="cuda")
-    shard_lat = full_lat[rank * per:(rank + 1) * per]
-    shard_loss = full_loss[rank * per:(rank + 1) * per]
+    rows = world * per if gather else per
+    full_lat = torch.empty((rows, n), dtype=torch.int64, device="cuda")
+    full_loss = torch.empty((rows, n), dtype=torch.float32, device="cuda")
+    if not gather:
+        rank_off = 0
+    else:
+        rank_off = rank * per
+    shard_lat = full_lat[rank_off:rank_off + per]
+    shard_loss = full_loss[rank_off:rank_off + per]
     err = N.Error()
 
     def step():
@@ -120,7 +126,7 @@ def sharded_build(eng, world, rank, n, algo, steps, warmup, keep=False):
             st = eng.lib.shd_routing_run(eng.ctx, algo, rb, re, N.ptr(shard_lat), N.ptr(shard_loss),
                                          C.byref(err))
             N.check(st, "shd_routing_run", err)
-        if world > 1:
+        if world > 1 and gather:
             import torch.distributed as dist
             dist.all_gather_into_tensor(full_lat, shard_lat)
             dist.all_gather_into_tensor(full_loss, shard_loss)
@@ -195,18 +201,24 @@ def c3_leg(eng, reps=2):
                 algorithms=res)
 
 
-def c4_leg(eng, world, rank, steps):
+def c4_leg(eng, world, rank, steps, gather=False):
+    """C4: the 50k-node table is 30 GB (12 B/pair).  At N > 1 the row shards stay resident by
+    default: an all-gather would move 26 GB into every GPU (minutes over xGMI) per build, and the
+    relay needs only its source hosts' rows.  --c4-gather times the full all-gather as well."""
     from shadow_amd import _native as N
     from shadow_amd import synth
     el = synth.barabasi_albert(50_000, 4, 3)
     n = prepare(eng, el)
-    r = sharded_build(eng, world, rank, n, N.ALGO_DELTA, steps, 0 if steps > 1 else 1)
+    gather = gather and world > 1
+    r = sharded_build(eng, world, rank, n, N.ALGO_DELTA, steps, 0 if steps > 1 else 1, gather=gather)
     kernel_ms = max_over_ranks(float(np.mean([i["ms_main"] for i in r["infos"]])), world)
+    how = ("source rows sharded + RCCL all-gather of the table" if gather else
+           "source rows sharded, shards resident (no all-gather)" if world > 1 else "1 GPU, whole table")
     return dict(workload="C4: 50k-node Barabasi-Albert m=4 + self-loops, all 50k rows, global-label "
-                         "delta-stepping SSSP, source rows sharded + RCCL all-gather of the table",
+                         "delta-stepping SSSP, " + how,
                 nodes=n, arcs=int(r["infos"][-1]["arcs"]), steps=steps, ms_per_build=r["ms_per_step"],
                 sssp_kernel_ms_per_rank=kernel_ms, value=n * n / (r["ms_per_step"] * 1e-3),
-                unit="node-pairs/s", scaling="strong")
+                unit="node-pairs/s", scaling="strong", all_gather=bool(gather))
 
 
 def relay_inputs():
@@ -444,6 +456,7 @@ def main():
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--no-codel", action="store_true")
     ap.add_argument("--no-tbucket", action="store_true")
+    ap.add_argument("--c4-gather", action="store_true")
     args = ap.parse_args()
     world, rank, local = dist_setup(args.gpus)
     from shadow_amd.routing import Engine
@@ -502,7 +515,7 @@ def main():
     if world == 1 and not args.no_c3:
         res["c3"] = c3_leg(eng)
     if not args.no_c4:
-        res["c4"] = c4_leg(eng, world, rank, args.c4_steps)
+        res["c4"] = c4_leg(eng, world, rank, args.c4_steps, gather=args.c4_gather)
     if world == 1 and not args.no_codel:
         res["codel"] = codel_leg(eng, cpu=not args.no_cpu_baseline)
     if world == 1 and not args.no_tbucket:
