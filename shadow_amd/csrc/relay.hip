@@ -618,6 +618,11 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     __shared__ uint32_t s_rowof[kS5Hosts], s_rownode[kS5Hosts], s_run[kS5Hosts], s_base[kS5Hosts];
     __shared__ uint32_t s_wsum[kS6Threads / 64], s_nrows;
     __shared__ uint8_t s_own[kS6Cap];   // chunk position -> host slot in the group
+    __shared__ uint32_t s_pfnode[kS5RowLds / kS6Threads], s_pfn;   // next group's path rows
+    static_assert(kS5RowLds % kS6Threads == 0, "row prefetch: whole entries per thread");
+    constexpr uint32_t kPf = kS5RowLds / kS6Threads;
+    uint2 pf[kPf];             // the next group's staged path rows, prefetched during this group
+    bool have_pf = false;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
 #ifdef SHD_STAMP_PROF
     uint64_t sp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, sp_t = __builtin_amdgcn_s_memtime();
@@ -696,11 +701,18 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
         const bool staged = (uint64_t)s_nrows * a.n_nodes <= kS5RowLds;
         if (staged) {
             const uint32_t tot = s_nrows * a.n_nodes;
-            for (uint32_t e = tid; e < tot; e += kS6Threads) {
-                const uint32_t rr = e / a.n_nodes, c = e - rr * a.n_nodes;
-                s_rows[e] = a.path[(size_t)s_rownode[rr] * a.n_nodes + c];
+            if (have_pf) {   // rows loaded during the previous group (same node list by construction)
+#pragma unroll
+                for (uint32_t j = 0; j < kPf; ++j)
+                    if (tid + j * kS6Threads < tot) s_rows[tid + j * kS6Threads] = pf[j];
+            } else {
+                for (uint32_t e = tid; e < tot; e += kS6Threads) {
+                    const uint32_t rr = e / a.n_nodes, c = e - rr * a.n_nodes;
+                    s_rows[e] = a.path[(size_t)s_rownode[rr] * a.n_nodes + c];
+                }
             }
         }
+        have_pf = false;
         fill_owner(0, nh);
         if (tid < 64) fetch_hosts(nxt);
         __syncthreads();
@@ -708,6 +720,17 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
         const uint32_t T = s_pre[nh];
         for (uint32_t c0 = 0; c0 < T; c0 += kS6Cap) {
             const uint32_t cn = min(kS6Cap, T - c0);
+            if (c0 == 0 && tid < 64) {   // the next group's distinct source nodes, as at its start
+                const uint32_t nh2 = nxt < n_groups ? min(kS5Hosts, a.n_hosts - nxt * kS5Hosts) : 0u;
+                const uint32_t nd = p_nd, prev = __shfl_up(nd, 1);
+                const bool first = tid < nh2 && (tid == 0 || nd != prev);
+                const uint64_t fm = __ballot(first);
+                if (first) {
+                    const uint32_t ri = (uint32_t)__popcll(fm & ((2ull << tid) - 1ull)) - 1u;
+                    if (ri < kPf) s_pfnode[ri] = nd;
+                }
+                if (tid == 0) s_pfn = (uint32_t)__popcll(fm);
+            }
             // (a) positions -> packet indices through the owner map (positions past the chunk end
             // are clamped onto its last packet so every load below is in bounds and unconditional)
             uint32_t idx[kS6Per], hl[kS6Per], kk[kS6Per];
@@ -772,6 +795,20 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
             SP_MARK(10);
             __syncthreads();
             SP_MARK(3);
+            if (c0 == 0) {   // prefetch the next group's rows; they land while this group runs
+                const uint32_t pn = s_pfn;
+                if (pn && (uint64_t)pn * a.n_nodes <= kS5RowLds) {
+#pragma unroll
+                    for (uint32_t j = 0; j < kPf; ++j) {
+                        const uint32_t e = tid + j * kS6Threads;
+                        if (e < pn * a.n_nodes) {
+                            const uint32_t rr = e / a.n_nodes, c = e - rr * a.n_nodes;
+                            pf[j] = path_global(a.path, (size_t)s_pfnode[rr] * a.n_nodes + c);
+                        }
+                    }
+                    have_pf = true;
+                }
+            }
             {   // block-wide exclusive scan of the sent flags (kS6Per consecutive entries per thread)
                 uint32_t v[kS6Per], sum = 0;
 #pragma unroll
