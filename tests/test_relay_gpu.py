@@ -270,3 +270,47 @@ def test_sim_end_inside_round_and_wide_event_ids(engine):
         rl.round(b.src_off, t, b.dst_host, b.payload, 10**9 + 10**6, sim_end, 0)
     st2, nid2 = rl.host_state()
     assert np.array_equal(st, st2) and np.array_equal(nid, nid2)
+
+
+def test_bin_pipeline_failed_round_keeps_state(engine):
+    """Pipeline 7: a round naming an unknown host fails with NO_HOST (the stamp skips placing
+    that packet, the histogram skips counting it) and leaves RNG streams and event ids
+    untouched; the next valid round runs on pipeline 7 bit-exact."""
+    from shadow_amd.relay import Relay
+    from shadow_amd._native import ShdError
+    H, NN = 2000, 40
+    lat, loss, host_node, rng0, b = _c5_like(H, NN, 100_000, 21)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    bad = b.dst_host.copy()
+    bad[::997] = H + 3
+    with pytest.raises(ShdError, match="NO_HOST"):
+        rl.round(b.src_off, b.send_time, bad, b.payload, 10**9 + 10**6, 10**12, 0)
+    st, nid = rl.host_state()
+    assert np.array_equal(st, rng0) and (nid == 0).all()
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss,
+                         rng0.copy(), np.zeros(H, np.uint64), 10**9 + 10**6, 10**12, 0)
+    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, 10**9 + 10**6, 10**12, 0)
+    assert rl.last_pipeline() == 7
+    assert np.array_equal(r.status, o["status"]) and np.array_equal(r.ev_off, o["events"]["off"])
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(r, "ev_" + k), o["events"][k]), k
+
+
+def test_bin_pipeline_slot_counter_overflow_falls_back(engine):
+    """64 hosts = one stamp workgroup, 5,000 sends into two bins: every bin fits pipeline 7's
+    LDS stage but the workgroup's 8-bit slot counters would overflow, so the round reruns on
+    the radix pipeline, bit-exact."""
+    from shadow_amd.relay import Relay
+    H, NN = 64, 8
+    lat, loss, host_node, rng0, b = _c5_like(H, NN, 5_000, 23)
+    orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss,
+                         orng, onid, 10**9 + 10**6, 10**12, 0)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, 10**9 + 10**6, 10**12, 0)
+    assert rl.last_pipeline() == 3
+    assert np.array_equal(r.status, o["status"]) and np.array_equal(r.ev_off, o["events"]["off"])
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(r, "ev_" + k), o["events"][k]), k
+    st, nid = rl.host_state()
+    assert np.array_equal(st, orng) and np.array_equal(nid, onid)
