@@ -75,13 +75,19 @@ __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* la
             cand[i] = ok ? pack_key(cl, fold_q(qu, __uint_as_float(a[i].z))) : kKeyInf;
             tgt[i] = ok ? a[i].x : scratch;
         }
+        // global labels: they only decrease, so a candidate not below the label read now cannot
+        // improve it; the read filters the device-scope atomics (few relaxations improve a label)
         if constexpr (GLAB) {   // global labels: no scratch slots, skip dead slots instead
+            uint64_t cur[R];
+#pragma unroll
+            for (int i = 0; i < R; ++i) cur[i] = cand[i] != kKeyInf ? ld_lab<GLAB>(&lab[a[i].x]) : 0ull;
 #pragma unroll
             for (int i = 0; i < R; ++i)
-                old[i] = cand[i] != kKeyInf
+                old[i] = cand[i] < cur[i]
                              ? atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[i].x]), (unsigned long long)cand[i])
-                             : 0ull;
-        } else {
+                             : cur[i];
+        } else {   // LDS labels: unconditional atomics, one LDS round trip for the R arcs (a
+                   // filtering read first measured slower: C2 172 -> 205 us, C3 11.2 -> 13.5 ms)
 #pragma unroll
             for (int i = 0; i < R; ++i)
                 old[i] = atomicMin(reinterpret_cast<unsigned long long*>(&lab[tgt[i]]), (unsigned long long)cand[i]);
