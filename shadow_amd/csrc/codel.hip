@@ -27,6 +27,7 @@ constexpr uint64_t kInterval = 100000000ull;
 constexpr uint64_t kMtu = 1500;
 constexpr uint32_t kPop = 0xFFFFFFFFu;
 constexpr uint32_t kHasIntervalEnd = 1u, kHasDropNext = 2u, kModeDrop = 4u;
+constexpr uint32_t kOpBatch = 16;   // ops per lane loaded ahead of the state machine
 
 struct CodelHost {   // 48 bytes per host
     uint64_t interval_end, drop_next, cur, prev, total;
@@ -144,24 +145,41 @@ __global__ __launch_bounds__(256) void codel_run(uint32_t n_hosts, const uint32_
     L.fate = fate;
     L.n_ids = n_ids;
     L.status = status;
-    for (uint32_t k = off[h]; k < off[h + 1]; ++k) {
-        const uint64_t now = time[k];
-        const uint32_t sz = size[k];
-        if (sz == kPop) {
-            const uint32_t got = L.pop(now, k);
-            pop_out[k] = got;
-            if (got != kPop) L.mark(got, k, 1);
-        } else {
-            pop_out[k] = kPop;
-            if (L.s.count == cap) {   // the reference's queue never fills (LIMIT = usize::MAX)
-                atomicOr(status, 1u);
-                continue;
+    // The host's ops are read kOpBatch at a time into registers (loads clamped into the range,
+    // all issued before the state machine runs), so a lane waits for one memory latency per
+    // batch instead of one per op, and its consecutive 8-byte times share cache lines.
+    const uint32_t kb = off[h], ke = off[h + 1];
+    for (uint32_t k0 = kb; k0 < ke; k0 += kOpBatch) {
+        uint64_t tm[kOpBatch];
+        uint32_t sz[kOpBatch], pk[kOpBatch];
+#pragma unroll
+        for (uint32_t i = 0; i < kOpBatch; ++i) {
+            const uint32_t k = min(k0 + i, ke - 1);
+            tm[i] = time[k];
+            sz[i] = size[k];
+            pk[i] = pkt[k];
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kOpBatch; ++i) {
+            const uint32_t k = k0 + i;
+            if (k >= ke) break;
+            const uint64_t now = tm[i];
+            if (sz[i] == kPop) {
+                const uint32_t got = L.pop(now, k);
+                pop_out[k] = got;
+                if (got != kPop) L.mark(got, k, 1);
+            } else {
+                pop_out[k] = kPop;
+                if (L.s.count == cap) {   // the reference's queue never fills (LIMIT = usize::MAX)
+                    atomicOr(status, 1u);
+                    continue;
+                }
+                uint32_t tail = L.s.head + L.s.count;
+                if (tail >= cap) tail -= cap;
+                L.ring_w[tail] = make_uint4(pk[i], sz[i], (uint32_t)now, (uint32_t)(now >> 32));
+                ++L.s.count;
+                L.s.total += sz[i];
             }
-            uint32_t tail = L.s.head + L.s.count;
-            if (tail >= cap) tail -= cap;
-            L.ring_w[tail] = make_uint4(pkt[k], sz, (uint32_t)now, (uint32_t)(now >> 32));
-            ++L.s.count;
-            L.s.total += sz;
         }
     }
     st[h] = L.s;

@@ -55,6 +55,8 @@ __device__ __forceinline__ uint64_t emutime_sat_add(uint64_t t, uint64_t d) {
     return (s < t || s > kEmutimeMax) ? kEmutimeMax : s;
 }
 
+constexpr uint32_t kAttBatch = 8;   // attempts per lane loaded ahead of the state machine
+
 __global__ __launch_bounds__(256) void tb_run(uint32_t n_relays, const uint32_t* __restrict__ off,
                                               const uint64_t* __restrict__ time, const uint32_t* __restrict__ size,
                                               const uint8_t* __restrict__ flags, TbRelay* __restrict__ st,
@@ -64,49 +66,66 @@ __global__ __launch_bounds__(256) void tb_run(uint32_t n_relays, const uint32_t*
     if (r >= n_relays) return;
     TbRelay s = st[r];
     bool bad = false;
-    const uint32_t e = off[r + 1];
-    for (uint32_t k = off[r]; k < e; ++k) {
-        const uint64_t now = time[k];
-        uint8_t stt = kTbForwarded;
-        uint64_t v;
-        if (now < s.pending) {             // Pending: no forwarding before the scheduled task
-            stt = kTbSkipped;
-            v = s.pending;
-        } else if (s.capacity == 0) {      // RateLimit::Unlimited
-            v = ~0ull;
-        } else if (flags[k] & kTbExempt) { // local or bootstrapping: no tokens taken
-            v = s.balance;
-        } else {
-            // lazy_refill (token_bucket.rs:127-157)
-            const bool before = now < s.last_refill;   // duration_since(..).unwrap() panics
-            bad |= before;
-            uint64_t span = before ? 0ull : now - s.last_refill;
-            if (span >= s.interval) {
-                const uint64_t n = span / s.interval;
-                const uint64_t tok = __umul64hi(s.increment, n) ? ~0ull : s.increment * n;
-                const uint64_t sum = s.balance + tok < s.balance ? ~0ull : s.balance + tok;
-                s.balance = sum < s.capacity ? sum : s.capacity;
-                s.last_refill = emutime_sat_add(s.last_refill, simtime_sat_mul(s.interval, n, bad));
-                bad |= now < s.last_refill;
-                span = now < s.last_refill ? 0ull : now - s.last_refill;
-            }
-            const uint64_t next_span = s.interval - span;
-            const uint64_t dec = size[k];
-            if (s.balance >= dec) {
-                s.balance -= dec;
-                v = s.balance;
-            } else {   // compute_conforming_duration (token_bucket.rs:94-120)
-                const uint64_t req = dec - s.balance;
-                const uint64_t nr = req / s.increment + (req % s.increment ? 1u : 0u);
-                v = nr == 0 ? 0ull
-                  : nr == 1 ? next_span
-                            : simtime_sat_add(next_span, simtime_sat_mul(s.interval, nr - 1, bad), bad);
-                stt = kTbBlocked;
-                s.pending = emutime_sat_add(now, v);
-            }
+    const uint32_t b = off[r], e = off[r + 1];
+    // attempts are read kAttBatch at a time into registers (loads clamped into the range, all
+    // issued before the state machine runs): one memory latency per batch instead of per attempt
+    for (uint32_t k0 = b; k0 < e; k0 += kAttBatch) {
+        uint64_t tm[kAttBatch];
+        uint32_t sz[kAttBatch];
+        uint8_t fl[kAttBatch];
+#pragma unroll
+        for (uint32_t i = 0; i < kAttBatch; ++i) {
+            const uint32_t k = min(k0 + i, e - 1);
+            tm[i] = time[k];
+            sz[i] = size[k];
+            fl[i] = flags[k];
         }
-        status[k] = stt;
-        value[k] = v;
+#pragma unroll
+        for (uint32_t i = 0; i < kAttBatch; ++i) {
+            const uint32_t k = k0 + i;
+            if (k >= e) break;
+            const uint64_t now = tm[i];
+            uint8_t stt = kTbForwarded;
+            uint64_t v;
+            if (now < s.pending) {             // Pending: no forwarding before the scheduled task
+                stt = kTbSkipped;
+                v = s.pending;
+            } else if (s.capacity == 0) {      // RateLimit::Unlimited
+                v = ~0ull;
+            } else if (fl[i] & kTbExempt) { // local or bootstrapping: no tokens taken
+                v = s.balance;
+            } else {
+                // lazy_refill (token_bucket.rs:127-157)
+                const bool before = now < s.last_refill;   // duration_since(..).unwrap() panics
+                bad |= before;
+                uint64_t span = before ? 0ull : now - s.last_refill;
+                if (span >= s.interval) {
+                    const uint64_t n = span / s.interval;
+                    const uint64_t tok = __umul64hi(s.increment, n) ? ~0ull : s.increment * n;
+                    const uint64_t sum = s.balance + tok < s.balance ? ~0ull : s.balance + tok;
+                    s.balance = sum < s.capacity ? sum : s.capacity;
+                    s.last_refill = emutime_sat_add(s.last_refill, simtime_sat_mul(s.interval, n, bad));
+                    bad |= now < s.last_refill;
+                    span = now < s.last_refill ? 0ull : now - s.last_refill;
+                }
+                const uint64_t next_span = s.interval - span;
+                const uint64_t dec = sz[i];
+                if (s.balance >= dec) {
+                    s.balance -= dec;
+                    v = s.balance;
+                } else {   // compute_conforming_duration (token_bucket.rs:94-120)
+                    const uint64_t req = dec - s.balance;
+                    const uint64_t nr = req / s.increment + (req % s.increment ? 1u : 0u);
+                    v = nr == 0 ? 0ull
+                      : nr == 1 ? next_span
+                                : simtime_sat_add(next_span, simtime_sat_mul(s.interval, nr - 1, bad), bad);
+                    stt = kTbBlocked;
+                    s.pending = emutime_sat_add(now, v);
+                }
+            }
+            status[k] = stt;
+            value[k] = v;
+        }
     }
     st[r] = s;
     if (bad) atomicOr(err, 1u);
