@@ -18,7 +18,7 @@
 //
 // Layout: D is Vp x Vp u32 row-major (Vp = V rounded up to the tile T), INF = 2^32-1, D[i][i] = 0.
 // One round per diagonal block r (Vp / T rounds), three launches each:
-//   fw_diag    1 workgroup      closes the T x T diagonal block (T sequential steps in LDS)
+//   fw_diag    1 workgroup      closes the T x T diagonal block (T sequential steps, registers)
 //   fw_panels  2 (nb-1) WGs     row panel D[r][j] = Drr* (x) D[r][j]; column panel D[i][r] = D[i][r] (x) Drr*
 //   fw_rest    (nb-1)^2 WGs     D[i][j] = min(D[i][j], D[i][r] (x) D[r][j])
 // (x) is the min-plus product of two T x T tiles, k streamed through LDS in chunks of KC; each
@@ -48,43 +48,60 @@ __global__ __launch_bounds__(256) void fw_scatter(const uint32_t* __restrict__ o
         atomicMin(&D[(size_t)u * Vp + adst[k]], alat[k]);
 }
 
-// Phase 1: close the diagonal block r in LDS.  Thread (i0, j) holds rows i0, i0+RS, ... of
-// column j in registers; after step k only column k+1 and row k+1 are published to LDS (the
-// only entries step k+1 reads; neither changes during its own step since D[k][k] = 0).
-template <int T>
-__global__ __launch_bounds__(256) void fw_diag(uint32_t* __restrict__ D, uint32_t Vp, uint32_t r) {
-    constexpr int RS = 256 / T;          // row step between a thread's entries
-    constexpr int E = T / RS;            // entries per thread
-    __shared__ uint32_t s[T][T + 1];
-    const uint32_t tid = threadIdx.x, j = tid % T, i0 = tid / T;
+// Phase 1: close the diagonal block r.  NTH threads; thread (q, j) holds column j of the E =
+// T / (NTH / T) consecutive rows q*E .. q*E+E-1 in registers.  Step k needs only column k and
+// row k of the block (neither changes during step k, since D[k][k] = 0), so after each step the
+// owners publish column k+1 and row k+1 to a second LDS buffer (double-buffered: one barrier per
+// step).  A wave shares q, so its column reads are 16-byte broadcasts and its row reads are
+// consecutive words.
+template <int T, int NTH>
+__global__ __launch_bounds__(NTH) void fw_diag(uint32_t* __restrict__ D, uint32_t Vp, uint32_t r) {
+    constexpr int QN = NTH / T, E = T / QN;
+    static_assert(T >= 64 && E % 4 == 0, "a wave must share its row group");
+    __shared__ __attribute__((aligned(16))) uint32_t col[2][T];   // D[i][k] of the block
+    __shared__ uint32_t rowv[2][T];                                // D[k][j] of the block
+    const uint32_t tid = threadIdx.x, j = tid % T, q = tid / T;
     uint32_t* base = D + (size_t)r * T * Vp + (size_t)r * T;
     uint32_t v[E];
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        v[m] = base[(size_t)(i0 + m * RS) * Vp + j];
-        s[i0 + m * RS][j] = v[m];
+    for (int m = 0; m < E; ++m) v[m] = base[(size_t)(q * E + m) * Vp + j];
+    if (j == 0) {
+#pragma unroll
+        for (int m = 0; m < E; ++m) col[0][q * E + m] = v[m];
     }
+    if (q == 0) rowv[0][j] = v[0];
     __syncthreads();
     for (int k = 0; k < T; ++k) {
-        const uint32_t bkj = s[k][j];
+        const int bf = k & 1;
+        const uint32_t bkj = rowv[bf][j];
 #pragma unroll
-        for (int m = 0; m < E; ++m) v[m] = min(v[m], sat_add(s[i0 + m * RS][k], bkj));
+        for (int g = 0; g < E / 4; ++g) {
+            const uint4 c = *reinterpret_cast<const uint4*>(&col[bf][q * E + 4 * g]);
+            v[4 * g + 0] = min(v[4 * g + 0], sat_add(c.x, bkj));
+            v[4 * g + 1] = min(v[4 * g + 1], sat_add(c.y, bkj));
+            v[4 * g + 2] = min(v[4 * g + 2], sat_add(c.z, bkj));
+            v[4 * g + 3] = min(v[4 * g + 3], sat_add(c.w, bkj));
+        }
         const int kn = k + 1;
         if (kn < T) {
             if ((int)j == kn) {
 #pragma unroll
-                for (int m = 0; m < E; ++m) s[i0 + m * RS][j] = v[m];
+                for (int g = 0; g < E / 4; ++g)
+                    *reinterpret_cast<uint4*>(&col[bf ^ 1][q * E + 4 * g]) =
+                        make_uint4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
             }
-            if ((int)i0 == kn % RS) {
+            if ((int)q == kn / E) {
+                uint32_t x = v[0];
 #pragma unroll
-                for (int m = 0; m < E; ++m)
-                    if (m == kn / RS) s[kn][j] = v[m];
+                for (int m = 1; m < E; ++m)
+                    if (m == kn % E) x = v[m];
+                rowv[bf ^ 1][j] = x;
             }
         }
         __syncthreads();
     }
 #pragma unroll
-    for (int m = 0; m < E; ++m) base[(size_t)(i0 + m * RS) * Vp + j] = v[m];
+    for (int m = 0; m < E; ++m) base[(size_t)(q * E + m) * Vp + j] = v[m];
 }
 
 // acc = min(acc, A (x) B) over one T x T output tile; A rows i / cols k and B rows k / cols j are
@@ -257,13 +274,13 @@ shd_status fw_latency(shd_ctx* ctx, uint32_t* D, uint32_t Vp, uint32_t T) {
                                  ctx->g_lat.as<uint32_t>(), Vp, D);
     for (uint32_t r = 0; r < nb; ++r) {
         if (T == 64) {
-            fw_diag<64><<<1, 256, 0, s>>>(D, Vp, r);
+            fw_diag<64, 512><<<1, 512, 0, s>>>(D, Vp, r);
             if (nb > 1) {
                 fw_panels<64, 4><<<2 * (nb - 1), 256, 0, s>>>(D, Vp, r);
                 fw_rest<64, 4><<<(nb - 1) * (nb - 1), 256, 0, s>>>(D, Vp, r);
             }
         } else {
-            fw_diag<128><<<1, 256, 0, s>>>(D, Vp, r);
+            fw_diag<128, 1024><<<1, 1024, 0, s>>>(D, Vp, r);
             if (nb > 1) {
                 fw_panels<128, 8><<<2 * (nb - 1), 256, 0, s>>>(D, Vp, r);
                 fw_rest<128, 8><<<(nb - 1) * (nb - 1), 256, 0, s>>>(D, Vp, r);
