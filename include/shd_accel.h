@@ -154,7 +154,9 @@ shd_status shd_routing_smallest_latency(shd_ctx* ctx, uint64_t* latency_ns);
  * Host tables for the relay: host -> used-node index (IpAssignment + RoutingInfo keys,
  * worker.rs:529-543), the n_nodes x n_nodes table (NULL => the context's resident table from
  * the last full routing build), each host's Xoshiro256++ state (4 x u64, host.rs:218) and next
- * event id (host.rs:580-584).
+ * event id (host.rs:580-584).  A relay set up on the resident table stops at the next
+ * shd_routing_prepare / shd_routing_build / resident shd_routing_run (relay calls return
+ * SHD_ERR_STATE until it is set up again); caller-passed tables are copied and stay valid.
  */
 shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_node,
                            uint32_t n_nodes, const uint64_t* lat, const float* loss,
@@ -225,7 +227,88 @@ shd_status shd_events_merge_device(shd_ctx* ctx, uint32_t n_runs, uint32_t n_dst
                                    const uint64_t* d_seq, const uint32_t* d_pkt,
                                    uint64_t n_events, shd_relay_out* d_out);
 
-/* Read back the per-host RNG states / next event ids (e.g. to hand RNG use back to the CPU). */
+/* ---------------------------------------------------------------- multi-GPU */
+/*
+ * The reference is one process whose manager thread runs every round to a barrier
+ * (core/manager.rs:404-464); it has no multi-GPU path.  The engine shards the two paths along
+ * their natural seams -- routing source rows, relay hosts by id -- over a communicator:
+ *   shd_comm_init        one process per GPU, RCCL over xGMI; rank 0 makes the id with
+ *                        shd_comm_unique_id and the caller hands it to every rank (MPI, a file,
+ *                        torch.distributed ...); collective over the ranks
+ *   shd_comm_init_local  every rank in this process (one host thread per rank must then drive
+ *                        each sharded call concurrently): device copies between the contexts
+ * Shards are contiguous blocks of ceil(total / n_ranks) (shd_shard_range).  Initialising or
+ * destroying a communicator requires shd_relay_setup again.
+ */
+#define SHD_COMM_ID_BYTES 128
+shd_status shd_comm_unique_id(uint8_t* id /* SHD_COMM_ID_BYTES */);
+shd_status shd_comm_init(shd_ctx* ctx, int32_t n_ranks, int32_t rank, const uint8_t* id);
+shd_status shd_comm_init_local(shd_ctx** ctxs, int32_t n_ranks);
+shd_status shd_comm_info(const shd_ctx* ctx, int32_t* n_ranks, int32_t* rank);
+shd_status shd_comm_destroy(shd_ctx* ctx);
+shd_status shd_shard_range(uint32_t total, int32_t n_ranks, int32_t rank, uint32_t* lo, uint32_t* hi);
+
+/*
+ * Routing build over the communicator (after shd_routing_prepare of the same graph on every
+ * rank): each rank builds its source rows into its slice of the full table, then one
+ * all-gather leaves the whole table on every rank.  d_lat_full / d_loss_full are device buffers
+ * of n_ranks * ceil(n_used / n_ranks) rows of n_used (rows >= n_used are padding).  Every rank
+ * returns the same status: the lowest failing rank's error.  Replaces the rayon fan-out of
+ * compute_shortest_paths (graph/mod.rs:192-210) across GPUs.
+ */
+shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_full,
+                                   float* d_loss_full, shd_error* err);
+
+/*
+ * One relay round over the communicator.  shd_relay_setup (after the communicator, same
+ * arguments on every rank) makes this rank own hosts [lo, hi) = shd_shard_range(n_hosts):
+ * their RNG streams, event ids and destination events.  d_batch holds the sends of the own
+ * hosts only (src_off has hi - lo + 1 entries; host lo + k's sends are [src_off[k],
+ * src_off[k+1])); d_out->status (device, n_packets) receives their statuses.  The round's
+ * events for the own destinations come back in engine-owned device arrays, valid until the next
+ * round: d_out->ev_off[hi - lo + 1] and ev_deliver / ev_src / ev_seq / ev_pkt (ev_pkt = the
+ * packet's index in its sender rank's batch; the sender rank owns ev_src).  min_deliver,
+ * min_latency and n_sent are reduced over all ranks.  A round that fails on any rank fails on
+ * every rank with that rank's status and commits no host state anywhere.
+ */
+shd_status shd_relay_round_sharded(shd_ctx* ctx, const shd_batch* d_batch, const shd_round* round,
+                                   shd_relay_out* d_out);
+
+/* ---------------------------------------------------------------- destination event queues */
+/*
+ * Device-resident packet-event queues of this context's destination hosts:
+ * WorkerShared::push_packet_to_host / EventQueue::push (worker.rs:619-629,
+ * event_queue.rs:28-48) and the pop loop of Host::execute (host.rs:697-706) for packet events.
+ * shd_equeue_advance merges a round's events (a relay output on the device, NULL for none) into
+ * the pending queues and pops, per host, every event with deliver < window_end in EventQueue
+ * order (time, src host, src event id; event.rs:84-155); later events stay pending for later
+ * rounds.  The popped events are in engine-owned device arrays valid until the next advance.
+ * tag = (number of the batch that carried the event << 32) | its ev_pkt in that batch.
+ */
+typedef struct shd_equeue_out {
+    const uint32_t* off;        /* device [n_hosts + 1]: host h's events are [off[h], off[h+1]) */
+    const uint64_t* deliver;    /* device [n_popped] */
+    const uint32_t* src;
+    const uint64_t* seq;
+    const uint64_t* tag;
+    uint64_t n_popped;
+    uint64_t n_pending;         /* events left in the queues */
+    uint64_t next_time;         /* earliest pending deliver time (EventQueue::next_event_time
+                                   minimum over the hosts); UINT64_MAX when none is left */
+} shd_equeue_out;
+
+shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_hosts);
+shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64_t window_end,
+                              shd_equeue_out* out);
+/* Host copies of the last advance's popped events (any pointer may be NULL). */
+shd_status shd_equeue_copy_popped(shd_ctx* ctx, uint32_t* off, uint64_t* deliver, uint32_t* src,
+                                  uint64_t* seq, uint64_t* tag);
+/* Host copy of the pending queues (same layout; any pointer may be NULL). */
+shd_status shd_equeue_pending(shd_ctx* ctx, uint32_t* off, uint64_t* deliver, uint32_t* src,
+                              uint64_t* seq, uint64_t* tag, uint64_t* n_pending);
+
+/* Read back the per-host RNG states / next event ids (e.g. to hand RNG use back to the CPU).
+ * A sharded context's own hosts carry their current state, the others their setup state. */
 shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t* next_event_id);
 
 /* Per-path packet counters (RoutingInfo::increment_packet_count, graph/mod.rs:451-458): on by
@@ -267,7 +350,8 @@ shd_status shd_codel_setup(shd_ctx* ctx, uint32_t n_hosts, uint32_t capacity);
 /* Run a batch.  pop_out[k] = packet id a pop returned (SHD_CODEL_POP for none or for a push);
  * fate[id] = (op index << 2) | 1 (dequeued) or | 2 (dropped) for every packet this batch
  * dequeued or dropped (other entries untouched).  SHD_ERR_INVALID: a queue exceeded its
- * capacity or a packet id >= n_ids (the batch ran; the affected pushes/marks were skipped). */
+ * capacity or a packet id >= n_ids (the batch ran with the affected pushes/marks skipped, so the
+ * queues are left undefined: every later call returns SHD_ERR_STATE until shd_codel_setup). */
 shd_status shd_codel_run_device(shd_ctx* ctx, const shd_codel_ops* ops, uint32_t* pop_out,
                                 uint64_t* fate, uint32_t n_ids);
 shd_status shd_codel_get_state(shd_ctx* ctx, uint32_t host, shd_codel_state* out);

@@ -132,17 +132,25 @@ static uint64_t mix64(uint64_t z) {
  * Returns ORC_* ; on error err_a / err_b hold the GML-order node indices involved.
  * lat_out/loss_out: n_used x n_used row-major (used-list order).
  */
-int orc_shortest_paths(uint32_t V, uint32_t E, const uint32_t* es, const uint32_t* ed,
-                       const uint64_t* el, const float* ep, int directed,
-                       const uint32_t* used, uint32_t n_used, int variant, int threads,
-                       uint64_t* lat_out, float* loss_out, uint32_t* err_a, uint32_t* err_b) {
+/*
+ * Rows [rb, re) of the n_used x n_used table (sources used[rb..re)); lat_out/loss_out hold
+ * (re - rb) x n_used.  The self-loop rule is checked over every used node in `nodes` order as
+ * the reference does; unreachable pairs only over the rows built.  This is what checks a few
+ * source rows of a graph whose full table does not fit (C4: 50k x 50k = 30 GB).
+ */
+int orc_shortest_paths_rows(uint32_t V, uint32_t E, const uint32_t* es, const uint32_t* ed,
+                            const uint64_t* el, const float* ep, int directed,
+                            const uint32_t* used, uint32_t n_used, uint32_t rb, uint32_t re,
+                            int variant, int threads, uint64_t* lat_out, float* loss_out,
+                            uint32_t* err_a, uint32_t* err_b) {
     adj_t a;
+    if (rb > re || re > n_used) return ORC_NOMEM;
     if (build_adj(V, E, es, ed, el, ep, directed, &a)) return ORC_NOMEM;
     int32_t* col = (int32_t*)malloc(V * sizeof(int32_t));
     for (uint32_t v = 0; v < V; v++) col[v] = -1;
     for (uint32_t i = 0; i < n_used; i++) col[used[i]] = (int32_t)i;
     const uint64_t UNSET = ~0ULL;
-    size_t nn = (size_t)n_used * n_used;
+    const size_t nn = (size_t)(re - rb) * n_used;
     for (size_t i = 0; i < nn; i++) lat_out[i] = UNSET;
 
     hslot* map = NULL; size_t mcap = 0;
@@ -161,8 +169,9 @@ int orc_shortest_paths(uint32_t V, uint32_t E, const uint32_t* es, const uint32_
         uint32_t* touched = (uint32_t*)malloc(V * sizeof(uint32_t));
         heap_t h = {0, 0, 0};
 #pragma omp for schedule(dynamic, 1)
-        for (uint32_t si = 0; si < n_used; si++) {
+        for (uint32_t si = rb; si < re; si++) {
             uint32_t src = used[si];
+            const size_t orow = (size_t)(si - rb) * n_used;
             for (uint32_t v = 0; v < V; v++) { score_lat[v] = UNSET; visited[v] = 0; }
             uint32_t nt = 0;
             score_lat[src] = 0; score_loss[src] = 0.0f; touched[nt++] = src;
@@ -195,7 +204,7 @@ int orc_shortest_paths(uint32_t V, uint32_t E, const uint32_t* es, const uint32_
                     cj = -1;
                     for (uint32_t q = 0; q < n_used; q++) if (used[q] == v) { cj = (int32_t)q; break; }
                     if (cj < 0) continue;
-                    uint64_t key = ((uint64_t)si << 32) | (uint32_t)cj;
+                    uint64_t key = ((uint64_t)(si - rb) << 32) | (uint32_t)cj;
                     size_t pos = mix64(key) & (mcap - 1);
                     for (;;) {
                         uint64_t cur = __atomic_load_n(&map[pos].key, __ATOMIC_RELAXED);
@@ -210,8 +219,8 @@ int orc_shortest_paths(uint32_t V, uint32_t E, const uint32_t* es, const uint32_
                 } else {
                     cj = col[v];
                     if (cj < 0) continue;
-                    lat_out[(size_t)si * n_used + cj] = score_lat[v];
-                    loss_out[(size_t)si * n_used + cj] = score_loss[v];
+                    lat_out[orow + cj] = score_lat[v];
+                    loss_out[orow + cj] = score_loss[v];
                 }
             }
         }
@@ -232,19 +241,28 @@ int orc_shortest_paths(uint32_t V, uint32_t E, const uint32_t* es, const uint32_
         uint64_t l; float p;
         int r = edge_weight(&a, used[i], used[i], &l, &p);
         if (r != ORC_OK) { rc = r; *err_a = used[i]; *err_b = used[i]; break; }
-        lat_out[(size_t)i * n_used + i] = l;
-        loss_out[(size_t)i * n_used + i] = p;
+        if (i < rb || i >= re) continue;
+        lat_out[(size_t)(i - rb) * n_used + i] = l;
+        loss_out[(size_t)(i - rb) * n_used + i] = p;
     }
     if (rc == ORC_OK) {
         for (size_t i = 0; i < nn; i++) {
             if (lat_out[i] == UNSET) {
-                rc = ORC_UNREACHABLE; *err_a = used[i / n_used]; *err_b = used[i % n_used];
+                rc = ORC_UNREACHABLE; *err_a = used[rb + i / n_used]; *err_b = used[i % n_used];
                 break;
             }
         }
     }
     free_adj(&a); free(col);
     return rc;
+}
+
+int orc_shortest_paths(uint32_t V, uint32_t E, const uint32_t* es, const uint32_t* ed,
+                       const uint64_t* el, const float* ep, int directed,
+                       const uint32_t* used, uint32_t n_used, int variant, int threads,
+                       uint64_t* lat_out, float* loss_out, uint32_t* err_a, uint32_t* err_b) {
+    return orc_shortest_paths_rows(V, E, es, ed, el, ep, directed, used, n_used, 0, n_used,
+                                   variant, threads, lat_out, loss_out, err_a, err_b);
 }
 
 /* get_direct_paths (mod.rs:232-254): src-major over nodes, first error wins */

@@ -29,6 +29,10 @@ def lib():
         _lib.orc_shortest_paths.restype = C.c_int
         _lib.orc_shortest_paths.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P,
                                             C.c_uint32, C.c_int, C.c_int, P, P, P, P]
+        _lib.orc_shortest_paths_rows.restype = C.c_int
+        _lib.orc_shortest_paths_rows.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P,
+                                                 C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
+                                                 P, P, P, P]
         _lib.orc_direct_paths.restype = C.c_int
         _lib.orc_direct_paths.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P,
                                           C.c_uint32, P, P, P, P]
@@ -45,18 +49,21 @@ def _p(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
 
 
-def routing(n_nodes, es, ed, el, ep, directed, used, shortest=True, variant=TIDY, threads=0):
-    """Returns (code, lat[n,n] u64, loss[n,n] f32, (err_a, err_b))."""
+def routing(n_nodes, es, ed, el, ep, directed, used, shortest=True, variant=TIDY, threads=0,
+            rows=None):
+    """Returns (code, lat[r,n] u64, loss[r,n] f32, (err_a, err_b)); ``rows = (rb, re)`` builds
+    only source rows [rb, re) of the used-node table (r = re - rb; default: all n rows)."""
     es = np.ascontiguousarray(es, np.uint32); ed = np.ascontiguousarray(ed, np.uint32)
     el = np.ascontiguousarray(el, np.uint64); ep = np.ascontiguousarray(ep, np.float32)
     used = np.ascontiguousarray(used, np.uint32)
     n = len(used)
-    lat = np.zeros((n, n), np.uint64); loss = np.zeros((n, n), np.float32)
+    rb, re = (0, n) if rows is None else (int(rows[0]), int(rows[1]))
+    lat = np.zeros((re - rb, n), np.uint64); loss = np.zeros((re - rb, n), np.float32)
     ea = np.zeros(1, np.uint32); eb = np.zeros(1, np.uint32)
     if shortest:
-        rc = lib().orc_shortest_paths(n_nodes, len(es), _p(es), _p(ed), _p(el), _p(ep),
-                                      int(directed), _p(used), n, variant, threads, _p(lat),
-                                      _p(loss), _p(ea), _p(eb))
+        rc = lib().orc_shortest_paths_rows(n_nodes, len(es), _p(es), _p(ed), _p(el), _p(ep),
+                                           int(directed), _p(used), n, rb, re, variant, threads,
+                                           _p(lat), _p(loss), _p(ea), _p(eb))
     else:
         rc = lib().orc_direct_paths(n_nodes, len(es), _p(es), _p(ed), _p(el), _p(ep),
                                     int(directed), _p(used), n, _p(lat), _p(loss), _p(ea), _p(eb))

@@ -105,3 +105,42 @@ def runahead(min_used_latency, min_possible_latency: int, runahead_config: int) 
     """``Runahead::get`` (runahead.rs:43-56)."""
     r = min_possible_latency if min_used_latency is None else min_used_latency
     return max(r, runahead_config)
+
+
+class EventQueues:
+    """Per-host packet ``EventQueue`` (``src/main/core/work/event_queue.rs:10-49``): a min-heap
+    of ``Reverse(Event)`` ordered by (time, Packet before Local, src host id, src event id)
+    (``event.rs:84-155``; only packet events here), fed by ``push_packet_to_host``
+    (``worker.rs:619-629``) and drained by ``Host::execute``'s pop loop: every event whose time is
+    below the window end, in order (``host.rs:697-706``).  ``pop`` asserts time never goes
+    backwards, as ``EventQueue::pop`` does (``event_queue.rs:36-40``)."""
+
+    def __init__(self, n_hosts: int):
+        import heapq
+        self._hq = heapq
+        self.q = [[] for _ in range(n_hosts)]
+        self.last = [0] * n_hosts
+
+    def push(self, dst: int, deliver: int, src: int, seq: int, tag):
+        self._hq.heappush(self.q[dst], (int(deliver), int(src), int(seq), tag))
+
+    def push_round(self, events: dict, batch_no: int):
+        """A round's events (``RelayResult.events``: dst -> [(deliver, src, seq, pkt)])."""
+        for d, evs in events.items():
+            for t, s, q, p in evs:
+                self.push(d, t, s, q, (batch_no << 32) | int(p))
+
+    def next_event_time(self, h: int):
+        return self.q[h][0][0] if self.q[h] else None
+
+    def pop_until(self, h: int, window_end: int):
+        out = []
+        while self.q[h] and self.q[h][0][0] < window_end:
+            ev = self._hq.heappop(self.q[h])
+            assert ev[0] >= self.last[h], "EventQueue::pop: time moved backwards"
+            self.last[h] = ev[0]
+            out.append(ev)
+        return out
+
+    def pending(self, h: int):
+        return sorted(self.q[h])

@@ -31,7 +31,11 @@ EXPORTED = [
     "shd_gml_parse", "shd_gml_graph", "shd_gml_node_bandwidth", "shd_gml_free",
     "shd_codel_setup", "shd_codel_run_device", "shd_codel_get_state",
     "shd_tb_setup", "shd_tb_run_device", "shd_tb_get_state",
+    "shd_comm_unique_id", "shd_comm_init", "shd_comm_init_local", "shd_comm_info", "shd_comm_destroy",
+    "shd_shard_range", "shd_routing_run_sharded", "shd_relay_round_sharded",
+    "shd_equeue_setup", "shd_equeue_advance", "shd_equeue_copy_popped", "shd_equeue_pending",
 ]
+COMM_ID_BYTES = 128
 
 
 class ShdError(RuntimeError):
@@ -73,6 +77,12 @@ class RelayOut(C.Structure):
     _fields_ = [("status", C.c_void_p), ("ev_off", C.c_void_p), ("ev_deliver", C.c_void_p),
                 ("ev_src", C.c_void_p), ("ev_seq", C.c_void_p), ("ev_pkt", C.c_void_p),
                 ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64)]
+
+
+class EqueueOut(C.Structure):
+    _fields_ = [("off", C.c_void_p), ("deliver", C.c_void_p), ("src", C.c_void_p), ("seq", C.c_void_p),
+                ("tag", C.c_void_p), ("n_popped", C.c_uint64), ("n_pending", C.c_uint64),
+                ("next_time", C.c_uint64)]
 
 
 class CodelOps(C.Structure):
@@ -147,6 +157,18 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_tb_setup": (I32, [P, U32, P, P, P, P]),
         "shd_tb_run_device": (I32, [P, P, P, P]),
         "shd_tb_get_state": (I32, [P, U32, P]),
+        "shd_comm_unique_id": (I32, [P]),
+        "shd_comm_init": (I32, [P, I32, I32, P]),
+        "shd_comm_init_local": (I32, [P, I32]),
+        "shd_comm_info": (I32, [P, P, P]),
+        "shd_comm_destroy": (I32, [P]),
+        "shd_shard_range": (I32, [U32, I32, I32, P, P]),
+        "shd_routing_run_sharded": (I32, [P, U32, P, P, P]),
+        "shd_relay_round_sharded": (I32, [P, P, P, P]),
+        "shd_equeue_setup": (I32, [P, U32]),
+        "shd_equeue_advance": (I32, [P, P, U64, P]),
+        "shd_equeue_copy_popped": (I32, [P, P, P, P, P, P]),
+        "shd_equeue_pending": (I32, [P, P, P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -2,6 +2,7 @@
 // resident-table lookups.  The relay entry points live in relay.hip.
 #include <cstdlib>
 #include <new>
+#include <vector>
 
 #include "ctx.h"
 
@@ -14,6 +15,14 @@ shd_status min_u64_device(shd_ctx* ctx, const uint64_t* d, uint64_t n, uint64_t*
 }  // namespace shd
 
 using namespace shd;
+
+// The resident table is about to be rebuilt or replaced: nothing may keep reading it.  A relay
+// set up on the resident table (shd_relay_setup with NULL tables) must be set up again.
+static void drop_resident_table(shd_ctx* ctx) {
+    ctx->t_rows = 0;
+    ctx->t_full = false;
+    if (ctx->relay.ready && !ctx->relay.own_table) ctx->relay.ready = false;
+}
 
 extern "C" {
 
@@ -136,7 +145,7 @@ shd_status shd_routing_prepare(shd_ctx* ctx, const shd_graph* g, const uint32_t*
                                uint32_t n_used, uint32_t mode, shd_error* err) {
     if (!ctx) return SHD_ERR_INVALID;
     SHD_HIP(hipSetDevice(ctx->device));
-    ctx->t_rows = 0;
+    drop_resident_table(ctx);
     return routing_prepare_impl(ctx, g, used, n_used, mode, err);
 }
 
@@ -151,9 +160,9 @@ shd_status shd_routing_run(shd_ctx* ctx, uint32_t algo, uint32_t row_begin, uint
     if ((d_lat_out == nullptr) != (d_loss_out == nullptr)) return SHD_ERR_INVALID;
     if (!d_lat_out) {  // into the context's resident table
         const size_t cells = (size_t)(re - row_begin) * n;
+        drop_resident_table(ctx);
         SHD_TRY(ctx->t_lat.ensure(cells * 8));
         SHD_TRY(ctx->t_loss.ensure(cells * 4));
-        ctx->t_rows = 0;
         SHD_TRY(routing_run_impl(ctx, algo, row_begin, re, ctx->t_lat.as<uint64_t>(),
                                  ctx->t_loss.as<float>(), err));
         ctx->t_rows = re - row_begin;
@@ -174,9 +183,9 @@ shd_status shd_routing_build(shd_ctx* ctx, const shd_graph* g, const uint32_t* u
     const uint32_t re = row_end ? row_end : n_used;
     if (row_begin >= re || re > n_used) return SHD_ERR_INVALID;
     const size_t cells = (size_t)(re - row_begin) * n_used;
+    drop_resident_table(ctx);
     SHD_TRY(ctx->t_lat.ensure(cells * 8));
     SHD_TRY(ctx->t_loss.ensure(cells * 4));
-    ctx->t_rows = 0;
     SHD_TRY(routing_prepare_impl(ctx, g, used, n_used, mode, err));
     SHD_TRY(routing_run_impl(ctx, algo, row_begin, re, ctx->t_lat.as<uint64_t>(),
                              ctx->t_loss.as<float>(), err));
@@ -189,6 +198,48 @@ shd_status shd_routing_build(shd_ctx* ctx, const shd_graph* g, const uint32_t* u
     if (loss_out)
         SHD_HIP(hipMemcpyAsync(loss_out, ctx->t_loss.p, cells * 4, hipMemcpyDeviceToHost, ctx->stream));
     SHD_HIP(hipStreamSynchronize(ctx->stream));
+    return SHD_OK;
+}
+
+// Rows of this rank's shard into its slice of the full (padded) table, then one all-gather:
+// the source rows are independent, so the only collective is the final gather.
+// Every rank learns every rank's outcome first, so all of them return the same error (the
+// lowest rank's: its rows come first, as the reference's first failing pair would).
+shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_full,
+                                   float* d_loss_full, shd_error* err) {
+    if (!ctx || !d_lat_full || !d_loss_full) return SHD_ERR_INVALID;
+    if (!ctx->comm || !ctx->prep.ready) return SHD_ERR_STATE;
+    SHD_HIP(hipSetDevice(ctx->device));
+    Comm& C = *ctx->comm;
+    const uint32_t n = ctx->prep.n_used;
+    const uint64_t per = ((uint64_t)n + C.size - 1) / C.size;
+    uint32_t rb = 0, re = 0;
+    shard_range(n, C.size, C.rank, &rb, &re);
+    shd_error e{SHD_OK, 0, 0};
+    shd_status st = SHD_OK;
+    if (re > rb)
+        st = routing_run_impl(ctx, algo, rb, re, d_lat_full + (size_t)C.rank * per * n,
+                              d_loss_full + (size_t)C.rank * per * n, &e);
+    hipStream_t s = ctx->stream;
+    SHD_TRY(ctx->comm_scratch.ensure((size_t)(C.size + 1) * 16));
+    uint64_t* w = ctx->comm_scratch.as<uint64_t>();
+    ctx->h_pin[40] = ((uint64_t)(uint32_t)st << 32) | (uint32_t)e.code;
+    ctx->h_pin[41] = ((uint64_t)e.node_a << 32) | e.node_b;
+    SHD_HIP(hipMemcpyAsync(w + 2 * C.size, ctx->h_pin + 40, 16, hipMemcpyHostToDevice, s));
+    SHD_TRY(C.all_gather(w + 2 * C.size, w, 16, s));
+    std::vector<uint64_t> all(2 * (size_t)C.size);
+    SHD_HIP(hipMemcpyAsync(all.data(), w, all.size() * 8, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    for (int r = 0; r < C.size; ++r) {
+        const shd_status sr = (shd_status)(uint32_t)(all[2 * r] >> 32);
+        if (sr == SHD_OK) continue;
+        if (err) *err = shd_error{(int32_t)(uint32_t)all[2 * r], (uint32_t)(all[2 * r + 1] >> 32),
+                                  (uint32_t)all[2 * r + 1]};
+        return sr;
+    }
+    SHD_TRY(C.all_gather(d_lat_full + (size_t)C.rank * per * n, d_lat_full, per * n * 8, s));
+    SHD_TRY(C.all_gather(d_loss_full + (size_t)C.rank * per * n, d_loss_full, per * n * 4, s));
+    SHD_HIP(hipStreamSynchronize(s));
     return SHD_OK;
 }
 

@@ -226,7 +226,14 @@ shd_status shd_codel_run_device(shd_ctx* ctx, const shd_codel_ops* ops, uint32_t
     SHD_HIP(hipMemcpyAsync(ctx->h_pin + 24, C.status.p, 4, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     const uint32_t st = (uint32_t)ctx->h_pin[24];
-    return st ? SHD_ERR_INVALID : SHD_OK;
+    if (st) {
+        // the batch ran with the offending pushes / marks skipped: the queues now hold a state
+        // the reference never reaches (and a ring slot freed by a pop may have been reused), so
+        // they cannot be rolled back -- shd_codel_setup must run again before the next batch
+        C.ready = false;
+        return SHD_ERR_INVALID;
+    }
+    return SHD_OK;
 }
 
 shd_status shd_codel_get_state(shd_ctx* ctx, uint32_t host, shd_codel_state* out) {

@@ -1,0 +1,226 @@
+// Multi-GPU transports (comm.h) and the communicator entry points of the C ABI.
+//
+// The reference has no multi-process or multi-GPU path: its parallelism is worker
+// threads over hosts inside one process, with a barrier per round (core/manager.rs:404-464).
+// The engine shards along the two seams SURVEY §8(e) names -- routing source rows, relay hosts
+// -- and moves the bytes with RCCL over xGMI between one process per GPU, or with device
+// copies between ranks that share this process.
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "ctx.h"
+
+namespace shd {
+
+#define SHD_NCCL(call)                                                                    \
+    do {                                                                                  \
+        ncclResult_t r_ = (call);                                                         \
+        if (r_ != ncclSuccess) {                                                          \
+            std::fprintf(stderr, "shd_accel: %s failed: %s (%s:%d)\n", #call,             \
+                         ncclGetErrorString(r_), __FILE__, __LINE__);                     \
+            return SHD_ERR_HIP;                                                           \
+        }                                                                                 \
+    } while (0)
+
+// ------------------------------------------------------------------------------------ RCCL
+struct RcclComm final : Comm {
+    ncclComm_t comm = nullptr;
+    ~RcclComm() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    shd_status all_to_all_u64(const uint64_t* send, uint64_t* recv, size_t count, hipStream_t s) override {
+        SHD_NCCL(ncclAllToAll(send, recv, count, ncclUint64, comm, s));
+        return SHD_OK;
+    }
+    shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes, void* const* recv,
+                        const size_t* recv_bytes, hipStream_t s) override {
+        for (int k = 0; k < n_parts; ++k) {   // own part: a device copy
+            const size_t i = (size_t)rank * n_parts + k;
+            if (send_bytes[i] != recv_bytes[i]) return SHD_ERR_INVALID;
+            if (send_bytes[i])
+                SHD_HIP(hipMemcpyAsync(recv[i], send[i], send_bytes[i], hipMemcpyDeviceToDevice, s));
+        }
+        SHD_NCCL(ncclGroupStart());
+        for (int r = 0; r < size; ++r) {
+            if (r == rank) continue;
+            for (int k = 0; k < n_parts; ++k) {
+                const size_t i = (size_t)r * n_parts + k;
+                if (send_bytes[i]) SHD_NCCL(ncclSend(send[i], send_bytes[i], ncclUint8, r, comm, s));
+                if (recv_bytes[i]) SHD_NCCL(ncclRecv(recv[i], recv_bytes[i], ncclUint8, r, comm, s));
+            }
+        }
+        SHD_NCCL(ncclGroupEnd());
+        return SHD_OK;
+    }
+    shd_status all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        if (bytes) SHD_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, comm, s));
+        return SHD_OK;
+    }
+};
+
+// ------------------------------------------------------------------------------------ local
+struct LocalGroup {
+    int n = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    std::vector<int> device;
+    std::vector<const void*> ptr;     // published per rank (exchange: n * n * parts pointers)
+    std::vector<size_t> bytes;
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+
+struct LocalComm final : Comm {
+    std::shared_ptr<LocalGroup> g;
+    int device = 0;
+    // every collective: the rank's inputs are complete (stream sync), pointers are published
+    // (barrier), each rank pulls what it receives onto its own stream, syncs, and a second
+    // barrier keeps the senders' buffers alive until every pull has finished
+    shd_status copy(void* dst, const void* src, int src_dev, size_t n, hipStream_t s) {
+        if (!n) return SHD_OK;
+        if (src_dev == device) SHD_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, s));
+        else SHD_HIP(hipMemcpyPeerAsync(dst, device, src, src_dev, n, s));
+        return SHD_OK;
+    }
+    shd_status all_to_all_u64(const uint64_t* send, uint64_t* recv, size_t count, hipStream_t s) override {
+        SHD_HIP(hipStreamSynchronize(s));
+        g->ptr[rank] = send;
+        g->barrier();
+        shd_status st = SHD_OK;
+        for (int q = 0; q < size && st == SHD_OK; ++q)
+            st = copy(recv + (size_t)q * count, static_cast<const uint64_t*>(g->ptr[q]) + (size_t)rank * count,
+                      g->device[q], count * 8, s);
+        const hipError_t e = hipStreamSynchronize(s);
+        g->barrier();
+        return st != SHD_OK ? st : e == hipSuccess ? SHD_OK : SHD_ERR_HIP;
+    }
+    shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes, void* const* recv,
+                        const size_t* recv_bytes, hipStream_t s) override {
+        if (n_parts < 1 || n_parts > 4) return SHD_ERR_INVALID;   // the group's pointer slots
+        SHD_HIP(hipStreamSynchronize(s));
+        const size_t per_rank = (size_t)size * n_parts;
+        for (size_t i = 0; i < per_rank; ++i) {
+            g->ptr[rank * per_rank + i] = send[i];
+            g->bytes[rank * per_rank + i] = send_bytes[i];
+        }
+        g->barrier();
+        shd_status st = SHD_OK;
+        for (int q = 0; q < size && st == SHD_OK; ++q)
+            for (int k = 0; k < n_parts && st == SHD_OK; ++k) {
+                const size_t from = (size_t)q * per_rank + (size_t)rank * n_parts + k;   // q's part k to me
+                const size_t to = (size_t)q * n_parts + k;
+                if (g->bytes[from] != recv_bytes[to]) st = SHD_ERR_INVALID;
+                else st = copy(recv[to], g->ptr[from], g->device[q], recv_bytes[to], s);
+            }
+        const hipError_t e = hipStreamSynchronize(s);
+        g->barrier();
+        return st != SHD_OK ? st : e == hipSuccess ? SHD_OK : SHD_ERR_HIP;
+    }
+    shd_status all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        SHD_HIP(hipStreamSynchronize(s));
+        g->ptr[rank] = send;
+        g->barrier();
+        shd_status st = SHD_OK;
+        for (int q = 0; q < size && st == SHD_OK; ++q) {
+            char* dst = static_cast<char*>(recv) + (size_t)q * bytes;
+            if (dst != g->ptr[q]) st = copy(dst, g->ptr[q], g->device[q], bytes, s);
+        }
+        const hipError_t e = hipStreamSynchronize(s);
+        g->barrier();
+        return st != SHD_OK ? st : e == hipSuccess ? SHD_OK : SHD_ERR_HIP;
+    }
+};
+
+}  // namespace shd
+
+using namespace shd;
+
+extern "C" {
+
+shd_status shd_comm_unique_id(uint8_t* id) {
+    if (!id) return SHD_ERR_INVALID;
+    ncclUniqueId u;
+    SHD_NCCL(ncclGetUniqueId(&u));
+    static_assert(sizeof(u) == SHD_COMM_ID_BYTES, "RCCL unique id size");
+    std::memcpy(id, &u, sizeof(u));
+    return SHD_OK;
+}
+
+shd_status shd_comm_init(shd_ctx* ctx, int32_t n_ranks, int32_t rank, const uint8_t* id) {
+    if (!ctx || !id || n_ranks < 1 || rank < 0 || rank >= n_ranks) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    auto c = std::unique_ptr<RcclComm>(new (std::nothrow) RcclComm());
+    if (!c) return SHD_ERR_NOMEM;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    SHD_NCCL(ncclCommInitRank(&c->comm, n_ranks, u, rank));
+    c->rank = rank;
+    c->size = n_ranks;
+    ctx->comm = std::move(c);
+    ctx->relay.ready = false;   // the relay's source shard follows the communicator: set up again
+    return SHD_OK;
+}
+
+shd_status shd_comm_init_local(shd_ctx** ctxs, int32_t n_ranks) {
+    if (!ctxs || n_ranks < 1) return SHD_ERR_INVALID;
+    for (int r = 0; r < n_ranks; ++r)
+        if (!ctxs[r]) return SHD_ERR_INVALID;
+    auto g = std::make_shared<LocalGroup>();
+    g->n = n_ranks;
+    g->device.resize(n_ranks);
+    const size_t slots = (size_t)n_ranks * n_ranks * 4;   // exchange: up to 4 parts per peer
+    g->ptr.assign(slots, nullptr);
+    g->bytes.assign(slots, 0);
+    for (int r = 0; r < n_ranks; ++r) g->device[r] = ctxs[r]->device;
+    for (int r = 0; r < n_ranks; ++r) {
+        auto c = std::unique_ptr<LocalComm>(new (std::nothrow) LocalComm());
+        if (!c) return SHD_ERR_NOMEM;
+        c->g = g;
+        c->device = ctxs[r]->device;
+        c->rank = r;
+        c->size = n_ranks;
+        ctxs[r]->comm = std::move(c);
+        ctxs[r]->relay.ready = false;
+    }
+    return SHD_OK;
+}
+
+shd_status shd_comm_info(const shd_ctx* ctx, int32_t* n_ranks, int32_t* rank) {
+    if (!ctx) return SHD_ERR_INVALID;
+    if (n_ranks) *n_ranks = ctx->comm ? ctx->comm->size : 1;
+    if (rank) *rank = ctx->comm ? ctx->comm->rank : 0;
+    return SHD_OK;
+}
+
+shd_status shd_comm_destroy(shd_ctx* ctx) {
+    if (!ctx) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    if (ctx->stream) SHD_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->comm && ctx->relay.sharded) ctx->relay.ready = false;
+    ctx->comm.reset();
+    return SHD_OK;
+}
+
+shd_status shd_shard_range(uint32_t total, int32_t n_ranks, int32_t rank, uint32_t* lo, uint32_t* hi) {
+    if (!lo || !hi || n_ranks < 1 || rank < 0 || rank >= n_ranks) return SHD_ERR_INVALID;
+    shard_range(total, n_ranks, rank, lo, hi);
+    return SHD_OK;
+}
+
+}  // extern "C"

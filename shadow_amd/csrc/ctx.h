@@ -1,7 +1,9 @@
 // Engine context (one per GPU) and grow-only device scratch.
 #pragma once
+#include <memory>
 #include <vector>
 
+#include "comm.h"
 #include "common.h"
 
 namespace shd {
@@ -46,6 +48,16 @@ struct CodelState {   // CoDel router queues (codel.hip)
     bool ready = false;
 };
 
+struct EqState {   // destination event queues (equeue.hip): pending runs, double-buffered
+    DevBuf off[2], deliver[2], src[2], seq[2], tag[2];
+    DevBuf pd, ps, pq, pt;                       // the last call's popped events
+    DevBuf pop_cnt, keep_cnt, pop_off, next, scan_tmp;
+    int cur = 0;
+    uint32_t n_hosts = 0;
+    uint64_t n_pending = 0, n_popped = 0, batches = 0;
+    bool ready = false;
+};
+
 struct TbState {   // token-bucket relays (tbucket.hip)
     DevBuf st, err;
     uint32_t n_relays = 0;
@@ -55,6 +67,10 @@ struct TbState {   // token-bucket relays (tbucket.hip)
 struct RelayState {
     bool ready = false;
     uint32_t n_hosts = 0;
+    // source hosts this context stamps: all hosts, or (set up under a communicator of > 1
+    // ranks) the rank's shard [src_lo, src_lo + n_src), which is also its destination shard
+    uint32_t src_lo = 0, n_src = 0;
+    bool sharded = false;
     uint32_t n_nodes = 0;
     bool own_table = false;   // table copied by shd_relay_setup (else: routing resident table)
     bool table_narrow = false;  // every path latency < 2^32 ns -> 16-byte event records (v2)
@@ -64,13 +80,21 @@ struct RelayState {
     bool count_on = true;       // per-path packet counters (RoutingInfo::increment_packet_count)
     bool last_v2 = false;
     uint64_t seq_bound = 0;     // >= every host's next event id
+    uint64_t last_recv = 0;     // events this rank received in the last sharded round
     uint32_t hn_bits = 0, hn_words = 0;   // packed host -> node map (0 bits: not used)
     unsigned long long red_host[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    DevBuf host_node, order, hn_packed, lat, loss, path, rng, next_id, rng2, next_id2, counts;
+    // counts: per-path packet counters over all committed rounds; counts_round: the running
+    // round's increments, added to counts only when the round commits (a failed or rerun round
+    // leaves counts untouched)
+    DevBuf host_node, order, hn_packed, lat, loss, path, rng, next_id, rng2, next_id2, counts,
+        counts_round;
     // per-round scratch
     DevBuf pk_off, pk_time, pk_dst, pk_pay, pk_chance, st, ev_key, ev_key2, ev_val, ev_val2,
         ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, scan_tmp, red, rec, brec, tmp, draws,
         bin_cnt, bin_base, bin_lb;
+    // sharded rounds: packed outgoing events, exchange words, per-peer offset blocks, what was
+    // received, and the merged events of this rank's destinations (engine-owned outputs)
+    DevBuf x_rec, x_words, x_off, x_roff, x_rrec, m_off, m_deliver, m_src, m_seq, m_pkt;
 };
 
 struct PreparedGraph {
@@ -122,7 +146,11 @@ struct shd_ctx {
     shd::DevBuf g_off, g_dst, g_lat, g_q, g_lat64, g_used, g_diag_lat, g_diag_loss, g_flags,
         g_dense, g_prune_dst, g_prune_cnt, g_labels, g_aux, g_arc16, g_fw, g_glab;
 
+    std::unique_ptr<shd::Comm> comm;   // multi-GPU communicator (shd_comm_init*), or none
+    shd::DevBuf comm_scratch;
+
     shd::RelayState relay;
+    shd::EqState eq;
     shd::CodelState codel;
     shd::TbState tb;
 };

@@ -63,7 +63,8 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 
 struct RelayArgs {
     uint32_t n_hosts, n_nodes;
-    const uint32_t* src_off;
+    uint32_t src_lo, n_src;    // source hosts of this context: [src_lo, src_lo + n_src)
+    const uint32_t* src_off;   // [n_src + 1], host src_lo + k's sends are [src_off[k], src_off[k+1])
     const uint64_t* send_time;
     const uint32_t* dst_host;
     const uint32_t* payload;
@@ -86,15 +87,15 @@ struct RelayArgs {
 };
 
 __global__ __launch_bounds__(256) void relay_stamp(RelayArgs a) {
-    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t hl = blockIdx.x * 256 + threadIdx.x, h = a.src_lo + hl;
     uint64_t my_min_d = ~0ull, my_min_l = ~0ull, my_sent = 0;
-    if (h < a.n_hosts) {
+    if (hl < a.n_src) {
         Xoshiro r{a.rng[4 * (size_t)h], a.rng[4 * (size_t)h + 1], a.rng[4 * (size_t)h + 2],
                   a.rng[4 * (size_t)h + 3]};
         uint64_t id = a.next_id[h];
         const uint32_t sn = a.host_node[h];
-        const uint32_t i1 = a.src_off[h + 1];
-        for (uint32_t i = a.src_off[h]; i < i1; ++i) {
+        const uint32_t i1 = a.src_off[hl + 1];
+        for (uint32_t i = a.src_off[hl]; i < i1; ++i) {
             const uint64_t now = a.send_time[i];
             uint8_t st = kStSkipped;
             if (now < a.sim_end) {
@@ -153,7 +154,7 @@ __device__ __forceinline__ uint32_t owner_of(const uint32_t* off, uint32_t n_hos
 }
 
 __global__ __launch_bounds__(256) void relay_scatter(
-    uint64_t n, uint32_t n_hosts, const uint32_t* __restrict__ src_off,
+    uint64_t n, uint32_t n_src, uint32_t src_lo, const uint32_t* __restrict__ src_off,
     const uint8_t* __restrict__ status, const uint32_t* __restrict__ dst_host,
     const uint32_t* __restrict__ slot, const uint64_t* __restrict__ deliver,
     const uint64_t* __restrict__ seq, const uint32_t* __restrict__ ev_off,
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(256) void relay_scatter(
     if (i >= n || status[i] != kStSent) return;
     const uint32_t pos = ev_off[dst_host[i]] + slot[i];
     ev_deliver[pos] = deliver[i];
-    ev_src[pos] = owner_of(src_off, n_hosts, (uint32_t)i);
+    ev_src[pos] = src_lo + owner_of(src_off, n_src, (uint32_t)i);
     ev_seq[pos] = seq[i];
     ev_pkt[pos] = (uint32_t)i;
 }
@@ -295,13 +296,14 @@ __global__ __launch_bounds__(256) void segment_sort_big(
 // ==========================================================================================
 struct RelayArgs3 {
     uint32_t n_hosts, n_nodes;
-    const uint32_t* src_off;
+    uint32_t src_lo, n_src;    // source hosts of this context: [src_lo, src_lo + n_src)
+    const uint32_t* src_off;   // [n_src + 1], indexed by host - src_lo
     const uint64_t* send_time;
     const uint32_t* dst_host;
     const uint32_t* payload;
     const double* chance;
     const uint32_t* host_node;
-    const uint32_t* order;     // host ids sorted by host_node (workgroup -> hosts)
+    const uint32_t* order;     // the n_src source host ids sorted by host_node (workgroup -> hosts)
     const uint2* path;         // {latency ns (u32), packet loss bits} per node pair
     const uint64_t* rng;
     const uint64_t* next_id;
@@ -333,11 +335,11 @@ constexpr uint32_t kDrawSlice = 16;   // draws per host per LDS transpose (16: 4
 __global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint64_t* __restrict__ draw) {
     __shared__ uint64_t s[kDrawSlice][65];
     __shared__ uint32_t s_beg[64], s_nd[64];
-    const uint32_t lane = threadIdx.x, h = blockIdx.x * 64 + lane;
+    const uint32_t lane = threadIdx.x, hl = blockIdx.x * 64 + lane, h = a.src_lo + hl;
     uint32_t nd = 0;
     Xoshiro r{0, 0, 0, 0};
-    if (h < a.n_hosts) {
-        const uint32_t b = a.src_off[h], e = a.src_off[h + 1];
+    if (hl < a.n_src) {
+        const uint32_t b = a.src_off[hl], e = a.src_off[hl + 1];
         nd = e - b;
         if (nd && !(a.send_time[e - 1] < a.sim_end)) {   // first send with now >= sim_end
             uint32_t lo = b, hi = e;
@@ -371,7 +373,7 @@ __global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint64_t* __rest
         }
         __builtin_amdgcn_wave_barrier();
     }
-    if (h < a.n_hosts) {
+    if (hl < a.n_src) {
         a.rng_out[4 * (size_t)h] = r.s0;
         a.rng_out[4 * (size_t)h + 1] = r.s1;
         a.rng_out[4 * (size_t)h + 2] = r.s2;
@@ -408,13 +410,13 @@ __global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint64
     __shared__ uint32_t s_wsum[4], s_nrows;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t h0 = blockIdx.x * kS5Hosts;
-    const uint32_t nh = min(kS5Hosts, a.n_hosts - h0);
+    const uint32_t nh = min(kS5Hosts, a.n_src - h0);
     if (tid < 64) {   // wave 0: this workgroup's hosts, their ranges (prefix) and staged rows
         uint32_t len = 0, nd = 0;
         if (tid < nh) {
             const uint32_t h = a.order[h0 + tid];
-            const uint32_t b = a.src_off[h];
-            len = a.src_off[h + 1] - b;
+            const uint32_t b = a.src_off[h - a.src_lo];
+            len = a.src_off[h - a.src_lo + 1] - b;
             nd = a.host_node[h];
             s_host[tid] = h;
             s_beg[tid] = b;
@@ -630,7 +632,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     for (uint32_t i = tid; i < n_words; i += kS6Threads) s_tbl[i] = packed[i];
     if (BIN)
         for (uint32_t i = tid; i < (a.n_bins + 3) / 4; i += kS6Threads) s_cur[i] = 0;
-    const uint32_t n_groups = (a.n_hosts + kS5Hosts - 1) / kS5Hosts;
+    const uint32_t n_groups = (a.n_src + kS5Hosts - 1) / kS5Hosts;
     uint64_t min_d = ~0ull, min_l = ~0ull, ns_total = 0;
     bool wide = false, disorder = false;
     // wave 0 keeps the next group's host descriptors in registers: order[] is fetched when a
@@ -639,14 +641,14 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     uint32_t p_h = 0, p_b = 0, p_len = 0, p_nd = 0, p_base = 0;
     auto fetch_hosts = [&](uint32_t g) {
         const uint32_t hh0 = g * kS5Hosts;
-        if (g < n_groups && tid < min(kS5Hosts, a.n_hosts - hh0)) {
-            p_b = a.src_off[p_h];
-            p_len = a.src_off[p_h + 1] - p_b;
+        if (g < n_groups && tid < min(kS5Hosts, a.n_src - hh0)) {
+            p_b = a.src_off[p_h - a.src_lo];
+            p_len = a.src_off[p_h - a.src_lo + 1] - p_b;
             p_nd = a.host_node[p_h];
             p_base = a.abs_seq ? (uint32_t)a.next_id[p_h] : 0u;
         }
     };
-    if (tid < 64 && blockIdx.x < n_groups && tid < min(kS5Hosts, a.n_hosts - blockIdx.x * kS5Hosts)) {
+    if (tid < 64 && blockIdx.x < n_groups && tid < min(kS5Hosts, a.n_src - blockIdx.x * kS5Hosts)) {
         p_h = a.order[blockIdx.x * kS5Hosts + tid];
     }
     if (tid < 64) fetch_hosts(blockIdx.x);
@@ -662,7 +664,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     const uint64_t* __restrict__ rsrc = a.chance ? reinterpret_cast<const uint64_t*>(a.chance) : draw;
     for (uint32_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
         const uint32_t h0 = grp * kS5Hosts;
-        const uint32_t nh = min(kS5Hosts, a.n_hosts - h0);
+        const uint32_t nh = min(kS5Hosts, a.n_src - h0);
         const uint32_t nxt = grp + gridDim.x;
         __syncthreads();   // the previous group's host arrays / rows are no longer read
         SP_MARK(0);
@@ -677,7 +679,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 s_run[tid] = 0;
                 s_base[tid] = p_base;
             }
-            if (nxt < n_groups && tid < min(kS5Hosts, a.n_hosts - nxt * kS5Hosts))
+            if (nxt < n_groups && tid < min(kS5Hosts, a.n_src - nxt * kS5Hosts))
                 p_h = a.order[nxt * kS5Hosts + tid];
             uint32_t incl = len;
             for (uint32_t o = 1; o < 64; o <<= 1) {
@@ -721,7 +723,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
         for (uint32_t c0 = 0; c0 < T; c0 += kS6Cap) {
             const uint32_t cn = min(kS6Cap, T - c0);
             if (c0 == 0 && tid < 64) {   // the next group's distinct source nodes, as at its start
-                const uint32_t nh2 = nxt < n_groups ? min(kS5Hosts, a.n_hosts - nxt * kS5Hosts) : 0u;
+                const uint32_t nh2 = nxt < n_groups ? min(kS5Hosts, a.n_src - nxt * kS5Hosts) : 0u;
                 const uint32_t nd = p_nd, prev = __shfl_up(nd, 1);
                 const bool first = tid < nh2 && (tid == 0 || nd != prev);
                 const uint64_t fm = __ballot(first);
@@ -1328,6 +1330,8 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
     RelayArgs a{};
     a.n_hosts = H;
     a.n_nodes = R.n_nodes;
+    a.src_lo = R.src_lo;
+    a.n_src = R.n_src;
     a.src_off = b->src_off;
     a.send_time = b->send_time;
     a.dst_host = b->dst_host;
@@ -1340,7 +1344,7 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.next_id = R.next_id.as<uint64_t>();
     a.rng_out = R.rng2.as<uint64_t>();
     a.next_id_out = R.next_id2.as<uint64_t>();
-    a.counts = R.count_on ? R.counts.as<unsigned long long>() : nullptr;
+    a.counts = R.count_on ? R.counts_round.as<unsigned long long>() : nullptr;
     a.round_end = rd->round_end;
     a.sim_end = rd->sim_end;
     a.bootstrap_end = rd->bootstrap_end;
@@ -1350,7 +1354,7 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.slot = R.ev_val.as<uint32_t>();
     a.dst_cnt = R.dst_cnt.as<uint32_t>();
     a.red = R.red.as<unsigned long long>();
-    relay_stamp<<<div_up(H, 256), 256, 0, s>>>(a);
+    relay_stamp<<<div_up(std::max<uint32_t>(R.n_src, 1), 256), 256, 0, s>>>(a);
     SHD_HIP(hipGetLastError());
     size_t tmp_bytes = 0;
     SHD_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off, 0u,
@@ -1359,7 +1363,7 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
     SHD_HIP(rocprim::exclusive_scan(R.scan_tmp.p, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off,
                                     0u, (size_t)H + 1, rocprim::plus<uint32_t>(), s));
     if (n)
-        relay_scatter<<<div_up(n, 256), 256, 0, s>>>(n, H, b->src_off, o->status, b->dst_host,
+        relay_scatter<<<div_up(n, 256), 256, 0, s>>>(n, R.n_src, R.src_lo, b->src_off, o->status, b->dst_host,
                                                      R.ev_val.as<uint32_t>(), R.ev_key.as<uint64_t>(),
                                                      R.ev_key2.as<uint64_t>(), o->ev_off, o->ev_deliver,
                                                      o->ev_src, o->ev_seq, o->ev_pkt);
@@ -1416,16 +1420,16 @@ __global__ __launch_bounds__(256) void relay_bin_hist(RelayArgs3 a, uint32_t G, 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t g = blockIdx.x / kHistSplit, k = blockIdx.x % kHistSplit;
     for (uint32_t i = tid; i < a.n_bins; i += 256) s_cnt[i] = 0;
-    const uint32_t n_groups = (a.n_hosts + kS5Hosts - 1) / kS5Hosts;
+    const uint32_t n_groups = (a.n_src + kS5Hosts - 1) / kS5Hosts;
     for (uint32_t grp = g + k * G; grp < n_groups; grp += kHistSplit * G) {
-        const uint32_t h0 = grp * kS5Hosts, nh = min(kS5Hosts, a.n_hosts - h0);
+        const uint32_t h0 = grp * kS5Hosts, nh = min(kS5Hosts, a.n_src - h0);
         __syncthreads();
         if (tid < 64) {
             uint32_t len = 0;
             if (tid < nh) {
                 const uint32_t h = a.order[h0 + tid];
-                s_beg[tid] = a.src_off[h];
-                len = a.src_off[h + 1] - s_beg[tid];
+                s_beg[tid] = a.src_off[h - a.src_lo];
+                len = a.src_off[h - a.src_lo + 1] - s_beg[tid];
             }
             uint32_t incl = len;
             for (uint32_t o = 1; o < 64; o <<= 1) {
@@ -1771,6 +1775,8 @@ static RelayArgs3 relay_args3(shd_ctx* ctx, const shd_batch* b, const shd_round*
     RelayArgs3 a{};
     a.n_hosts = H;
     a.n_nodes = R.n_nodes;
+    a.src_lo = R.src_lo;
+    a.n_src = R.n_src;
     a.src_off = b->src_off;
     a.send_time = b->send_time;
     a.dst_host = b->dst_host;
@@ -1783,7 +1789,7 @@ static RelayArgs3 relay_args3(shd_ctx* ctx, const shd_batch* b, const shd_round*
     a.next_id = R.next_id.as<uint64_t>();
     a.rng_out = R.rng2.as<uint64_t>();
     a.next_id_out = R.next_id2.as<uint64_t>();
-    a.counts = R.count_on ? R.counts.as<unsigned long long>() : nullptr;
+    a.counts = R.count_on ? R.counts_round.as<unsigned long long>() : nullptr;
     a.round_end = rd->round_end;
     a.sim_end = rd->sim_end;
     a.bootstrap_end = rd->bootstrap_end;
@@ -1812,15 +1818,16 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.ev_val2.as<uint32_t>());
     RelayArgs3 a = relay_args3(ctx, b, rd, o);
     const uint64_t* seq_base = a.abs_seq ? nullptr : R.next_id.as<uint64_t>();
-    if (!b->chance)   // K0: the per-host generator streams
-        relay_draws<<<div_up(H, 64), 64, 0, s>>>(a, R.draws.as<uint64_t>());
-    if (R.hn_bits) {   // host -> node map fits the LDS: persistent stamp, no node gathers
-        const uint32_t groups = div_up(H, kS5Hosts);
+    if (!b->chance && R.n_src)   // K0: the per-host generator streams
+        relay_draws<<<div_up(R.n_src, 64), 64, 0, s>>>(a, R.draws.as<uint64_t>());
+    if (R.n_src == 0) {
+    } else if (R.hn_bits) {   // host -> node map fits the LDS: persistent stamp, no node gathers
+        const uint32_t groups = div_up(R.n_src, kS5Hosts);
         relay_stamp_v6<false><<<std::min<uint32_t>(groups, (uint32_t)ctx->n_cu), kS6Threads,
                          (size_t)R.hn_words * 4, s>>>(a, R.draws.as<uint64_t>(),
                                                       R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     } else {
-        relay_stamp_v5<<<div_up(H, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint64_t>());
+        relay_stamp_v5<<<div_up(R.n_src, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint64_t>());
     }
     SHD_HIP(hipGetLastError());
     // stable LSD radix sort of the records by destination (keys <= H)
@@ -1855,7 +1862,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
 static bool relay_v7_ok(shd_ctx* ctx, uint64_t n) {
     RelayState& R = ctx->relay;
     if (!R.hn_bits || R.force_v3 || R.n_hosts > kV7MaxHosts || n > kV7MaxPackets) return false;
-    if (std::min<uint32_t>(div_up(R.n_hosts, kS5Hosts), (uint32_t)ctx->n_cu) > kColMaxG) return false;
+    if (R.n_src == 0 || std::min<uint32_t>(div_up(R.n_src, kS5Hosts), (uint32_t)ctx->n_cu) > kColMaxG) return false;
     static size_t stat_lds = 0;
     if (!stat_lds) {
         hipFuncAttributes at{};
@@ -1874,7 +1881,7 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     const uint32_t H = R.n_hosts;
     const size_t nn = std::max<uint64_t>(n, 1);
     const uint32_t n_bins = div_up(H, kBinDst);
-    const uint32_t G = std::min<uint32_t>(div_up(H, kS5Hosts), (uint32_t)ctx->n_cu);
+    const uint32_t G = std::min<uint32_t>(div_up(R.n_src, kS5Hosts), (uint32_t)ctx->n_cu);
     SHD_TRY(R.rec.ensure(nn * 16));
     SHD_TRY(R.draws.ensure(nn * 8));
     SHD_TRY(R.bin_cnt.ensure((size_t)G * (kHistSplit + 1) * n_bins * 4));
@@ -1890,7 +1897,7 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     if (!b->chance) {   // K0: the per-host generator streams, on the side stream next to the bins
         SHD_HIP(hipEventRecord(ctx->sev[0], s));
         SHD_HIP(hipStreamWaitEvent(ctx->side, ctx->sev[0], 0));
-        relay_draws<<<div_up(H, 64), 64, 0, ctx->side>>>(a, R.draws.as<uint64_t>());
+        relay_draws<<<div_up(R.n_src, 64), 64, 0, ctx->side>>>(a, R.draws.as<uint64_t>());
         SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));
     }
     relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
@@ -1914,39 +1921,294 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
 
 // One round: the new host state (RNG streams, event ids) is written to the second buffer and
 // committed only when the round succeeds, so a failed round leaves the hosts untouched.
-static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
-                               shd_relay_out* o) {
+__global__ __launch_bounds__(256) void counts_commit(unsigned long long* __restrict__ counts,
+                                                     const unsigned long long* __restrict__ delta,
+                                                     uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n && delta[i]) {   // RoutingInfo::increment_packet_count saturates (graph/mod.rs:451-458)
+        const unsigned long long c = counts[i], d = delta[i];
+        counts[i] = c + d < c ? ~0ull : c + d;
+    }
+}
+
+// The round's pipelines and checks; nothing of the hosts' state is committed yet.
+static shd_status relay_run(shd_ctx* ctx, const shd_batch* b, const shd_round* rd, shd_relay_out* o) {
     RelayState& R = ctx->relay;
     const uint32_t H = R.n_hosts;
+    const uint64_t nn = (uint64_t)R.n_nodes * R.n_nodes;
     SHD_TRY(R.red.ensure(64));
     SHD_TRY(R.dst_cnt.ensure((size_t)(H + 1) * 4));
     SHD_TRY(R.scan_tmp.ensure(64));
+    // every pipeline attempt counts into a zeroed per-round buffer; only the committed attempt
+    // reaches the counters (a rerun or a failed round must not count)
+    auto zero_counts = [&]() -> shd_status {
+        if (R.count_on) SHD_HIP(hipMemsetAsync(R.counts_round.p, 0, nn * 8, ctx->stream));
+        return SHD_OK;
+    };
+    if (R.count_on) SHD_TRY(R.counts_round.ensure(nn * 8));
     bool v2 = R.table_narrow && !R.force_v1;
     R.last_pipe = 1;
     if (v2) {
         bool done = false;
         if (relay_v7_ok(ctx, b->n_packets)) {
+            SHD_TRY(zero_counts());
             SHD_TRY(relay_device_v7(ctx, b, rd, o));
             done = !R.red_host[6];   // else a bin overflowed: redo with the radix pipeline
             R.last_pipe = 7;
         }
         if (!done) {
+            SHD_TRY(zero_counts());
             SHD_TRY(relay_device_v3(ctx, b, rd, o));
             R.last_pipe = 3;
         }
         if (R.red_host[4]) v2 = false;   // a deliver offset needs 64 bits: redo with v1
     }
     if (!v2) R.last_pipe = 1;
-    if (!v2) SHD_TRY(relay_device_v1(ctx, b, rd, o));
+    if (!v2) {
+        SHD_TRY(zero_counts());
+        SHD_TRY(relay_device_v1(ctx, b, rd, o));
+    }
     if (R.red_host[3] != ~0ull) return SHD_ERR_NO_HOST;
     if (v2 && R.red_host[5]) return SHD_ERR_INVALID;   // a host's send times went backwards
+    R.last_v2 = v2;
+    return SHD_OK;
+}
+
+// Commit a successful round: the per-path counters, the new RNG streams and event ids.
+static shd_status relay_commit(shd_ctx* ctx, shd_relay_out* o) {
+    RelayState& R = ctx->relay;
+    const uint64_t nn = (uint64_t)R.n_nodes * R.n_nodes;
+    if (R.count_on && nn) {
+        counts_commit<<<div_up(nn, 256), 256, 0, ctx->stream>>>(
+            R.counts.as<unsigned long long>(), R.counts_round.as<unsigned long long>(), nn);
+        SHD_HIP(hipGetLastError());
+    }
     std::swap(R.rng, R.rng2);
     std::swap(R.next_id, R.next_id2);
     R.seq_bound += R.red_host[2];
     o->min_deliver = R.red_host[0];
     o->min_latency = R.red_host[1];
     o->n_sent = R.red_host[2];
-    R.last_v2 = v2;
+    return SHD_OK;
+}
+
+static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                               shd_relay_out* o) {
+    SHD_TRY(relay_run(ctx, b, rd, o));
+    return relay_commit(ctx, o);
+}
+
+// ------------------------------------------------------------------------------------------
+// Sharded rounds (hosts split by id over the ranks).  Each rank stamps its own
+// source hosts (their RNG streams and event ids live there) into events grouped by destination
+// over ALL hosts; the events bound for rank r's hosts are one contiguous slice.  Per round:
+//   1. local pipeline (as one GPU) -> events grouped by destination, in EventQueue order;
+//   2. pack them as 24-byte records (deliver, seq, src, packet) and write, per peer, the
+//      peer's per-destination offsets; one all-to-all of 5 words per peer carries the event
+//      count for that peer and this rank's (status, min deliver, min latency, sent) -- the
+//      round's reductions ride on the sizing exchange, no separate all-reduce;
+//   3. one host sync: sizes, and every rank's status (a failed round on any rank fails the
+//      round everywhere, no host state is committed);
+//   4. one grouped point-to-point exchange (offsets + records to every peer);
+//   5. device k-way merge of the per-sender runs into this rank's destinations' events: the
+//      senders own disjoint source ranges, so the merge by (deliver, src, seq) is EventQueue
+//      order again (event.rs:84-155).
+// ------------------------------------------------------------------------------------------
+struct Ev24 {
+    uint64_t deliver, seq;
+    uint32_t src, pkt;
+};
+static_assert(sizeof(Ev24) == 24, "24-byte event record");
+constexpr uint32_t kXWords = 5;   // per peer: count, status, min deliver, min latency, sent
+
+__global__ __launch_bounds__(256) void pack_events24(uint64_t n, const uint64_t* __restrict__ t,
+                                                     const uint64_t* __restrict__ q, const uint32_t* __restrict__ sv,
+                                                     const uint32_t* __restrict__ p, Ev24* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = Ev24{t[i], q[i], sv[i], p[i]};
+}
+
+__device__ __forceinline__ void shard_of(uint32_t total, uint32_t world, uint32_t r, uint32_t* lo, uint32_t* hi) {
+    const uint64_t per = ((uint64_t)total + world - 1) / world;
+    const uint64_t a = min((uint64_t)r * per, (uint64_t)total);
+    *lo = (uint32_t)a;
+    *hi = (uint32_t)min(a + per, (uint64_t)total);
+}
+
+__global__ __launch_bounds__(64) void shard_words(uint32_t world, uint32_t H, const uint32_t* __restrict__ ev_off,
+                                                  uint64_t st, uint64_t md, uint64_t ml, uint64_t ns,
+                                                  uint64_t* __restrict__ words) {
+    const uint32_t r = threadIdx.x;
+    if (r >= world) return;
+    uint32_t lo, hi;
+    shard_of(H, world, r, &lo, &hi);
+    uint64_t* w = words + (size_t)r * kXWords;
+    w[0] = ev_off ? (uint64_t)(ev_off[hi] - ev_off[lo]) : 0ull;
+    w[1] = st;
+    w[2] = md;
+    w[3] = ml;
+    w[4] = ns;
+}
+
+// peer r's block: its destinations' offsets relative to the slice start, at stage[lo_r + r ..]
+__global__ __launch_bounds__(256) void shard_offsets(uint32_t world, uint32_t H, const uint32_t* __restrict__ ev_off,
+                                                     uint32_t* __restrict__ stage) {
+    const uint32_t r = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    uint32_t lo, hi;
+    shard_of(H, world, r, &lo, &hi);
+    if (i <= hi - lo) stage[lo + r + i] = ev_off[lo + i] - ev_off[lo];
+}
+
+// thread per received event: its rank among its destination's events of all runs
+__global__ __launch_bounds__(256) void merge_runs24(uint32_t n_runs, uint32_t n_dst,
+                                                    const uint32_t* __restrict__ base,   // [n_runs + 1]
+                                                    const uint32_t* __restrict__ off,    // [n_runs][n_dst + 1]
+                                                    const Ev24* __restrict__ in,
+                                                    const uint32_t* __restrict__ out_off,
+                                                    uint64_t* __restrict__ out_t, uint32_t* __restrict__ out_s,
+                                                    uint64_t* __restrict__ out_q, uint32_t* __restrict__ out_p) {
+    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= base[n_runs]) return;
+    uint32_t r = 0;
+    while (r + 1 < n_runs && base[r + 1] <= e) ++r;
+    const uint32_t le = e - base[r];
+    const uint32_t* o = off + (size_t)r * (n_dst + 1);
+    uint32_t lo = 0, hi = n_dst;   // d with o[d] <= le < o[d+1]
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (o[m] <= le) lo = m; else hi = m;
+    }
+    const uint32_t d = lo;
+    const Ev24 x = in[e];
+    uint32_t rank = le - o[d];
+    for (uint32_t r2 = 0; r2 < n_runs; ++r2) {
+        if (r2 == r) continue;
+        const uint32_t* o2 = off + (size_t)r2 * (n_dst + 1);
+        uint32_t a = base[r2] + o2[d], b = base[r2] + o2[d + 1];
+        const uint32_t a0 = a;
+        while (a < b) {   // run r2's events of destination d that come before this one
+            const uint32_t m = (a + b) >> 1;
+            const Ev24 y = in[m];
+            if (ev3_less(y.deliver, y.src, y.seq, x.deliver, x.src, x.seq)) a = m + 1; else b = m;
+        }
+        rank += a - a0;
+    }
+    const uint32_t pos = out_off[d] + rank;
+    out_t[pos] = x.deliver;
+    out_s[pos] = x.src;
+    out_q[pos] = x.seq;
+    out_p[pos] = x.pkt;
+}
+
+static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                                      shd_relay_out* d_out) {
+    RelayState& R = ctx->relay;
+    Comm& C = *ctx->comm;
+    hipStream_t s = ctx->stream;
+    const uint32_t H = R.n_hosts, world = (uint32_t)C.size;
+    const uint64_t n = b->n_packets;
+    const size_t nn = std::max<uint64_t>(n, 1);
+    // 1. the local pipeline into internal buffers (the caller's status array)
+    shd_status st = SHD_OK;
+    shd_relay_out lo{};
+    if (R.ev_off.ensure((size_t)(H + 1) * 4) != SHD_OK || R.ev_deliver.ensure(nn * 8) != SHD_OK ||
+        R.ev_src.ensure(nn * 4) != SHD_OK || R.ev_seq.ensure(nn * 8) != SHD_OK ||
+        R.ev_pkt.ensure(nn * 4) != SHD_OK || R.x_rec.ensure(nn * 24) != SHD_OK)
+        st = SHD_ERR_NOMEM;
+    if (st == SHD_OK) {
+        lo.status = d_out->status;
+        lo.ev_off = R.ev_off.as<uint32_t>();
+        lo.ev_deliver = R.ev_deliver.as<uint64_t>();
+        lo.ev_src = R.ev_src.as<uint32_t>();
+        lo.ev_seq = R.ev_seq.as<uint64_t>();
+        lo.ev_pkt = R.ev_pkt.as<uint32_t>();
+        st = relay_run(ctx, b, rd, &lo);
+    }
+    // 2. records, per-peer offset blocks, the sizing words (with this rank's reductions)
+    SHD_TRY(R.x_words.ensure((size_t)world * kXWords * 16));
+    SHD_TRY(R.x_off.ensure(((size_t)H + world) * 4));
+    uint64_t* w_send = R.x_words.as<uint64_t>();
+    uint64_t* w_recv = w_send + (size_t)world * kXWords;
+    const uint64_t ns_local = st == SHD_OK ? R.red_host[2] : 0;
+    if (st == SHD_OK && ns_local)
+        pack_events24<<<div_up(ns_local, 256), 256, 0, s>>>(ns_local, lo.ev_deliver, lo.ev_seq, lo.ev_src,
+                                                            lo.ev_pkt, R.x_rec.as<Ev24>());
+    shard_words<<<1, 64, 0, s>>>(world, H, st == SHD_OK ? lo.ev_off : nullptr, (uint64_t)st,
+                                 st == SHD_OK ? R.red_host[0] : ~0ull, st == SHD_OK ? R.red_host[1] : ~0ull,
+                                 ns_local, w_send);
+    if (st == SHD_OK)
+        shard_offsets<<<dim3(div_up((uint64_t)(H + world - 1) / world + 1, 256), world), 256, 0, s>>>(
+            world, H, lo.ev_off, R.x_off.as<uint32_t>());
+    SHD_HIP(hipGetLastError());
+    SHD_TRY(C.all_to_all_u64(w_send, w_recv, kXWords, s));
+    // 3. one host sync: what every peer sends here, and every rank's outcome
+    std::vector<uint64_t> w(2 * (size_t)world * kXWords);
+    SHD_HIP(hipMemcpyAsync(w.data(), w_send, w.size() * 8, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    const uint64_t* ws = w.data();
+    const uint64_t* wr = w.data() + (size_t)world * kXWords;
+    uint64_t md = ~0ull, ml = ~0ull, ns = 0;
+    for (uint32_t q = 0; q < world; ++q) {
+        const uint64_t* x = wr + (size_t)q * kXWords;
+        if ((shd_status)x[1] != SHD_OK) return (shd_status)x[1];   // the lowest failing rank's
+        md = std::min<uint64_t>(md, x[2]);
+        ml = std::min<uint64_t>(ml, x[3]);
+        ns += x[4];
+    }
+    // 4. the exchange: part 0 = offsets block, part 1 = records
+    uint32_t own_lo = 0, own_hi = 0;
+    shard_range(H, (int)world, C.rank, &own_lo, &own_hi);
+    const uint32_t n_own = own_hi - own_lo;
+    std::vector<uint32_t> rbase(world + 1, 0);
+    for (uint32_t q = 0; q < world; ++q) rbase[q + 1] = rbase[q] + (uint32_t)wr[(size_t)q * kXWords];
+    const uint64_t n_recv = rbase[world];
+    SHD_TRY(R.x_roff.ensure((size_t)world * (n_own + 1) * 4 + (size_t)(world + 1) * 4));
+    SHD_TRY(R.x_rrec.ensure(std::max<uint64_t>(n_recv, 1) * 24));
+    std::vector<const void*> sp(2 * world);
+    std::vector<void*> rp(2 * world);
+    std::vector<size_t> sb(2 * world), rb(2 * world);
+    uint64_t sent_before = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+        uint32_t a = 0, z = 0;
+        shard_range(H, (int)world, (int)r, &a, &z);
+        sp[2 * r] = R.x_off.as<uint32_t>() + a + r;
+        sb[2 * r] = (size_t)(z - a + 1) * 4;
+        sp[2 * r + 1] = R.x_rec.as<Ev24>() + sent_before;
+        sb[2 * r + 1] = (size_t)ws[(size_t)r * kXWords] * 24;
+        sent_before += ws[(size_t)r * kXWords];
+        rp[2 * r] = R.x_roff.as<uint32_t>() + (size_t)r * (n_own + 1);
+        rb[2 * r] = (size_t)(n_own + 1) * 4;
+        rp[2 * r + 1] = R.x_rrec.as<Ev24>() + rbase[r];
+        rb[2 * r + 1] = (size_t)wr[(size_t)r * kXWords] * 24;
+    }
+    SHD_TRY(C.exchange(2, sp.data(), sb.data(), rp.data(), rb.data(), s));
+    // 5. merge the per-sender runs
+    SHD_TRY(R.m_off.ensure((size_t)(n_own + 1) * 4));
+    SHD_TRY(R.m_deliver.ensure(std::max<uint64_t>(n_recv, 1) * 8));
+    SHD_TRY(R.m_src.ensure(std::max<uint64_t>(n_recv, 1) * 4));
+    SHD_TRY(R.m_seq.ensure(std::max<uint64_t>(n_recv, 1) * 8));
+    SHD_TRY(R.m_pkt.ensure(std::max<uint64_t>(n_recv, 1) * 4));
+    uint32_t* d_base = R.x_roff.as<uint32_t>() + (size_t)world * (n_own + 1);
+    SHD_HIP(hipMemcpyAsync(d_base, rbase.data(), (world + 1) * 4, hipMemcpyHostToDevice, s));
+    merge_offsets<<<div_up((uint64_t)n_own + 1, 256), 256, 0, s>>>(world, n_own, R.x_roff.as<uint32_t>(),
+                                                                  R.m_off.as<uint32_t>());
+    if (n_recv)
+        merge_runs24<<<div_up(n_recv, 256), 256, 0, s>>>(world, n_own, d_base, R.x_roff.as<uint32_t>(),
+                                                        R.x_rrec.as<Ev24>(), R.m_off.as<uint32_t>(),
+                                                        R.m_deliver.as<uint64_t>(), R.m_src.as<uint32_t>(),
+                                                        R.m_seq.as<uint64_t>(), R.m_pkt.as<uint32_t>());
+    SHD_HIP(hipGetLastError());
+    SHD_TRY(relay_commit(ctx, &lo));
+    SHD_HIP(hipStreamSynchronize(s));   // rbase (host memory) was read by the copy above
+    d_out->ev_off = R.m_off.as<uint32_t>();
+    d_out->ev_deliver = R.m_deliver.as<uint64_t>();
+    d_out->ev_src = R.m_src.as<uint32_t>();
+    d_out->ev_seq = R.m_seq.as<uint64_t>();
+    d_out->ev_pkt = R.m_pkt.as<uint32_t>();
+    d_out->min_deliver = md;
+    d_out->min_latency = ml;
+    d_out->n_sent = ns;
+    R.last_recv = n_recv;
     return SHD_OK;
 }
 
@@ -1985,17 +2247,28 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
     SHD_TRY(R.next_id2.ensure((size_t)n_hosts * 8));
     SHD_TRY(R.counts.ensure((size_t)n_nodes * n_nodes * 8));
     SHD_HIP(hipMemcpyAsync(R.host_node.p, host_node, (size_t)n_hosts * 4, hipMemcpyHostToDevice, s));
+    // under a communicator of > 1 ranks this context stamps only its shard of the hosts
+    R.sharded = ctx->comm && ctx->comm->size > 1;
+    uint32_t src_lo = 0, src_hi = n_hosts;
+    if (R.sharded) shard_range(n_hosts, ctx->comm->size, ctx->comm->rank, &src_lo, &src_hi);
+    R.src_lo = src_lo;
+    R.n_src = src_hi - src_lo;
     {   // stamp workgroups take hosts in source-node order: their path gathers share table rows
-        std::vector<uint32_t> ord(n_hosts);
-        for (uint32_t h = 0; h < n_hosts; h++) ord[h] = h;
+        std::vector<uint32_t> ord(R.n_src);
+        for (uint32_t h = 0; h < R.n_src; h++) ord[h] = src_lo + h;
         std::stable_sort(ord.begin(), ord.end(),
                          [&](uint32_t x, uint32_t y) { return host_node[x] < host_node[y]; });
-        SHD_TRY(R.order.ensure((size_t)n_hosts * 4));
-        SHD_HIP(hipMemcpyAsync(R.order.p, ord.data(), (size_t)n_hosts * 4, hipMemcpyHostToDevice, s));
+        SHD_TRY(R.order.ensure(std::max<size_t>(ord.size(), 1) * 4));
+        if (!ord.empty())
+            SHD_HIP(hipMemcpyAsync(R.order.p, ord.data(), ord.size() * 4, hipMemcpyHostToDevice, s));
         SHD_HIP(hipStreamSynchronize(s));
     }
+    // both state buffers hold every host: a round writes only its source hosts' entries into the
+    // second buffer, so the others keep their values across the swap
     SHD_HIP(hipMemcpyAsync(R.rng.p, rng_state, (size_t)n_hosts * 32, hipMemcpyHostToDevice, s));
     SHD_HIP(hipMemcpyAsync(R.next_id.p, next_event_id, (size_t)n_hosts * 8, hipMemcpyHostToDevice, s));
+    SHD_HIP(hipMemcpyAsync(R.rng2.p, rng_state, (size_t)n_hosts * 32, hipMemcpyHostToDevice, s));
+    SHD_HIP(hipMemcpyAsync(R.next_id2.p, next_event_id, (size_t)n_hosts * 8, hipMemcpyHostToDevice, s));
     R.seq_bound = 0;   // upper bound of every next event id (grows by n_sent per round)
     for (uint32_t h = 0; h < n_hosts; h++) R.seq_bound = std::max<uint64_t>(R.seq_bound, next_event_id[h]);
     SHD_HIP(hipMemsetAsync(R.counts.p, 0, (size_t)n_nodes * n_nodes * 8, s));
@@ -2050,7 +2323,7 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
 shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const shd_round* round,
                                   shd_relay_out* d_out) {
     if (!ctx || !d_batch || !round || !d_out) return SHD_ERR_INVALID;
-    if (!ctx->relay.ready) return SHD_ERR_STATE;
+    if (!ctx->relay.ready || ctx->relay.sharded) return SHD_ERR_STATE;
     if (!d_batch->src_off || (d_batch->n_packets && (!d_batch->send_time || !d_batch->dst_host ||
                                                      !d_batch->payload)))
         return SHD_ERR_INVALID;
@@ -2065,7 +2338,7 @@ shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round
                            shd_relay_out* out) {
     if (!ctx || !batch || !round || !out || !batch->src_off) return SHD_ERR_INVALID;
     RelayState& R = ctx->relay;
-    if (!R.ready) return SHD_ERR_STATE;
+    if (!R.ready || R.sharded) return SHD_ERR_STATE;
     SHD_HIP(hipSetDevice(ctx->device));
     const uint64_t n = batch->n_packets;
     const uint32_t H = R.n_hosts;
@@ -2120,6 +2393,19 @@ shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round
     out->min_latency = dout.min_latency;
     out->n_sent = ns;
     return SHD_OK;
+}
+
+shd_status shd_relay_round_sharded(shd_ctx* ctx, const shd_batch* d_batch, const shd_round* round,
+                                   shd_relay_out* d_out) {
+    if (!ctx || !d_batch || !round || !d_out) return SHD_ERR_INVALID;
+    if (!ctx->comm || !ctx->relay.ready || ctx->relay.sharded != (ctx->comm->size > 1))
+        return SHD_ERR_STATE;
+    if (!d_batch->src_off || (d_batch->n_packets && (!d_batch->send_time || !d_batch->dst_host ||
+                                                     !d_batch->payload)))
+        return SHD_ERR_INVALID;
+    if (d_batch->n_packets && !d_out->status) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    return relay_round_sharded(ctx, d_batch, round, d_out);
 }
 
 shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t* next_event_id) {

@@ -642,6 +642,9 @@ static shd_status validate(const shd_graph* g, const uint32_t* used, uint32_t n_
         return SHD_ERR_INVALID;
     for (uint32_t i = 0; i < g->n_edges; i++) {
         if (g->edge_src[i] >= g->n_nodes || g->edge_dst[i] >= g->n_nodes) return SHD_ERR_INVALID;
+        // ShadowEdge::try_from rejects latency 0 (graph/mod.rs:107); the kernels rely on every
+        // arc strictly increasing latency (unique fixed point = Dijkstra's pop-order result)
+        if (g->edge_latency_ns[i] == 0) return SHD_ERR_INVALID;
         const float p = g->edge_packet_loss[i];
         if (!(p >= 0.0f && p <= 1.0f)) return SHD_ERR_INVALID;  // ShadowEdge::try_from range
     }

@@ -170,3 +170,9 @@ def test_capacity_overflow_reported(engine):
     off = np.array([0, 5, 5], np.uint32)
     with pytest.raises(ShdError, match="INVALID"):
         q.run(off, [START] * 5, [1500] * 5, list(range(5)))
+    # the overflowing batch left the queues undefined: no further batch until set up again
+    with pytest.raises(ShdError, match="STATE"):
+        q.run(off, [START] * 5, [1500] * 5, list(range(5)))
+    q2 = CoDelQueues(engine, 2, 8)
+    pop, _ = q2.run(off, [START] * 5, [1500] * 5, list(range(5)))
+    assert (pop == 0xFFFFFFFF).all()

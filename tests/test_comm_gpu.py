@@ -1,0 +1,206 @@
+"""GPU tests of the engine's multi-GPU path through the C ABI (shd_comm_*, shd_*_sharded).
+
+RCCL refuses two ranks on one GPU ("Duplicate GPU detected"), so the two-rank tests use the
+in-process communicator (shd_comm_init_local): two contexts on cuda:0, each driven by its own
+host thread, exactly as two ranks would run; the sharding, the sizing exchange, the packed
+record exchange and the merge are the same code as under RCCL.  The RCCL transport itself runs
+at world size 1 here (and at 8 in the driver's scaling bench)."""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import corc
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_ranks(fns):
+    res, errs = [None] * len(fns), []
+
+    def wrap(i):
+        try:
+            res[i] = fns[i]()
+        except BaseException as e:   # noqa: BLE001 -- reported below
+            errs.append(e)
+    ts = [threading.Thread(target=wrap, args=(i,)) for i in range(len(fns))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in ts), "a rank hung"
+    if errs:
+        raise errs[0]
+    return res
+
+
+def _case(H, NN, seed):
+    from shadow_amd import synth
+    el = synth.complete_graph(NN, seed)
+    used = np.arange(NN, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(NN, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    return el, lat, loss, synth.c5_host_nodes(H, NN), synth.host_rng_states(H, 1)
+
+
+def _slice_batch(b, lo, hi):
+    a, e = int(b.src_off[lo]), int(b.src_off[hi])
+    return (b.src_off[lo:hi + 1] - b.src_off[lo]).astype(np.uint32), b.send_time[a:e], b.dst_host[a:e], b.payload[a:e], a
+
+
+def _check_rank(rank_out, o, lo, hi, a_of, b):
+    status, ev, md, ml, ns = rank_out
+    a, e = int(b.src_off[lo]), int(b.src_off[hi])
+    assert np.array_equal(status, o["status"][a:e])
+    oe = o["events"]
+    s0, s1 = int(oe["off"][lo]), int(oe["off"][hi])
+    assert np.array_equal(ev["off"], (oe["off"][lo:hi + 1] - oe["off"][lo]).astype(np.uint32))
+    assert np.array_equal(ev["deliver"], oe["deliver"][s0:s1])
+    assert np.array_equal(ev["src"], oe["src"][s0:s1])
+    assert np.array_equal(ev["seq"], oe["seq"][s0:s1])
+    # ev_pkt is the index in the sender rank's batch: the sender's batch base gives the global one
+    glob = ev["pkt"].astype(np.int64) + a_of(ev["src"])
+    assert np.array_equal(glob, oe["pkt"][s0:s1].astype(np.int64))
+    assert (md, ml, ns) == (o["min_deliver"], o["min_latency"], o["n_sent"])
+
+
+def test_local_two_ranks_relay_rounds(engine):
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd.routing import Engine
+    H, NN, P = 5000, 50, 400_000
+    _, lat, loss, host_node, rng0 = _case(H, NN, 3)
+    engines = [Engine(0), Engine(0)]
+    try:
+        D.comm_init_local(engines)
+        rels = [D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss) for e in engines]
+        assert [(r.lo, r.hi) for r in rels] == [(0, 2500), (2500, 5000)]
+        orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+        start, ra = 10**9, 10**6
+        for rnd in range(3):
+            b = synth.packet_batch(H, P, start, start + ra, seed=90 + rnd)
+            o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, orng, onid,
+                                 start + ra, start + 10**12, start + ra // 2 if rnd == 0 else 0)
+            rd = (start + ra, start + 10**12, start + ra // 2 if rnd == 0 else 0)
+            parts = [_slice_batch(b, r.lo, r.hi) for r in rels]
+            outs = _run_ranks([lambda r=r, p=p: r.round(*p[:4], rd) for r, p in zip(rels, parts)])
+            bases = np.array([p[4] for p in parts], np.int64)
+
+            def a_of(src):
+                return bases[(src >= 2500).astype(np.int64)]
+            for r, out in zip(rels, outs):
+                _check_rank(out, o, r.lo, r.hi, a_of, b)
+            for r in rels:   # each rank's own hosts carry the advanced streams and ids
+                st, nid = r.host_state()
+                assert np.array_equal(st[r.lo:r.hi], orng[r.lo:r.hi])
+                assert np.array_equal(nid[r.lo:r.hi], onid[r.lo:r.hi])
+            start += ra
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_local_two_ranks_failure_is_global(engine):
+    """A bad destination on rank 1 fails the round on both ranks; no rank commits state."""
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd._native import ShdError
+    from shadow_amd.routing import Engine
+    H, NN = 1000, 20
+    _, lat, loss, host_node, rng0 = _case(H, NN, 5)
+    engines = [Engine(0), Engine(0)]
+    try:
+        D.comm_init_local(engines)
+        rels = [D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss) for e in engines]
+        b = synth.packet_batch(H, 50_000, 10**9, 10**9 + 10**6, seed=7)
+        parts = [list(_slice_batch(b, r.lo, r.hi)) for r in rels]
+        parts[1][2] = parts[1][2].copy()
+        parts[1][2][5] = H + 9
+        rd = (10**9 + 10**6, 10**12, 0)
+
+        def go(r, p):
+            try:
+                r.round(*p[:4], rd)
+            except ShdError as e:
+                return e.code
+            return "OK"
+        codes = _run_ranks([lambda r=r, p=p: go(r, p) for r, p in zip(rels, parts)])
+        assert codes == ["NO_HOST", "NO_HOST"]
+        for r in rels:
+            st, nid = r.host_state()
+            assert np.array_equal(st, rng0) and not nid.any()
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_local_two_ranks_routing_sharded(engine):
+    import torch
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd.routing import Engine
+    from tests.graphs import engine_graph_from_edges
+    import ctypes as C
+    from shadow_amd import _native as N
+    n = 301
+    el = synth.complete_graph(n, 12)
+    used = np.arange(n, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(n, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    engines = [Engine(0), Engine(0)]
+    try:
+        D.comm_init_local(engines)
+        g = engine_graph_from_edges(el)
+        per = (n + 1) // 2
+        bufs = []
+        for e in engines:
+            cg = g._cgraph()
+            err = N.Error()
+            N.check(e.lib.shd_routing_prepare(e.ctx, C.byref(cg), N.ptr(used), n, N.ROUTE_SHORTEST, C.byref(err)),
+                    "prepare", err)
+            bufs.append((torch.empty((2 * per, n), dtype=torch.int64, device="cuda"),
+                         torch.empty((2 * per, n), dtype=torch.float32, device="cuda")))
+        torch.cuda.synchronize()
+        _run_ranks([lambda e=e, b=b: D.routing_run_sharded(e, N.ALGO_AUTO, b[0], b[1]) for e, b in zip(engines, bufs)])
+        for lt, ls in bufs:
+            assert np.array_equal(lt[:n].cpu().numpy().view(np.uint64), lat)
+            assert np.array_equal(ls[:n].cpu().numpy().view(np.uint32), loss.view(np.uint32))
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_rccl_world_one(engine):
+    """The RCCL transport at world size 1: the sharded relay and routing calls go through
+    ncclAllToAll / grouped send-recv / ncclAllGather with this rank alone."""
+    import ctypes as C
+
+    import torch
+    from shadow_amd import _native as N
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd.routing import Engine
+    from tests.graphs import engine_graph_from_edges
+    H, NN = 2000, 40
+    el, lat, loss, host_node, rng0 = _case(H, NN, 8)
+    e = Engine(0)
+    try:
+        D.comm_init_rccl(e)
+        r = D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss)
+        b = synth.packet_batch(H, 100_000, 10**9, 10**9 + 10**6, seed=8)
+        o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(),
+                             np.zeros(H, np.uint64), 10**9 + 10**6, 10**12, 0)
+        out = r.round(b.src_off, b.send_time, b.dst_host, b.payload, (10**9 + 10**6, 10**12, 0))
+        _check_rank(out, o, 0, H, lambda src: np.zeros(len(src), np.int64), b)
+        g = engine_graph_from_edges(el)
+        cg = g._cgraph()
+        used = np.arange(NN, dtype=np.uint32)
+        err = N.Error()
+        N.check(e.lib.shd_routing_prepare(e.ctx, C.byref(cg), N.ptr(used), NN, N.ROUTE_SHORTEST, C.byref(err)),
+                "prepare", err)
+        lt = torch.empty((NN, NN), dtype=torch.int64, device="cuda")
+        ls = torch.empty((NN, NN), dtype=torch.float32, device="cuda")
+        D.routing_run_sharded(e, N.ALGO_AUTO, lt, ls)
+        assert np.array_equal(lt.cpu().numpy().view(np.uint64), lat)
+        assert np.array_equal(ls.cpu().numpy().view(np.uint32), loss.view(np.uint32))
+    finally:
+        e.close()

@@ -1,0 +1,85 @@
+"""Parity at BASELINE.json's configured sizes, against the C restatement:
+
+  * C3 -- the 10k-node BA graph, the whole 10k x 10k table, every routing engine;
+  * C4 -- the 50k-node BA m=4 graph: its table is 30 GB, so source-row slices at the start, the
+          middle and the end of the used set, built by the global-label kernel, checked against
+          the row-range oracle (orc_shortest_paths_rows);
+  * C5 -- 100k hosts x 10M packets per round on the C2 table, two consecutive rounds (RNG
+          streams and event ids carried), every status and every event compared.
+"""
+import numpy as np
+import pytest
+
+from oracle import corc
+from tests.graphs import engine_graph_from_edges
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_rows(t, lat, loss):
+    assert np.array_equal(t.lat, lat)
+    assert np.array_equal(t.loss.view(np.uint32), loss.view(np.uint32))
+
+
+@pytest.fixture(scope="module")
+def c4():
+    from shadow_amd import synth
+    el = synth.barabasi_albert(50_000, 4, 3)
+    return el, engine_graph_from_edges(el), np.arange(50_000, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("rows", [(0, 64), (25_000, 25_064), (49_936, 50_000)])
+def test_c4_row_slices_bit_exact(engine, c4, rows):
+    el, g, used = c4
+    code, lat, loss, _ = corc.routing(50_000, el.src, el.dst, el.latency_ns, el.packet_loss, False,
+                                      used, rows=rows)
+    assert code == "OK"
+    for algo in (1, 3):   # label-correcting SSSP, delta-stepping (both on the global-label kernel)
+        t = g.compute_shortest_paths(used, engine, algo=algo, rows=rows)
+        info = engine.last_info()
+        assert info["algo_used"] == algo and info["wide_latency"] == 0
+        _assert_rows(t, lat, loss)
+
+
+def test_c3_full_table_bit_exact(engine):
+    from shadow_amd import synth
+    el = synth.barabasi_albert(10_000, 3, 2)
+    used = np.arange(10_000, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(10_000, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    g = engine_graph_from_edges(el)
+    for algo in (1, 3, 4):
+        t = g.compute_shortest_paths(used, engine, algo=algo)
+        assert engine.last_info()["algo_used"] == algo
+        _assert_rows(t, lat, loss)
+        del t
+
+
+def test_c5_full_two_rounds_bit_exact(engine):
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    H, P = 100_000, 10_000_000
+    el = synth.complete_graph(1000, 1)
+    used = np.arange(1000, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(1000, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    host_node = synth.c5_host_nodes(H, 1000)
+    rng0 = synth.host_rng_states(H, 1)
+    orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+    rl = Relay(host_node, rng0, onid.copy(), lat, loss, engine=engine)
+    start, ra = synth.SIM_START + 10**9, 10**6
+    for rnd in range(2):
+        b = synth.packet_batch(H, P, start, start + ra, seed=4 + rnd)
+        o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss,
+                             orng, onid, start + ra, start + 10**12, 0)
+        r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, start + ra, start + 10**12, 0)
+        assert rl.last_pipeline() == 7
+        assert np.array_equal(r.status, o["status"])
+        ev = o["events"]
+        assert np.array_equal(r.ev_off, ev["off"])
+        for k in ("deliver", "src", "seq", "pkt"):
+            assert np.array_equal(getattr(r, "ev_" + k), ev[k]), k
+        assert (r.min_deliver, r.min_latency, r.n_sent) == (o["min_deliver"], o["min_latency"], o["n_sent"])
+        st, nid = rl.host_state()
+        assert np.array_equal(st, orng) and np.array_equal(nid, onid)
+        start += ra

@@ -1,0 +1,84 @@
+"""GPU parity of the device-resident destination event queues against the
+EventQueue restatement (oracle/relay.py: BinaryHeap per host, event.rs order, the pop loop of
+Host::execute host.rs:697-706).  Path latencies (1-300 ms) exceed the 50 ms window, so events
+stay pending across several rounds before they are popped."""
+import numpy as np
+import pytest
+
+from oracle import corc
+from oracle.relay import EventQueues as OracleQueues
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(p, oq, H, window_end):
+    for h in range(H):
+        want = oq.pop_until(h, window_end)
+        got = p.events_for(h)
+        assert got == [(t, s, q, g) for t, s, q, g in want], h
+    n_pending = sum(len(q) for q in oq.q)
+    assert p.n_pending == n_pending
+    heads = [oq.next_event_time(h) for h in range(H)]
+    heads = [x for x in heads if x is not None]
+    assert p.next_time == (min(heads) if heads else 2**64 - 1)
+
+
+@pytest.mark.parametrize("chance_mode", [False, True])
+def test_queues_across_rounds_vs_oracle(engine, chance_mode):
+    from shadow_amd import synth
+    from shadow_amd.equeue import EventQueues
+    from shadow_amd.relay import Relay
+    H, NN, P = 3000, 60, 120_000
+    el = synth.complete_graph(NN, 31)
+    used = np.arange(NN, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(NN, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    host_node = synth.c5_host_nodes(H, NN)
+    rng0 = synth.host_rng_states(H, 1)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    q = EventQueues(engine, H)
+    oq = OracleQueues(H)
+    orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+    start, win = 10**9, 50 * 10**6
+    for rnd in range(6):
+        b = synth.packet_batch(H, P, start, start + win, seed=70 + rnd)
+        chance = np.random.default_rng(rnd).random(b.n) if chance_mode else None
+        r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, start + win, start + 10**12, 0,
+                     chance=chance)
+        o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, orng, onid,
+                             start + win, start + 10**12, 0, chance=chance)
+        ev = o["events"]
+        for d in range(H):
+            for k in range(int(ev["off"][d]), int(ev["off"][d + 1])):
+                oq.push(d, ev["deliver"][k], ev["src"][k], ev["seq"][k], (rnd << 32) | int(ev["pkt"][k]))
+        # the next round's window: [start + win, start + 2 win)
+        p = q.advance(r.ev_off, r.ev_deliver, r.ev_src, r.ev_seq, r.ev_pkt, window_end=start + 2 * win)
+        _check(p, oq, H, start + 2 * win)
+        assert p.n_pending > 0 and len(p.deliver) > 0
+        start += win
+    # no new batch: drain what is left in two windows
+    for w_end in (start + 3 * win, 2**63):
+        p = q.advance(window_end=w_end)
+        _check(p, oq, H, w_end)
+    assert p.n_pending == 0 and p.next_time == 2**64 - 1
+
+
+def test_empty_queues_and_empty_batch(engine):
+    from shadow_amd.equeue import EventQueues
+    q = EventQueues(engine, 5)
+    p = q.advance(window_end=10)
+    assert p.n_pending == 0 and len(p.deliver) == 0 and p.off.tolist() == [0] * 6
+    p = q.advance(np.zeros(6, np.uint32), np.zeros(0, np.uint64), np.zeros(0, np.uint32),
+                  np.zeros(0, np.uint64), np.zeros(0, np.uint32), window_end=10)
+    assert p.n_pending == 0 and p.next_time == 2**64 - 1
+    # equal delivery times: (src, seq) decides, across batches
+    off = np.array([0, 0, 3, 3, 3, 3], np.uint32)
+    p = q.advance(off, np.array([20, 20, 30], np.uint64), np.array([1, 4, 0], np.uint32),
+                  np.array([7, 2, 9], np.uint64), np.array([0, 1, 2], np.uint32), window_end=15)
+    assert len(p.deliver) == 0 and p.n_pending == 3 and p.next_time == 20
+    p = q.advance(off, np.array([20, 25, 40], np.uint64), np.array([1, 0, 0], np.uint32),
+                  np.array([6, 1, 2], np.uint64), np.array([5, 6, 7], np.uint32), window_end=31)
+    # batch numbers count every batch handed over (the empty one above was batch 0)
+    assert p.events_for(1) == [(20, 1, 6, (2 << 32) | 5), (20, 1, 7, 1 << 32), (20, 4, 2, (1 << 32) | 1),
+                               (25, 0, 1, (2 << 32) | 6), (30, 0, 9, (1 << 32) | 2)]
+    assert p.n_pending == 1 and p.next_time == 40

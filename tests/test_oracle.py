@@ -295,3 +295,20 @@ def test_relay_window_helpers():
     assert OR.next_window(1000, 10, 1000) is None
     assert OR.runahead(None, 5, 1_000_000) == 1_000_000
     assert OR.runahead(2_000_000, 5, 1_000_000) == 2_000_000
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_c_oracle_row_range_matches_full(seed):
+    """orc_shortest_paths_rows (the checker for C4 row slices) against the full build."""
+    rng = np.random.default_rng(300 + seed)
+    n = int(rng.integers(20, 200))
+    ids, s, d, l, p, directed = random_graph(rng, n, 0.08, bool(seed % 2), max_ms=20)
+    used = rng.permutation(n).astype(np.uint32)
+    code, lat, loss, _ = corc.routing(n, s, d, l, p, directed, used)
+    assert code == "OK"
+    for rb, re in ((0, 1), (3, 17), (n - 5, n)):
+        for variant in (corc.TIDY, corc.FAITHFUL):
+            c2, l2, p2, _ = corc.routing(n, s, d, l, p, directed, used, variant=variant, rows=(rb, re))
+            assert c2 == "OK"
+            assert np.array_equal(l2, lat[rb:re])
+            assert np.array_equal(p2.view(np.uint32), loss[rb:re].view(np.uint32))
