@@ -14,12 +14,14 @@ full table; the timed region includes that all-gather (strong scaling: the graph
 Side legs, each its own JSON object in the same line:
   * ``relay`` -- C5: one round of 100k hosts / 10M packets per step (stamp + loss draw + bucket
     by destination + per-destination sort), inputs resident in HBM.  At N > 1 the hosts are
-    sharded by id, every rank stamps its own sources, events are exchanged with one RCCL
-    all-to-all(v) and merged per destination (strong scaling: the round is fixed).
+    sharded by id, every rank stamps its own sources, and the engine exchanges the events over
+    its RCCL communicator and merges them per destination (strong scaling: the round is fixed).
   * ``c3`` (N = 1) -- the 10k-node sparse graph: label-correcting SSSP vs delta-stepping vs the
     blocked min-plus APSP, all bit-identical; the blocked kernel's VALU roofline.
   * ``c4`` -- the 50k-node graph, source rows sharded over the ranks, global-label SSSP
-    (delta-stepping) + RCCL all-gather of the 30 GB table.
+    (delta-stepping) + the engine's RCCL all-gather of the 30 GB table (on by default).
+  * ``routing_e2e`` / ``relay.e2e_host_buffers`` -- SURVEY 8(d)'s end-to-end figures (host
+    buffers in and out, PCIe included); ``relay.equeue`` -- relay + device event-queue merge.
 Rank 0 prints ONE JSON line.  Timing: barrier + device sync on both sides of exactly K steps,
 max over ranks.  The CPU baselines (rank 0, N = 1) time the C restatement of the reference
 (oracle/c) on bounded samples of the same workloads.
@@ -103,33 +105,32 @@ def prepare(eng, el):
     return n
 
 
+def run_rows(eng, algo, rb, re, lat, loss):
+    from shadow_amd import _native as N
+    err = N.Error()
+    N.check(eng.lib.shd_routing_run(eng.ctx, algo, rb, re, N.ptr(lat), N.ptr(loss), C.byref(err)),
+            "shd_routing_run", err)
+
+
 def sharded_build(eng, world, rank, n, algo, steps, warmup, keep=False, gather=True):
-    """Rows [rb, re) of an n x n build on this rank + all-gather (gather=False: the row shards
-    stay resident, SURVEY 8(e) "keep shards and gather on demand"); returns timings."""
+    """One step = the routing build of all n rows.  N = 1: every row on this GPU.  N > 1: this
+    rank's source rows, then (gather=True) the engine's RCCL all-gather of the table
+    (shd_routing_run_sharded) so every rank ends with all of it."""
     import torch
     from shadow_amd import _native as N
+    from shadow_amd import dist as D
     per = (n + world - 1) // world
-    rb, re = min(rank * per, n), min((rank + 1) * per, n)
-    rows = world * per if gather else per
-    full_lat = torch.empty((rows, n), dtype=torch.int64, device="cuda")
-    full_loss = torch.empty((rows, n), dtype=torch.float32, device="cuda")
-    if not gather:
-        rank_off = 0
-    else:
-        rank_off = rank * per
-    shard_lat = full_lat[rank_off:rank_off + per]
-    shard_loss = full_loss[rank_off:rank_off + per]
-    err = N.Error()
+    rb, re = D.shard_range(n, world, rank) if world > 1 else (0, n)
+    rows = world * per if (world > 1 and gather) else (re - rb)
+    lat = torch.empty((max(rows, 1), n), dtype=torch.int64, device="cuda")
+    loss = torch.empty((max(rows, 1), n), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
 
     def step():
-        if re > rb:
-            st = eng.lib.shd_routing_run(eng.ctx, algo, rb, re, N.ptr(shard_lat), N.ptr(shard_loss),
-                                         C.byref(err))
-            N.check(st, "shd_routing_run", err)
         if world > 1 and gather:
-            import torch.distributed as dist
-            dist.all_gather_into_tensor(full_lat, shard_lat)
-            dist.all_gather_into_tensor(full_loss, shard_loss)
+            D.routing_run_sharded(eng, algo, lat, loss)
+        elif re > rb:
+            run_rows(eng, algo, rb, re, lat, loss)
 
     for _ in range(warmup):
         step()
@@ -141,12 +142,12 @@ def sharded_build(eng, world, rank, n, algo, steps, warmup, keep=False, gather=T
         infos.append(eng.last_info())
     barrier_sync(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
-    out = dict(dt=dt, ms_per_step=dt / steps * 1e3, rows=re - rb, infos=infos)
+    out = dict(dt=dt, ms_per_step=dt / steps * 1e3, rows=re - rb, rb=rb, infos=infos)
     if keep:
-        out["lat"] = full_lat[:n].cpu().numpy().view(np.uint64)
-        out["loss"] = full_loss[:n].cpu().numpy()
-    del full_lat, full_loss, shard_lat, shard_loss
-    torch.cuda.empty_cache()
+        k = n if (world == 1 or gather) else 0
+        out["lat"] = lat[:k].cpu().numpy().view(np.uint64)
+        out["loss"] = loss[:k].cpu().numpy()
+    out["lat_dev"], out["loss_dev"] = lat, loss
     return out
 
 
@@ -156,6 +157,7 @@ def routing_leg(eng, world, rank, steps, warmup):
     el = synth.complete_graph(1000, 1)
     n = prepare(eng, el)
     r = sharded_build(eng, world, rank, n, N.ALGO_AUTO, steps, warmup, keep=True)
+    del r["lat_dev"], r["loss_dev"]
     info = r["infos"][-1]
     kernel_ms = max_over_ranks(float(np.mean([i["ms_main"] for i in r["infos"]])), world)
     ops_per_launch = 2.0 * r["rows"] * info["arcs"]      # one add + one min per arc per source row
@@ -165,7 +167,61 @@ def routing_leg(eng, world, rank, steps, warmup):
     return r
 
 
-def c3_leg(eng, reps=2):
+def routing_e2e(eng, el, reps=5):
+    """SURVEY 8(d)'s end-to-end figure: shd_routing_build from the host graph arrays (validation,
+    CSR build, H2D) to the whole table in pinned host memory (D2H)."""
+    import torch
+    from shadow_amd import _native as N
+    from shadow_amd.routing import NetworkGraph
+    g = NetworkGraph(el.node_ids, el.src, el.dst, el.latency_ns, el.packet_loss, el.directed)
+    n = g.n_nodes
+    used = np.arange(n, dtype=np.uint32)
+    lat = torch.empty((n, n), dtype=torch.int64).pin_memory()
+    loss = torch.empty((n, n), dtype=torch.float32).pin_memory()
+    cg = g._cgraph()
+    err = N.Error()
+
+    def once():
+        N.check(eng.lib.shd_routing_build(eng.ctx, C.byref(cg), N.ptr(used), n, N.ROUTE_SHORTEST, N.ALGO_AUTO,
+                                          0, n, C.c_void_p(lat.data_ptr()), C.c_void_p(loss.data_ptr()),
+                                          C.byref(err)), "shd_routing_build", err)
+    once()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        once()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"ms_per_build": ms, "node_pairs_per_s": n * n / (ms * 1e-3),
+            "what": "shd_routing_build: host graph arrays -> validation + CSR + H2D -> build -> D2H of the "
+                    "12 MB table into pinned host memory"}
+
+
+def sssp_roofline(n, arcs, V, ms):
+    """SURVEY 8(d) sparse-SSSP roofline: n * (E * 8 + V * 12) bytes per build over HBM."""
+    b = float(n) * (arcs * 8 + V * 12)
+    ach = b / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "work": "n * (E * 8 + V * 12) B: one 8-byte label read per arc relaxation + the 12-byte table write "
+                    "(SURVEY 8(d))", "bytes": b}
+
+
+def cpu_rows_baseline(el, rows, n_total, what):
+    """Faithful C restatement (per-source heap Dijkstra + Vec::contains filter + HashMap) on a
+    contiguous sample of source rows, all host cores; extrapolated to the whole build."""
+    from oracle import corc
+    used = np.arange(el.n_nodes, dtype=np.uint32)
+    threads = corc.max_threads()
+    t0 = time.perf_counter()
+    code, lat, loss, _ = corc.routing(el.n_nodes, el.src, el.dst, el.latency_ns, el.packet_loss, el.directed,
+                                      used, variant=corc.FAITHFUL, threads=threads, rows=rows)
+    dt = time.perf_counter() - t0
+    k = rows[1] - rows[0]
+    full_s = dt * n_total / k
+    return dict(value=n_total * n_total / full_s, unit="node-pairs/s", cores=threads, kind="port",
+                sample=f"{what}: source rows {rows[0]}-{rows[1] - 1} ({k} of {n_total}) in {dt:.2f} s, "
+                       f"extrapolated x{n_total / k:.0f} (faithful: heap Dijkstra + Vec::contains + HashMap)"), lat, loss
+
+
+def c3_leg(eng, reps=2, cpu=True):
     """C3 (10k-node sparse, BA m=3): the three algorithms on the same rows, bit-identical."""
     import torch
     from shadow_amd import _native as N
@@ -174,15 +230,15 @@ def c3_leg(eng, reps=2):
     n = prepare(eng, el)
     lat = torch.empty((n, n), dtype=torch.int64, device="cuda")
     loss = torch.empty((n, n), dtype=torch.float32, device="cuda")
-    err = N.Error()
     res, ref = {}, None
+    arcs = 0
     for name, algo in (("sssp", N.ALGO_SSSP), ("delta", N.ALGO_DELTA), ("blocked", N.ALGO_BLOCKED)):
         infos = []
         for _ in range(reps):
-            N.check(eng.lib.shd_routing_run(eng.ctx, algo, 0, n, N.ptr(lat), N.ptr(loss), C.byref(err)),
-                    "c3 run", err)
+            run_rows(eng, algo, 0, n, lat, loss)
             infos.append(eng.last_info())
         i = infos[-1]
+        arcs = int(i["arcs"])
         h = (int(lat.view(torch.int64).sum().item()), int(loss.view(torch.int32).to(torch.int64).sum().item()))
         ref = ref or h
         res[name] = dict(ms_total=i["ms_total"], ms_main=i["ms_main"], identical_to_sssp=h == ref)
@@ -193,18 +249,27 @@ def c3_leg(eng, reps=2):
                              roofline={"bound": "valu", "achieved": ach, "peak": VALU_PEAK_TOPS,
                                        "unit": "Tops/s", "frac": ach / VALU_PEAK_TOPS,
                                        "work": "2 V^3 int ops (add + min) of the min-plus closure"})
+        else:
+            res[name]["roofline"] = sssp_roofline(n, arcs, n, i["ms_main"])
     best = min(v["ms_total"] for v in res.values())
+    out = dict(workload="C3: 10k-node Barabasi-Albert m=3 + self-loops, all 10k rows",
+               nodes=n, arcs=arcs, node_pairs_per_s=n * n / (best * 1e-3), algorithms=res)
+    if cpu:
+        cb, clat, closs = cpu_rows_baseline(el, (0, 256), n, "C3")
+        cb["bit_exact_vs_gpu"] = bool(np.array_equal(clat, lat[:256].cpu().numpy().view(np.uint64)) and
+                                      np.array_equal(closs.view(np.uint32), loss[:256].cpu().numpy().view(np.uint32)))
+        out["cpu_baseline"] = cb
     del lat, loss
     torch.cuda.empty_cache()
-    return dict(workload="C3: 10k-node Barabasi-Albert m=3 + self-loops, all 10k rows",
-                nodes=n, arcs=int(eng.last_info()["arcs"]), node_pairs_per_s=n * n / (best * 1e-3),
-                algorithms=res)
+    return out
 
 
-def c4_leg(eng, world, rank, steps, gather=False):
-    """C4: the 50k-node table is 30 GB (12 B/pair).  At N > 1 the row shards stay resident by
-    default: an all-gather would move 26 GB into every GPU (minutes over xGMI) per build, and the
-    relay needs only its source hosts' rows.  --c4-gather times the full all-gather as well."""
+def c4_leg(eng, world, rank, steps, gather=True, cpu=True):
+    """C4: the 50k-node BA m=4 graph, all 50k source rows (global-label delta-stepping).  N > 1:
+    rows sharded over the ranks, then the engine's RCCL all-gather of the 30 GB table (BASELINE
+    config 4: "+ RCCL all-gather"); every rank ends with the whole table.  Over xGMI that moves
+    (N-1)/N x 30 GB into every GPU: ~26 GB at N = 8, tens of ms at the links' rate."""
+    import torch
     from shadow_amd import _native as N
     from shadow_amd import synth
     el = synth.barabasi_albert(50_000, 4, 3)
@@ -214,11 +279,22 @@ def c4_leg(eng, world, rank, steps, gather=False):
     kernel_ms = max_over_ranks(float(np.mean([i["ms_main"] for i in r["infos"]])), world)
     how = ("source rows sharded + RCCL all-gather of the table" if gather else
            "source rows sharded, shards resident (no all-gather)" if world > 1 else "1 GPU, whole table")
-    return dict(workload="C4: 50k-node Barabasi-Albert m=4 + self-loops, all 50k rows, global-label "
-                         "delta-stepping SSSP, " + how,
-                nodes=n, arcs=int(r["infos"][-1]["arcs"]), steps=steps, ms_per_build=r["ms_per_step"],
-                sssp_kernel_ms_per_rank=kernel_ms, value=n * n / (r["ms_per_step"] * 1e-3),
-                unit="node-pairs/s", scaling="strong", all_gather=bool(gather))
+    arcs = int(r["infos"][-1]["arcs"])
+    out = dict(workload="C4: 50k-node Barabasi-Albert m=4 + self-loops, all 50k rows, global-label "
+                        "delta-stepping SSSP, " + how,
+               nodes=n, arcs=arcs, steps=steps, ms_per_build=r["ms_per_step"],
+               sssp_kernel_ms_per_rank=kernel_ms, value=n * n / (r["ms_per_step"] * 1e-3),
+               unit="node-pairs/s", scaling="strong", all_gather=bool(gather),
+               roofline=sssp_roofline(r["rows"], arcs, n, kernel_ms))
+    if cpu and rank == 0 and world == 1:
+        cb, clat, closs = cpu_rows_baseline(el, (0, 64), n, "C4")
+        lat, loss = r["lat_dev"], r["loss_dev"]
+        cb["bit_exact_vs_gpu"] = bool(np.array_equal(clat, lat[:64].cpu().numpy().view(np.uint64)) and
+                                      np.array_equal(closs.view(np.uint32), loss[:64].cpu().numpy().view(np.uint32)))
+        out["cpu_baseline"] = cb
+    del r
+    torch.cuda.empty_cache()
+    return out
 
 
 def relay_inputs():
@@ -229,23 +305,30 @@ def relay_inputs():
     return H, P, start, runahead, b, synth.c5_host_nodes(H, 1000), synth.host_rng_states(H, 1)
 
 
-def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=False):
+def _dev(a, dt):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()
+
+
+def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=False, inputs=None):
     import torch
     from shadow_amd import _native as N
     from shadow_amd import dist as D
-    H, P, start, runahead, b, host_node, rng0 = relay_inputs()
+    H, P, start, runahead, b, host_node, rng0 = inputs or relay_inputs()
     nid0 = np.zeros(H, np.uint64)
-    N.check(eng.lib.shd_relay_setup(eng.ctx, H, N.ptr(host_node), 1000, N.ptr(lat_table),
-                                    N.ptr(loss_table), N.ptr(rng0), N.ptr(nid0)), "relay_setup")
+    rd = (start + runahead, start + 10**12, 0)
+    if world == 1:
+        N.check(eng.lib.shd_relay_setup(eng.ctx, H, N.ptr(host_node), 1000, N.ptr(lat_table),
+                                        N.ptr(loss_table), N.ptr(rng0), N.ptr(nid0)), "relay_setup")
+    else:
+        rel = D.ShardedRelay(eng, host_node, rng0, nid0, lat_table, loss_table)
     # per-path packet counters: the reference only reads them in log_packet_counts, which is
     # never called, and the CPU baseline does not keep them either -> off in both legs; the
     # cost with them on is reported separately (counters_on_ms_per_round)
     N.check(eng.lib.shd_relay_set_counters(eng.ctx, 1 if counters else 0), "set_counters")
-    dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()  # noqa: E731
-    rd = (start + runahead, start + 10**12, 0)
     if world == 1:
-        d_off, d_time = dev(b.src_off, np.int32), dev(b.send_time, np.int64)
-        d_dst, d_pay = dev(b.dst_host, np.int32), dev(b.payload, np.int32)
+        d_off, d_time = _dev(b.src_off, np.int32), _dev(b.send_time, np.int64)
+        d_dst, d_pay = _dev(b.dst_host, np.int32), _dev(b.payload, np.int32)
         st = torch.empty(P, dtype=torch.uint8, device="cuda")
         ev_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
         ev_deliver = torch.empty(P, dtype=torch.int64, device="cuda")
@@ -263,18 +346,17 @@ def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=F
                     "relay_round_device")
             return out.n_sent
     else:
-        # hosts sharded by id: this rank stamps its own sources; all-to-all + merge per round
-        lo, hi = D.host_shard(H, world, rank)
+        # hosts sharded by id: this rank's sources; the engine exchanges + merges the events
+        lo, hi = rel.lo, rel.hi
         a, e = int(b.src_off[lo]), int(b.src_off[hi])
-        off = np.zeros(H + 1, np.uint32)
-        off[lo + 1:hi + 1] = b.src_off[lo + 1:hi + 1] - a
-        off[hi + 1:] = e - a
-        d_off, d_time = dev(off, np.int32), dev(b.send_time[a:e], np.int64)
-        d_dst, d_pay = dev(b.dst_host[a:e], np.int32), dev(b.payload[a:e], np.int32)
-        ops = D.DeviceOps(eng, torch.device("cuda", torch.cuda.current_device()))
+        d_off = _dev((b.src_off[lo:hi + 1] - b.src_off[lo]).astype(np.uint32), np.int32)
+        d_time, d_dst = _dev(b.send_time[a:e], np.int64), _dev(b.dst_host[a:e], np.int32)
+        d_pay = _dev(b.payload[a:e], np.int32)
+        st = torch.empty(max(e - a, 1), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
 
         def step():
-            return D.sharded_relay_round(ops, H, d_off, d_time, d_dst, d_pay, rd)["n_sent"]
+            return rel.round_device(d_off, d_time, d_dst, d_pay, rd, st).n_sent
 
     for _ in range(warmup):
         step()
@@ -287,8 +369,54 @@ def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=F
     pipe = C.c_int32(0)
     N.check(eng.lib.shd_relay_last_pipeline(eng.ctx, C.byref(pipe)), "last_pipeline")
     return dict(H=H, P=P, dt=dt, ms_per_step=dt / steps * 1e3, n_sent=int(n_sent), batch=b,
-                pipeline=int(pipe.value),
-                host_node=host_node, rng0=rng0, start=start)
+                pipeline=int(pipe.value), host_node=host_node, rng0=rng0, start=start, rd=rd)
+
+
+def relay_check_and_e2e(eng, rl, lat_table, loss_table, reps=3):
+    """One round from the setup state through shd_relay_round with pinned host buffers (the
+    call INTEGRATION.md's manager makes: staged batch in, events out, PCIe both ways), timed,
+    and its statuses and events compared with the C restatement's."""
+    import torch
+    from oracle import corc
+    from shadow_amd import _native as N
+    b, H, P = rl["batch"], rl["H"], rl["P"]
+    pin = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).pin_memory()  # noqa: E731
+    h_off, h_time = pin(b.src_off, np.int32), pin(b.send_time, np.int64)
+    h_dst, h_pay = pin(b.dst_host, np.int32), pin(b.payload, np.int32)
+    st = torch.empty(P, dtype=torch.uint8).pin_memory()
+    ev_off = torch.empty(H + 1, dtype=torch.int32).pin_memory()
+    ev_d = torch.empty(P, dtype=torch.int64).pin_memory()
+    ev_s = torch.empty(P, dtype=torch.int32).pin_memory()
+    ev_q = torch.empty(P, dtype=torch.int64).pin_memory()
+    ev_p = torch.empty(P, dtype=torch.int32).pin_memory()
+    hp = lambda t: t.data_ptr()  # noqa: E731
+    batch = N.Batch(P, hp(h_off), hp(h_time), hp(h_dst), hp(h_pay), None)
+    out = N.RelayOut(hp(st), hp(ev_off), hp(ev_d), hp(ev_s), hp(ev_q), hp(ev_p), 0, 0, 0)
+    rnd = N.Round(*rl["rd"])
+
+    def setup():
+        N.check(eng.lib.shd_relay_setup(eng.ctx, H, N.ptr(rl["host_node"]), 1000, N.ptr(lat_table),
+                                        N.ptr(loss_table), N.ptr(rl["rng0"]), N.ptr(np.zeros(H, np.uint64))),
+                "relay_setup")
+    setup()
+    N.check(eng.lib.shd_relay_round(eng.ctx, C.byref(batch), C.byref(rnd), C.byref(out)), "shd_relay_round")
+    ns = out.n_sent
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, rl["host_node"], lat_table, loss_table,
+                         rl["rng0"].copy(), np.zeros(H, np.uint64), *rl["rd"], threads=corc.max_threads())
+    ev = o["events"]
+    ok = (np.array_equal(st.numpy(), o["status"]) and np.array_equal(ev_off.numpy().view(np.uint32), ev["off"])
+          and np.array_equal(ev_d.numpy()[:ns].view(np.uint64), ev["deliver"])
+          and np.array_equal(ev_s.numpy()[:ns].view(np.uint32), ev["src"])
+          and np.array_equal(ev_q.numpy()[:ns].view(np.uint64), ev["seq"])
+          and np.array_equal(ev_p.numpy()[:ns].view(np.uint32), ev["pkt"])
+          and (out.min_deliver, out.min_latency, ns) == (o["min_deliver"], o["min_latency"], o["n_sent"]))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        N.check(eng.lib.shd_relay_round(eng.ctx, C.byref(batch), C.byref(rnd), C.byref(out)), "shd_relay_round")
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    moved = (H + 1) * 4 + P * (8 + 4 + 4) + P + (H + 1) * 4 + ns * 24
+    return ok, {"ms_per_round": ms, "packets_per_s": P / (ms * 1e-3), "pcie_bytes": moved,
+                "what": "shd_relay_round with pinned host buffers: staged batch H2D, round, statuses + events D2H"}
 
 
 def cpu_baseline_routing(el, budget_s=8.0):
@@ -317,8 +445,7 @@ def cpu_baseline_relay(rl, lat_table, loss_table, budget_s=8.0):
         rng = rl["rng0"].copy()
         nid = np.zeros(rl["H"], np.uint64)
         corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, rl["host_node"], lat_table,
-                         loss_table, rng, nid, rl["start"] + 10**6, rl["start"] + 10**12, 0,
-                         threads=threads, want_events=False)
+                         loss_table, rng, nid, *rl["rd"], threads=threads, want_events=False)
         reps += 1
         if time.perf_counter() - t0 > budget_s or reps >= 5:
             break
@@ -327,6 +454,50 @@ def cpu_baseline_relay(rl, lat_table, loss_table, budget_s=8.0):
                 sample=f"{reps} full C5 rounds (per-packet send_packet restatement, per-destination "
                        f"mutex + binary-heap push, OpenMP over source hosts)")
 
+
+def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4):
+    """a14: the relay round plus the merge of its events into the device-resident destination
+    queues and the pop of the next window (shd_equeue_advance), round after round on C5 (1 ms
+    windows, 1-300 ms paths: events stay pending for many rounds)."""
+    import torch
+    from shadow_amd import _native as N
+    H, P = rl["H"], rl["P"]
+    N.check(eng.lib.shd_relay_setup(eng.ctx, H, N.ptr(rl["host_node"]), 1000, N.ptr(lat_table), N.ptr(loss_table),
+                                    N.ptr(rl["rng0"]), N.ptr(np.zeros(H, np.uint64))), "relay_setup")
+    N.check(eng.lib.shd_equeue_setup(eng.ctx, H), "equeue_setup")
+    st = torch.empty(P, dtype=torch.uint8, device="cuda")
+    ev = [torch.empty(H + 1, dtype=torch.int32, device="cuda"), torch.empty(P, dtype=torch.int64, device="cuda"),
+          torch.empty(P, dtype=torch.int32, device="cuda"), torch.empty(P, dtype=torch.int64, device="cuda"),
+          torch.empty(P, dtype=torch.int32, device="cuda")]
+    out = N.RelayOut(N.ptr(st).value, *(N.ptr(t).value for t in ev), 0, 0, 0)
+    qo = N.EqueueOut()
+    start = rl["start"]
+    t_relay = t_adv = 0.0
+    pops = pend = 0
+    b = rl["batch"]
+    d = [_dev(b.src_off, np.int32), _dev(b.send_time, np.int64), _dev(b.dst_host, np.int32),
+         _dev(b.payload, np.int32)]
+    t_base = d[1].clone()
+    for k in range(rounds):
+        d[1].copy_(t_base + k * 10**6)   # the same sends, one window later each round
+        batch = N.Batch(P, *(N.ptr(t).value for t in d), None)
+        rnd = N.Round(start + 10**6, start + 10**12, 0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        N.check(eng.lib.shd_relay_round_device(eng.ctx, C.byref(batch), C.byref(rnd), C.byref(out)), "relay")
+        t1 = time.perf_counter()
+        N.check(eng.lib.shd_equeue_advance(eng.ctx, C.byref(out), start + 2 * 10**6, C.byref(qo)), "advance")
+        t2 = time.perf_counter()
+        if k >= rounds - timed:
+            t_relay += t1 - t0
+            t_adv += t2 - t1
+            pops += qo.n_popped
+            pend += qo.n_pending
+        start += 10**6
+    return {"workload": "C5 rounds: relay + shd_equeue_advance (merge into the pending destination queues, pop "
+                        "the next 1 ms window)", "rounds": rounds, "timed_rounds": timed,
+            "relay_ms_per_round": t_relay / timed * 1e3, "advance_ms_per_round": t_adv / timed * 1e3,
+            "popped_per_round": pops / timed, "pending_mean": pend / timed}
 
 
 def codel_leg(eng, steps=5, cpu=True):
@@ -456,11 +627,17 @@ def main():
     ap.add_argument("--no-c4", action="store_true")
     ap.add_argument("--no-codel", action="store_true")
     ap.add_argument("--no-tbucket", action="store_true")
-    ap.add_argument("--c4-gather", action="store_true")
+    ap.add_argument("--no-equeue", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--c4-no-gather", action="store_true")
     args = ap.parse_args()
     world, rank, local = dist_setup(args.gpus)
     from shadow_amd.routing import Engine
     eng = Engine(local)
+    if world > 1:   # the engine's own communicator: RCCL over xGMI, one rank per GPU
+        from shadow_amd import dist as D
+        D.comm_init_rccl(eng)
+    cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
 
     r = routing_leg(eng, world, rank, args.steps, args.warmup)
     value = args.steps * r["n"] ** 2 / r["dt"]
@@ -473,7 +650,8 @@ def main():
                                "graph + self-loops, 1000 used nodes",
                    "nodes": r["n"], "arcs": int(r["arcs"]), "arcs_after_prune": int(r["arcs_kept"]),
                    "algo": int(r["algo"]),
-                   "parallelism": f"source-row shards x{world} + RCCL all-gather" if world > 1 else "1 GPU"},
+                   "parallelism": (f"source-row shards x{world} + engine RCCL all-gather (shd_routing_run_sharded)"
+                                   if world > 1 else "1 GPU")},
         "roofline": {"bound": "valu", "achieved": r["achieved"], "peak": VALU_PEAK_TOPS,
                      "unit": "Tops/s", "frac": r["achieved"] / VALU_PEAK_TOPS,
                      "traffic": load_pmc("routing"),
@@ -481,13 +659,16 @@ def main():
                      "work": "2 int ops (add, min) per arc relaxation per source row = 2*n*A "
                              "(A = arcs before pruning: the reference's Dijkstra work)"},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if cpu:
         cb, lat_cpu = cpu_baseline_routing(r["el"])
         cb["bit_exact_vs_gpu"] = bool(np.array_equal(lat_cpu, r["lat"]))
         res["cpu_baseline"] = cb
+    if world == 1 and not args.no_e2e:
+        res["routing_e2e"] = routing_e2e(eng, r["el"])
     if not args.no_relay:
         ks = args.relay_steps or max(3, args.steps // 2)
-        rl = relay_leg(eng, world, rank, ks, min(args.warmup, 2), r["lat"], r["loss"])
+        inputs = relay_inputs()
+        rl = relay_leg(eng, world, rank, ks, min(args.warmup, 2), r["lat"], r["loss"], inputs=inputs)
         pv = ks * rl["P"] / rl["dt"]
         ms = rl["ms_per_step"]
         bytes_round = RELAY_BYTES_PER_PACKET * rl["P"] + RELAY_BYTES_PER_HOST * rl["H"]
@@ -501,25 +682,33 @@ def main():
                "config": {"workload": "C5: 100k hosts on the C2 table, 10M packets per round "
                                       "(src uniform, dst != src, 20% ACK / 60% 1448 B / 20% U[1,1448])",
                           "hosts": rl["H"], "packets": rl["P"],
-                          "parallelism": (f"hosts sharded x{world}, RCCL all-to-all(v) + device "
-                                          f"k-way merge") if world > 1 else "1 GPU"},
+                          "parallelism": (f"hosts sharded x{world}: engine RCCL sizing all-to-all + grouped "
+                                          f"record exchange + device merge (shd_relay_round_sharded)")
+                          if world > 1 else "1 GPU"},
                "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ach / HBM_PEAK_GBS, "traffic": load_pmc("relay"),
                             "work": "84 B/packet + 80 B/host algorithmic (SURVEY 8(d)), whole round"}}
         if world == 1:
-            rl_c = relay_leg(eng, world, rank, max(2, ks // 3), 1, r["lat"], r["loss"], counters=True)
+            rl_c = relay_leg(eng, world, rank, max(2, ks // 3), 1, r["lat"], r["loss"], counters=True,
+                             inputs=inputs)
             rel["counters_on_ms_per_round"] = rl_c["ms_per_step"]
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            ok, e2e = relay_check_and_e2e(eng, rl, r["lat"], r["loss"])
+            rel["e2e_host_buffers"] = e2e
+            rel["bit_exact_vs_cpu"] = bool(ok)
+        if cpu:
             rel["cpu_baseline"] = cpu_baseline_relay(rl, r["lat"], r["loss"])
+            rel["cpu_baseline"]["bit_exact_vs_gpu"] = rel["bit_exact_vs_cpu"]
+        if world == 1 and not args.no_equeue:
+            rel["equeue"] = equeue_leg(eng, rl, r["lat"], r["loss"])
         res["relay"] = rel
     if world == 1 and not args.no_c3:
-        res["c3"] = c3_leg(eng)
+        res["c3"] = c3_leg(eng, cpu=cpu)
     if not args.no_c4:
-        res["c4"] = c4_leg(eng, world, rank, args.c4_steps, gather=args.c4_gather)
+        res["c4"] = c4_leg(eng, world, rank, args.c4_steps, gather=not args.c4_no_gather, cpu=cpu)
     if world == 1 and not args.no_codel:
-        res["codel"] = codel_leg(eng, cpu=not args.no_cpu_baseline)
+        res["codel"] = codel_leg(eng, cpu=cpu)
     if world == 1 and not args.no_tbucket:
-        res["tbucket"] = tbucket_leg(eng, cpu=not args.no_cpu_baseline)
+        res["tbucket"] = tbucket_leg(eng, cpu=cpu)
     if rank == 0:
         print(json.dumps(res), flush=True)
     eng.close()
