@@ -42,11 +42,18 @@ __device__ __forceinline__ uint64_t ld_lab(const uint64_t* p) {
                              GLAB ? __HIP_MEMORY_SCOPE_AGENT : __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// delta-stepping bucket of a latency for the global-label kernel's LDS bucket bytes: any
+// estimate works (it only orders the expansions), so a float multiply, saturating at 255
+__device__ __forceinline__ uint8_t bucket_of(uint32_t lat, float inv_delta) {
+    return (uint8_t)fminf(255.0f, (float)lat * inv_delta);
+}
+
 template <int G, int R, bool CACHE, bool GLAB>
 __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* lab, uint32_t* bits,
                                            uint32_t scratch, const uint2* rng, const uint32_t* __restrict__ abeg,
                                            const uint32_t* __restrict__ aend,
-                                           const uint4* __restrict__ arcs, bool& ovf, bool& dirty) {
+                                           const uint4* __restrict__ arcs, bool& ovf, bool& dirty,
+                                           uint8_t* bkt, float inv_delta) {
     const uint64_t ku = ld_lab<GLAB>(&lab[u]);
     const uint32_t lu = key_lat(ku);
     const float qu = one_minus(key_loss(ku));
@@ -99,12 +106,104 @@ __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* la
             dirty = true;
 #pragma unroll
             for (int i = 0; i < R; ++i)
-                if ((imp >> i) & 1u) atomicOr(&bits[a[i].x >> 5], 1u << (a[i].x & 31));
+                if ((imp >> i) & 1u) {
+                    if (bkt) bkt[a[i].x] = bucket_of(key_lat(cand[i]), inv_delta);
+                    atomicOr(&bits[a[i].x >> 5], 1u << (a[i].x & 31));
+                }
         }
     }
 }
 
 constexpr uint32_t kQCap = 64;   // per-wave expansion queue (+32 overflow slots)
+constexpr uint32_t kFlatWords = 257;   // per-wave scratch of expand_flat: pre[65], beg, lat, q [64]
+constexpr int kFlatR = 8;              // arcs per lane per round of expand_flat
+
+// Global labels: expand up to 64 queued nodes at once, edge-parallel.  The nodes' arc ranges
+// are laid end to end (a wave prefix sum of the degrees) and every lane takes kFlatR arcs of
+// the concatenation, so a round of the wave issues 64 x kFlatR independent arc loads, label
+// reads and atomics -- one chain of global round trips per ~512 relaxations instead of one per
+// node group.  The owner of an arc is the last node whose prefix is <= its position.  BA and
+// internet-like graphs mix hubs and low-degree nodes; this keeps every lane busy on both.
+__device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint32_t lane, uint64_t* lab,
+                                            uint32_t* bits, const uint32_t* __restrict__ abeg,
+                                            const uint32_t* __restrict__ aend, const uint4* __restrict__ arcs,
+                                            uint32_t* fx, bool& ovf, bool& dirty, uint8_t* bkt, float inv_delta) {
+    uint32_t* pre = fx;          // [65]
+    uint32_t* beg = fx + 65;     // [64]
+    uint32_t* nl = fx + 129;     // [64] latency of the node's label
+    uint32_t* nq = fx + 193;     // [64] q = 1f32 - loss of the node's label
+    for (uint32_t c0 = 0; c0 < qn; c0 += 64) {
+        const uint32_t cn = min(64u, qn - c0);
+        uint32_t deg = 0, b = 0;
+        uint64_t ku = kKeyInf;
+        if (lane < cn) {
+            const uint32_t u = q[c0 + lane];
+            b = abeg[u];
+            deg = aend[u] - b;
+            ku = ld_lab<true>(&lab[u]);
+        }
+        uint32_t incl = deg;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t T = __shfl(incl, 63);
+        pre[lane] = incl - deg;
+        beg[lane] = b;
+        nl[lane] = key_lat(ku);
+        nq[lane] = __float_as_uint(one_minus(key_loss(ku)));
+        if (lane == 0) pre[64] = T;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t t0 = 0; t0 < T; t0 += 64 * kFlatR) {
+            uint4 a[kFlatR];
+            uint32_t lu[kFlatR];
+            float qu[kFlatR];
+            bool live[kFlatR];
+#pragma unroll
+            for (int r = 0; r < kFlatR; ++r) {
+                const uint32_t t = t0 + r * 64 + lane;
+                live[r] = t < T;
+                const uint32_t tc = min(t, T - 1);   // dead slots load the last arc (in bounds)
+                uint32_t lo = 0, hi = 64;   // last j with pre[j] <= tc (zero-degree nodes are skipped)
+#pragma unroll
+                for (int it = 0; it < 6; ++it) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pre[mid] <= tc) lo = mid; else hi = mid;
+                }
+                lu[r] = nl[lo];
+                qu[r] = __uint_as_float(nq[lo]);
+                a[r] = arcs[beg[lo] + (tc - pre[lo])];
+            }
+            uint64_t cand[kFlatR], cur[kFlatR];
+#pragma unroll
+            for (int r = 0; r < kFlatR; ++r) {
+                const uint32_t cl = lu[r] + a[r].y;
+                const bool ok = live[r] && a[r].y != kLat32Inf && cl >= lu[r] && cl != kLat32Inf;
+                if (live[r] && a[r].y != kLat32Inf && !ok) ovf = true;   // leaves u32: wide rerun
+                cand[r] = ok ? pack_key(cl, fold_q(qu[r], __uint_as_float(a[r].z))) : kKeyInf;
+            }
+#pragma unroll
+            for (int r = 0; r < kFlatR; ++r) cur[r] = cand[r] != kKeyInf ? ld_lab<true>(&lab[a[r].x]) : 0ull;
+#pragma unroll
+            for (int r = 0; r < kFlatR; ++r) {
+                // labels only decrease: a candidate not below the label read now cannot improve it
+                if (cand[r] < cur[r]) {
+                    const uint64_t old =
+                        atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[r].x]), (unsigned long long)cand[r]);
+                    if (cand[r] < old) {
+                        dirty = true;
+                        if (bkt) bkt[a[r].x] = bucket_of(key_lat(cand[r]), inv_delta);
+                        atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
 
 // One source row: init, sweeps until nothing improves, emit the used columns.
 template <int BLOCK, int G, int R, bool CACHE, bool GLAB>
@@ -117,7 +216,9 @@ __device__ __forceinline__ void sssp_row(
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
-    uint32_t seed_stride) {
+    uint32_t seed_stride, uint8_t* bkt, uint32_t* flat) {
+    // bkt (global labels + delta-stepping): per node, the bucket of the latency that last
+    // activated it, in LDS, so choosing a sweep's nodes reads no global label
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
     const uint32_t W = (V + 31) >> 5;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -125,6 +226,11 @@ __device__ __forceinline__ void sssp_row(
     uint32_t* q = wq + wave * (kQCap + 32);
     const uint32_t src = used[row];
     const bool use_delta = delta != kLat32Inf;
+    const float inv_delta = use_delta ? 1.0f / (float)delta : 0.0f;
+    // the ordering key of an active node: its bucket byte, or its label's latency
+    auto act_key = [&](uint32_t v) -> uint32_t {
+        return bkt ? (uint32_t)bkt[v] : key_lat(ld_lab<GLAB>(&lab[v]));
+    };
 
     // seed_lat (blocked path): labels start at (final latency, +inf loss) so only the loss
     // part can still improve, and only through tight arcs
@@ -151,6 +257,7 @@ __device__ __forceinline__ void sssp_row(
     if (tid == 0) {
         if (!GLAB) lab[src] = 0;  // PathProperties::default() = (0 ns, 0.0)
         bits[src >> 5] = 1u << (src & 31);
+        if (bkt) bkt[src] = 0;
     }
     bool ovf = false;
     uint32_t expanded = 0, sweeps = 0;
@@ -166,14 +273,14 @@ __device__ __forceinline__ void sssp_row(
             for (uint32_t widx = wave; widx < W; widx += NW) {
                 const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (word == 0) continue;
-                if (lane < 32 && ((word >> lane) & 1u)) m = min(m, key_lat(ld_lab<GLAB>(&lab[widx * 32 + lane])));
+                if (lane < 32 && ((word >> lane) & 1u)) m = min(m, act_key(widx * 32 + lane));
             }
             for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
             if (lane == 0 && m != kLat32Inf) atomicMin(&ctl[1], m);
             __syncthreads();
             const uint32_t lo = ctl[1];
             if (lo == kLat32Inf) break;  // no active node anywhere
-            thr = lo + delta < lo ? kLat32Inf - 1 : lo + delta;
+            thr = bkt ? lo : lo + delta < lo ? kLat32Inf - 1 : lo + delta;
         }
         bool dirty = false;
         uint32_t qn = 0;  // wave-uniform queue length
@@ -183,7 +290,7 @@ __device__ __forceinline__ void sssp_row(
                 const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (word != 0) {  // wave-uniform
                     bool sel = lane < 32 && ((word >> lane) & 1u);
-                    if (use_delta && sel) sel = key_lat(ld_lab<GLAB>(&lab[widx * 32 + lane])) <= thr;
+                    if (use_delta && sel) sel = act_key(widx * 32 + lane) <= thr;
                     const uint32_t mask = (uint32_t)__ballot(sel);
                     if (mask) {
                         // words are owned by one wave; other waves only set bits: clearing is exact
@@ -198,10 +305,16 @@ __device__ __forceinline__ void sssp_row(
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 expanded += qn;
-                for (uint32_t t = 0; t < qn; t += NG) {
-                    const uint32_t qi = t + grp;
-                    if (qi < qn)
-                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs, ovf, dirty);
+                if (GLAB && flat) {
+                    expand_flat(q, qn, lane, lab, bits, abeg, aend, arcs, flat + wave * kFlatWords, ovf, dirty,
+                                bkt, inv_delta);
+                } else {
+                    for (uint32_t t = 0; t < qn; t += NG) {
+                        const uint32_t qi = t + grp;
+                        if (qi < qn)
+                            relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
+                                                          ovf, dirty, bkt, inv_delta);
+                    }
                 }
                 qn = 0;
                 __builtin_amdgcn_wave_barrier();
@@ -271,7 +384,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     sssp_row<BLOCK, G, R, CACHE, false>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
                                         row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
                                         diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
-                                        delta, stats, seed_lat, seed_stride);
+                                        delta, stats, seed_lat, seed_stride, nullptr, nullptr);
 }
 
 // Kernel 1b: labels in global memory, for graphs whose labels do not fit the LDS (C4: 50k
@@ -286,18 +399,21 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     const float* __restrict__ diag_loss, uint64_t* __restrict__ out_lat,
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
-    unsigned long long* __restrict__ stats, uint64_t* __restrict__ glab) {
+    unsigned long long* __restrict__ stats, uint64_t* __restrict__ glab, uint32_t use_bkt, uint32_t use_flat) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
     uint32_t* ctl = bits + W;
     uint32_t* wq = ctl + 4;
+    uint32_t* flat = use_flat ? wq + (BLOCK / 64) * (kQCap + 32) : nullptr;
+    uint8_t* bkt = use_bkt ? reinterpret_cast<uint8_t*>(wq + (BLOCK / 64) * (kQCap + 32 + (use_flat ? kFlatWords : 0)))
+                           : nullptr;
     uint64_t* lab = glab + (size_t)blockIdx.x * V;
     for (uint32_t row = row_begin + blockIdx.x; row < row_end; row += gridDim.x) {
         sssp_row<BLOCK, G, R, false, true>(lab, bits, ctl, wq, nullptr, abeg, aend, arcs, V, used,
                                            n_used, row, (size_t)(row - row_begin) * n_used,
                                            diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
-                                           delta, stats, nullptr, 0);
+                                           delta, stats, nullptr, 0, bkt, flat);
         __syncthreads();   // the next row re-initialises labels and bitmap
     }
 }
@@ -996,7 +1112,8 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
 
 template <int BLOCK, int G>
 static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint32_t grid,
-                          size_t lds, uint64_t* d_lat, float* d_loss, uint32_t delta) {
+                          size_t lds, uint64_t* d_lat, float* d_loss, uint32_t delta, uint32_t use_bkt,
+                          uint32_t use_flat) {
     PreparedGraph& P = ctx->prep;
     constexpr int R = G >= 32 ? 2 : 4;
     sssp_global_group<BLOCK, G, R><<<grid, BLOCK, lds, ctx->stream>>>(
@@ -1004,7 +1121,7 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
         ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
         delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
-        ctx->g_glab.as<uint64_t>());
+        ctx->g_glab.as<uint64_t>(), use_bkt, use_flat);
 }
 
 // Kernel 1b driver: labels in global memory (graphs whose labels exceed the LDS).
@@ -1014,8 +1131,14 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     hipStream_t s = ctx->stream;
     constexpr uint32_t BLOCK = 512;
     const uint32_t W = (P.V + 31) / 32;
-    const size_t lds = (size_t)W * 4 + 16 + (BLOCK / 64) * (kQCap + 32) * 4;
+    // bitmap + control + per-wave queues (+ delta-stepping: one bucket byte per node, when it
+    // fits beside the bitmap; else the sweeps read the active nodes' global labels)
+    const uint32_t use_flat = env_u32("SHD_SSSP_FLAT", 1) != 0;   // edge-parallel expansion
+    size_t lds = (size_t)W * 4 + 16 + (BLOCK / 64) * (kQCap + 32 + (use_flat ? kFlatWords : 0)) * 4;
     if (lds > ctx->max_lds) return SHD_ERR_INVALID;   // bitmap of > ~1.2M nodes
+    const size_t lds_bkt = lds + ((size_t)P.V + 3) / 4 * 4;
+    const uint32_t use_bkt = delta != kLat32Inf && lds_bkt <= ctx->max_lds && env_u32("SHD_SSSP_NO_BKT", 0) != 1;
+    if (use_bkt) lds = lds_bkt;
     const uint32_t per_cu = std::max<uint32_t>(1, env_u32("SHD_SSSP_SLOTS", 2));
     const uint32_t grid = std::min<uint32_t>(re - rb, (uint32_t)ctx->n_cu * per_cu);
     SHD_TRY(ctx->g_glab.ensure((size_t)grid * P.V * 8));
@@ -1023,9 +1146,9 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     const uint32_t G = env_u32("SHD_SSSP_G", deg >= 64 ? 16 : deg >= 24 ? 8 : 4);
     SHD_HIP(hipEventRecord(ctx->ev[2], s));
     switch (G) {
-        case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta); break;
-        case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta); break;
-        default: launch_global<BLOCK, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta); break;
+        case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat); break;
+        case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat); break;
+        default: launch_global<BLOCK, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat); break;
     }
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(ctx->ev[3], s));
