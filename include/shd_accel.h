@@ -135,6 +135,19 @@ shd_status shd_routing_prepare(shd_ctx* ctx, const shd_graph* g, const uint32_t*
 shd_status shd_routing_run(shd_ctx* ctx, uint32_t algo, uint32_t row_begin, uint32_t row_end,
                            uint64_t* d_lat_out, float* d_loss_out, shd_error* err);
 
+/*
+ * shd_routing_run plus next hops (the north star's; the reference keeps none: petgraph's
+ * dijkstra returns scores only, graph/mod.rs:197-200).  Definition, identical for
+ * every engine: pred(s, v) = the LOWEST node index u with an arc u -> v (u != v) whose final
+ * label extended by that arc equals v's label bit for bit (latency and left-folded loss);
+ * next_hop(s, d) = the node after s on d's pred chain, next_hop(s, s) = s (the self-loop), and
+ * in direct mode the destination itself.  d_next_hop (device) receives (row_end - row_begin) x
+ * n_used node indices (GML order); UINT32_MAX never appears in a successful build.
+ */
+shd_status shd_routing_run_next_hops(shd_ctx* ctx, uint32_t algo, uint32_t row_begin, uint32_t row_end,
+                                     uint64_t* d_lat_out, float* d_loss_out, uint32_t* d_next_hop,
+                                     shd_error* err);
+
 /* As shd_routing_build, writing the rows straight into device buffers (hipMalloc'd or torch
  * tensors) on the context's stream; the call returns when the rows are complete. */
 shd_status shd_routing_build_device(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
@@ -148,6 +161,22 @@ shd_status shd_routing_last_info(const shd_ctx* ctx, shd_routing_info* info);
 shd_status shd_routing_lookup(shd_ctx* ctx, uint32_t src_row, uint32_t dst_col,
                               uint64_t* latency_ns, float* packet_loss);
 shd_status shd_routing_smallest_latency(shd_ctx* ctx, uint64_t* latency_ns);
+
+/*
+ * assign_ips (src/main/core/sim_config.rs:399-420) with IpAssignment (graph/mod.rs:354-422),
+ * host code: hosts in HostId order; ip_in[h] = the host's configured IPv4 address (host byte
+ * order, 11.0.0.1 = 0x0B000001) or 0 for none (ip_in may be NULL: no host has one).  Configured
+ * addresses are registered first (a repeat is SHD_ERR_INVALID, *err_host = that host: "IP address
+ * has already been assigned"); every other host gets the next free address after the last one
+ * handed out, from 11.0.0.1 on, skipping x.x.x.0 and x.x.x.255.  ip_out[n_hosts] receives every
+ * host's address; used_gml (capacity n_hosts, may be NULL) the ids of the nodes that own an
+ * address, ascending (IpAssignment::get_nodes, the `nodes` of generate_routing_info,
+ * sim_config.rs:424-461), *n_used their count; host_col (may be NULL) each host's column in
+ * that list -- the relay's host -> node map (shd_relay_setup).
+ */
+shd_status shd_assign_ips(uint32_t n_hosts, const uint32_t* node_gml_id, const uint32_t* ip_in,
+                          uint32_t* ip_out, uint32_t* used_gml, uint32_t* n_used, uint32_t* host_col,
+                          uint32_t* err_host);
 
 /* ---------------------------------------------------------------- relay */
 /*
@@ -412,6 +441,11 @@ typedef struct shd_gml shd_gml;
  * SHD_ERR_LATENCY_OVERFLOW: an edge latency does not fit u64 ns (the reference panics in
  * convert(Nano).unwrap(), graph/mod.rs:338). */
 shd_status shd_gml_parse(const char* text, size_t len, shd_gml** out, char* msg, size_t msg_len);
+/* load_network_graph (graph/mod.rs:481-511) for a GML file: read `path` (xz != 0: decompress it
+ * as xz, read_xz :482-494 -- through the system liblzma), require strict UTF-8
+ * (String::from_utf8), then shd_gml_parse.  File, decompression and UTF-8 failures are
+ * SHD_ERR_INVALID with the reference's context message. */
+shd_status shd_gml_load(const char* path, int32_t xz, shd_gml** out, char* msg, size_t msg_len);
 /* View of the parsed graph; the arrays stay owned by `g` until shd_gml_free. */
 shd_status shd_gml_graph(const shd_gml* g, shd_graph* view);
 /* host_bandwidth_down / _up per node in bits/s (UINT64_MAX = attribute absent; values beyond

@@ -417,3 +417,59 @@ int64_t orc_relay_round(uint32_t n_hosts, const uint32_t* src_off, const uint64_
 }
 
 int orc_max_threads(void) { return omp_get_max_threads(); }
+
+/*
+ * Next hops from a finished table (test infrastructure: the checker of shd_routing_run_next_hops).
+ * The reference keeps none; the definition is the engine's: pred(s, v) = the lowest
+ * node index u with an arc u -> v, u != v, whose label extended by the arc equals v's label bit
+ * for bit (label(s, s) = PathProperties::default() = (0, 0.0), not the self-loop diagonal);
+ * next_hop(s, d) = the node after s on d's pred chain; next_hop(s, s) = s.  `used` must list every
+ * node (the table then holds every label).  Rows [rb, re) of the table are given.
+ */
+int orc_next_hops(uint32_t V, uint32_t E, const uint32_t* es, const uint32_t* ed, const uint64_t* el,
+                  const float* ep, int directed, const uint32_t* used, uint32_t n_used, uint32_t rb,
+                  uint32_t re, const uint64_t* lat, const float* loss, int threads, uint32_t* out) {
+    if (n_used != V) return ORC_NOMEM;
+    adj_t a;
+    if (build_adj(V, E, es, ed, el, ep, directed, &a)) return ORC_NOMEM;
+    int32_t* col = (int32_t*)malloc(V * sizeof(int32_t));
+    for (uint32_t i = 0; i < n_used; i++) col[used[i]] = (int32_t)i;
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel
+    {
+        uint32_t* pred = (uint32_t*)malloc(V * sizeof(uint32_t));
+#pragma omp for schedule(dynamic, 1)
+        for (uint32_t si = rb; si < re; si++) {
+            const uint32_t src = used[si];
+            const uint64_t* L = lat + (size_t)(si - rb) * n_used;
+            const float* P = loss + (size_t)(si - rb) * n_used;
+            for (uint32_t v = 0; v < V; v++) pred[v] = 0xFFFFFFFFu;
+            for (uint32_t u = 0; u < V; u++) {
+                const uint64_t lu = u == src ? 0 : L[col[u]];
+                const float pu = u == src ? 0.0f : P[col[u]];
+                for (uint32_t k = a.off[u]; k < a.off[u + 1]; k++) {
+                    const uint32_t v = a.dst[k];
+                    if (v == u || v == src) continue;
+                    const uint64_t cl = lu + a.lat[k];
+                    const float cp = fold(pu, a.loss[k] + 0.0f);
+                    if (cl == L[col[v]] && memcmp(&cp, &P[col[v]], 4) == 0 && u < pred[v]) pred[v] = u;
+                }
+            }
+            for (uint32_t j = 0; j < n_used; j++) {
+                const uint32_t v = used[j];
+                uint32_t nh = 0xFFFFFFFFu;
+                if (v == src) {
+                    nh = src;
+                } else {
+                    uint32_t w = v, pw = pred[w];
+                    for (uint32_t hop = 0; hop < V && pw != src && pw != 0xFFFFFFFFu; hop++) { w = pw; pw = pred[w]; }
+                    if (pw == src) nh = w;
+                }
+                out[(size_t)(si - rb) * n_used + j] = nh;
+            }
+        }
+        free(pred);
+    }
+    free_adj(&a); free(col);
+    return ORC_OK;
+}

@@ -33,6 +33,9 @@ def lib():
         _lib.orc_shortest_paths_rows.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P,
                                                  C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
                                                  P, P, P, P]
+        _lib.orc_next_hops.restype = C.c_int
+        _lib.orc_next_hops.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P, C.c_uint32, C.c_uint32,
+                                       C.c_uint32, P, P, C.c_int, P]
         _lib.orc_direct_paths.restype = C.c_int
         _lib.orc_direct_paths.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P,
                                           C.c_uint32, P, P, P, P]
@@ -68,6 +71,22 @@ def routing(n_nodes, es, ed, el, ep, directed, used, shortest=True, variant=TIDY
         rc = lib().orc_direct_paths(n_nodes, len(es), _p(es), _p(ed), _p(el), _p(ep),
                                     int(directed), _p(used), n, _p(lat), _p(loss), _p(ea), _p(eb))
     return CODES[rc], lat, loss, (int(ea[0]), int(eb[0]))
+
+
+def next_hops(n_nodes, es, ed, el, ep, directed, used, lat, loss, rows=None, threads=0):
+    """Next hops of table rows (the engine's definition; see oracle.c).  ``used`` must list every
+    node; ``lat``/``loss`` are the rows [rb, re) of the table the oracle built."""
+    used = np.ascontiguousarray(used, np.uint32)
+    n = len(used)
+    rb, re = (0, n) if rows is None else (int(rows[0]), int(rows[1]))
+    out = np.zeros((re - rb, n), np.uint32)
+    rc = lib().orc_next_hops(n_nodes, len(es), _p(np.ascontiguousarray(es, np.uint32)),
+                             _p(np.ascontiguousarray(ed, np.uint32)), _p(np.ascontiguousarray(el, np.uint64)),
+                             _p(np.ascontiguousarray(ep, np.float32)), int(directed), _p(used), n, rb, re,
+                             _p(np.ascontiguousarray(lat, np.uint64)), _p(np.ascontiguousarray(loss, np.float32)),
+                             threads, _p(out))
+    assert rc == 0, "next_hops: used must list every node"
+    return out
 
 
 def relay_round(src_off, send_time, dst_host, payload, host_node, lat, loss, rng, next_id,

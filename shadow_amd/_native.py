@@ -34,6 +34,7 @@ EXPORTED = [
     "shd_comm_unique_id", "shd_comm_init", "shd_comm_init_local", "shd_comm_info", "shd_comm_destroy",
     "shd_shard_range", "shd_routing_run_sharded", "shd_relay_round_sharded",
     "shd_equeue_setup", "shd_equeue_advance", "shd_equeue_copy_popped", "shd_equeue_pending",
+    "shd_routing_run_next_hops", "shd_assign_ips", "shd_gml_load",
 ]
 COMM_ID_BYTES = 128
 
@@ -166,6 +167,9 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_routing_run_sharded": (I32, [P, U32, P, P, P]),
         "shd_relay_round_sharded": (I32, [P, P, P, P]),
         "shd_equeue_setup": (I32, [P, U32]),
+        "shd_routing_run_next_hops": (I32, [P, U32, U32, U32, P, P, P, P]),
+        "shd_assign_ips": (I32, [U32, P, P, P, P, P, P, P]),
+        "shd_gml_load": (I32, [C.c_char_p, I32, P, P, C.c_size_t]),
         "shd_equeue_advance": (I32, [P, P, U64, P]),
         "shd_equeue_copy_popped": (I32, [P, P, P, P, P, P]),
         "shd_equeue_pending": (I32, [P, P, P, P, P, P, P]),

@@ -174,6 +174,21 @@ shd_status shd_routing_run(shd_ctx* ctx, uint32_t algo, uint32_t row_begin, uint
     return routing_run_impl(ctx, algo, row_begin, re, d_lat_out, d_loss_out, err);
 }
 
+shd_status shd_routing_run_next_hops(shd_ctx* ctx, uint32_t algo, uint32_t row_begin, uint32_t row_end,
+                                     uint64_t* d_lat_out, float* d_loss_out, uint32_t* d_next_hop,
+                                     shd_error* err) {
+    if (!ctx || !d_lat_out || !d_loss_out || !d_next_hop) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    if (!ctx->prep.ready) return SHD_ERR_STATE;
+    const uint32_t n = ctx->prep.n_used;
+    const uint32_t re = row_end ? row_end : n;
+    if (row_begin >= re || re > n) return SHD_ERR_INVALID;
+    ctx->nh_out = d_next_hop;
+    const shd_status st = routing_run_impl(ctx, algo, row_begin, re, d_lat_out, d_loss_out, err);
+    ctx->nh_out = nullptr;
+    return st;
+}
+
 shd_status shd_routing_build(shd_ctx* ctx, const shd_graph* g, const uint32_t* used,
                              uint32_t n_used, uint32_t mode, uint32_t algo, uint32_t row_begin,
                              uint32_t row_end, uint64_t* lat_out, float* loss_out,

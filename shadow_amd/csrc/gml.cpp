@@ -17,6 +17,8 @@
 // recursive-descent scanner over the bytes with no per-token allocation.  Errors carry the
 // reference's message text for every validation the reference names; grammar errors report
 // the byte offset (nom's VerboseError trace is not reproduced).
+#include <dlfcn.h>
+
 #include <cerrno>
 #include <cstdint>
 #include <cstdio>
@@ -494,6 +496,137 @@ shd_status shd_gml_parse(const char* text, size_t len, shd_gml** out, char* msg,
     }
     *out = g;
     return SHD_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// xz through the system liblzma (loaded on first use; the reference decompresses with lzma-rs
+// 0.3.0, graph/mod.rs:482-494).  liblzma's stable C ABI (5.x): an lzma_stream starts zeroed
+// (LZMA_STREAM_INIT), lzma_stream_decoder(strm, memlimit, flags), lzma_code(strm, action) with
+// LZMA_RUN = 0 / LZMA_FINISH = 3 returning LZMA_OK = 0 / LZMA_STREAM_END = 1, lzma_end(strm).
+struct XzStream {
+    const uint8_t* next_in;
+    size_t avail_in;
+    uint64_t total_in;
+    uint8_t* next_out;
+    size_t avail_out;
+    uint64_t total_out;
+    const void* allocator;
+    void* internal;
+    void* reserved_ptr[4];
+    uint64_t reserved_int1, reserved_int2;
+    size_t reserved_int3, reserved_int4;
+    int reserved_enum1, reserved_enum2;
+    unsigned char slack[64];   // room beyond the 5.x layout, never read by us
+};
+
+struct Lzma {
+    int (*decoder)(XzStream*, uint64_t, uint32_t) = nullptr;
+    int (*code)(XzStream*, int) = nullptr;
+    void (*end)(XzStream*) = nullptr;
+    bool ok = false;
+    Lzma() {
+        void* h = dlopen("liblzma.so.5", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        decoder = reinterpret_cast<int (*)(XzStream*, uint64_t, uint32_t)>(dlsym(h, "lzma_stream_decoder"));
+        code = reinterpret_cast<int (*)(XzStream*, int)>(dlsym(h, "lzma_code"));
+        end = reinterpret_cast<void (*)(XzStream*)>(dlsym(h, "lzma_end"));
+        ok = decoder && code && end;
+    }
+};
+
+bool xz_decompress(const std::string& in, std::string& out, std::string& why) {
+    static Lzma lz;
+    if (!lz.ok) {
+        why = "liblzma.so.5 not available";
+        return false;
+    }
+    XzStream st;
+    std::memset(&st, 0, sizeof(st));
+    if (lz.decoder(&st, UINT64_MAX, 0) != 0) {
+        why = "decoder init failed";
+        return false;
+    }
+    st.next_in = reinterpret_cast<const uint8_t*>(in.data());
+    st.avail_in = in.size();
+    out.clear();
+    std::vector<uint8_t> buf(1 << 20);
+    int rc = 0;
+    for (;;) {
+        st.next_out = buf.data();
+        st.avail_out = buf.size();
+        rc = lz.code(&st, 3);   // LZMA_FINISH: all input is given
+        out.append(reinterpret_cast<const char*>(buf.data()), buf.size() - st.avail_out);
+        if (rc != 0) break;
+    }
+    lz.end(&st);
+    if (rc != 1) {
+        why = "xz data error " + std::to_string(rc);
+        return false;
+    }
+    return true;
+}
+
+// String::from_utf8 (graph/mod.rs:493): strict UTF-8
+bool valid_utf8(const std::string& s) {
+    const auto* p = reinterpret_cast<const unsigned char*>(s.data());
+    const size_t n = s.size();
+    for (size_t i = 0; i < n;) {
+        const unsigned c = p[i];
+        size_t k;
+        uint32_t cp;
+        if (c < 0x80) { ++i; continue; }
+        if ((c & 0xE0) == 0xC0) { k = 1; cp = c & 0x1F; }
+        else if ((c & 0xF0) == 0xE0) { k = 2; cp = c & 0x0F; }
+        else if ((c & 0xF8) == 0xF0) { k = 3; cp = c & 0x07; }
+        else return false;
+        for (size_t j = 1; j <= k; ++j) {
+            if (i + j >= n || (p[i + j] & 0xC0) != 0x80) return false;
+            cp = (cp << 6) | (p[i + j] & 0x3F);
+        }
+        if ((k == 1 && cp < 0x80) || (k == 2 && cp < 0x800) || (k == 3 && cp < 0x10000) || cp > 0x10FFFF ||
+            (cp >= 0xD800 && cp <= 0xDFFF))
+            return false;
+        i += k + 1;
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+shd_status shd_gml_load(const char* path, int32_t xz, shd_gml** out, char* msg, size_t msg_len) {
+    if (msg && msg_len) msg[0] = 0;
+    if (!path || !out) return SHD_ERR_INVALID;
+    *out = nullptr;
+    auto fail = [&](const std::string& m) {
+        if (msg && msg_len) std::snprintf(msg, msg_len, "%s", m.c_str());
+        return SHD_ERR_INVALID;
+    };
+    std::string raw;
+    {
+        FILE* f = std::fopen(path, "rb");
+        if (!f) return fail(std::string(xz ? "Failed to open file: \"" : "Failed to read file: ") + path +
+                            (xz ? "\"" : ""));
+        char buf[1 << 16];
+        size_t k;
+        while ((k = std::fread(buf, 1, sizeof(buf), f)) > 0) raw.append(buf, k);
+        const bool err = std::ferror(f) != 0;
+        std::fclose(f);
+        if (err) return fail(std::string("Failed to read file: ") + path);
+    }
+    std::string text;
+    if (xz) {
+        std::string why;
+        if (!xz_decompress(raw, text, why)) return fail("Failed to decompress file: " + why);
+    } else {
+        text.swap(raw);
+    }
+    if (!valid_utf8(text)) return fail(xz ? "invalid utf-8 sequence" : std::string("Failed to read file: ") + path);
+    return shd_gml_parse(text.data(), text.size(), out, msg, msg_len);
 }
 
 shd_status shd_gml_graph(const shd_gml* g, shd_graph* view) {

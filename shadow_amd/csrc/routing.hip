@@ -216,7 +216,7 @@ __device__ __forceinline__ void sssp_row(
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
-    uint32_t seed_stride, uint8_t* bkt, uint32_t* flat) {
+    uint32_t seed_stride, uint8_t* bkt, uint32_t* flat, uint32_t* nh_out, uint32_t* pred) {
     // bkt (global labels + delta-stepping): per node, the bucket of the latency that last
     // activated it, in LDS, so choosing a sweep's nodes reads no global label
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
@@ -337,6 +337,49 @@ __device__ __forceinline__ void sssp_row(
         atomicAdd(&stats[0], (unsigned long long)expanded);
         if (wave == 0) atomicAdd(&stats[1], (unsigned long long)sweeps);
     }
+    if (nh_out) {
+        // Next hops (north star; the reference keeps none).  pred(v) = the lowest node
+        // index u with an arc u -> v that is tight for the final labels (key(u) (+) arc == key(v),
+        // bit for bit); every label is reached through such an arc (the fold is monotone), and
+        // latency strictly grows along it, so the pred chain of any reached node ends at the
+        // source.  next hop(src, d) = the node after src on d's pred chain.  pred lives where
+        // the arc-range cache was (LDS kernel) or in a global scratch row (global labels).
+        __syncthreads();
+        for (uint32_t v = tid; v < V; v += BLOCK) pred[v] = 0xFFFFFFFFu;
+        if (GLAB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (uint32_t u = tid; u < V; u += BLOCK) {
+            const uint64_t ku = ld_lab<GLAB>(&lab[u]);
+            if (ku == kKeyInf) continue;
+            const uint32_t lu = key_lat(ku);
+            const float qu = one_minus(key_loss(ku));
+            const uint32_t e = aend[u];
+            for (uint32_t k = abeg[u]; k < e; ++k) {
+                const uint4 a = arcs[k];
+                const uint32_t cl = lu + a.y;
+                if (a.x == u || a.y == kLat32Inf || cl < lu || cl == kLat32Inf) continue;
+                if (pack_key(cl, fold_q(qu, __uint_as_float(a.z))) == ld_lab<GLAB>(&lab[a.x]))
+                    atomicMin(&pred[a.x], u);
+            }
+        }
+        if (GLAB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (uint32_t j = tid; j < n_used; j += BLOCK) {
+            const uint32_t v = used[j];
+            uint32_t nh = 0xFFFFFFFFu;
+            if (v == src) {
+                nh = src;
+            } else {
+                uint32_t w = v, pw = GLAB ? __hip_atomic_load(&pred[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pred[w];
+                for (uint32_t hop = 0; hop < V && pw != src && pw != 0xFFFFFFFFu; ++hop) {
+                    w = pw;
+                    pw = GLAB ? __hip_atomic_load(&pred[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : pred[w];
+                }
+                if (pw == src) nh = w;
+            }
+            nh_out[orow + j] = nh;
+        }
+    }
     for (uint32_t j = tid; j < n_used; j += BLOCK) {
         uint64_t l;
         float p;
@@ -369,7 +412,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
-    uint32_t seed_stride) {
+    uint32_t seed_stride, uint32_t* __restrict__ nh_out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr uint32_t NW = BLOCK / 64;
     uint64_t* lab = reinterpret_cast<uint64_t*>(smem);   // V labels + 64 per-lane scratch labels
@@ -384,7 +427,8 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     sssp_row<BLOCK, G, R, CACHE, false>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
                                         row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
                                         diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
-                                        delta, stats, seed_lat, seed_stride, nullptr, nullptr);
+                                        delta, stats, seed_lat, seed_stride, nullptr, nullptr, nh_out,
+                                        reinterpret_cast<uint32_t*>(smem + rng_off));
 }
 
 // Kernel 1b: labels in global memory, for graphs whose labels do not fit the LDS (C4: 50k
@@ -399,7 +443,8 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     const float* __restrict__ diag_loss, uint64_t* __restrict__ out_lat,
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
-    unsigned long long* __restrict__ stats, uint64_t* __restrict__ glab, uint32_t use_bkt, uint32_t use_flat) {
+    unsigned long long* __restrict__ stats, uint64_t* __restrict__ glab, uint32_t use_bkt, uint32_t use_flat,
+    uint32_t* __restrict__ nh_out, uint32_t* __restrict__ gpred) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
@@ -413,7 +458,8 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
         sssp_row<BLOCK, G, R, false, true>(lab, bits, ctl, wq, nullptr, abeg, aend, arcs, V, used,
                                            n_used, row, (size_t)(row - row_begin) * n_used,
                                            diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
-                                           delta, stats, nullptr, 0, bkt, flat);
+                                           delta, stats, nullptr, 0, bkt, flat, nh_out,
+                                           gpred ? gpred + (size_t)blockIdx.x * V : nullptr);
         __syncthreads();   // the next row re-initialises labels and bitmap
     }
 }
@@ -689,6 +735,61 @@ __global__ void wide_emit(const uint64_t* __restrict__ lat, const float* __restr
     out_loss[o] = p;
 }
 
+// next hops on the wide path: pred(v) = lowest in-neighbour u whose final label extended by
+// the arc equals v's label bit for bit (see sssp_row), then the walk back to the source
+__global__ void wide_pred(const uint32_t* __restrict__ in_off, const uint32_t* __restrict__ in_src,
+                          const uint64_t* __restrict__ in_lat, const float* __restrict__ in_q, uint32_t V,
+                          const uint64_t* __restrict__ la, const float* __restrict__ pa,
+                          const uint32_t* __restrict__ used, uint32_t row0, uint32_t* __restrict__ pred) {
+    const uint32_t v = blockIdx.x * 256 + threadIdx.x;
+    const size_t s = blockIdx.y;
+    if (v >= V) return;
+    const uint64_t* al = la + s * V;
+    const float* ap = pa + s * V;
+    uint32_t best = 0xFFFFFFFFu;
+    const uint64_t lv = al[v];
+    if (v != used[row0 + s] && lv != ~0ull) {
+        const uint32_t pv = __float_as_uint(ap[v]);
+        for (uint32_t k = in_off[v]; k < in_off[v + 1]; ++k) {
+            const uint32_t u = in_src[k];
+            const uint64_t lu = al[u];
+            if (u == v || u >= best || lu == ~0ull) continue;
+            const uint64_t cl = lu + in_lat[k];
+            if (cl < lu || cl != lv) continue;
+            if (__float_as_uint(fold_q(one_minus(ap[u]), in_q[k])) == pv) best = u;
+        }
+    }
+    pred[s * V + v] = best;
+}
+
+__global__ void wide_next_hop(const uint32_t* __restrict__ pred, uint32_t V, const uint32_t* __restrict__ used,
+                              uint32_t n_used, uint32_t row0, uint32_t out_row0, uint32_t* __restrict__ out) {
+    const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+    const size_t s = blockIdx.y;
+    if (j >= n_used) return;
+    const uint32_t src = used[row0 + s], v = used[j];
+    const uint32_t* pr = pred + s * V;
+    uint32_t nh = 0xFFFFFFFFu;
+    if (v == src) {
+        nh = src;
+    } else {
+        uint32_t w = v, pw = pr[w];
+        for (uint32_t hop = 0; hop < V && pw != src && pw != 0xFFFFFFFFu; ++hop) {
+            w = pw;
+            pw = pr[w];
+        }
+        if (pw == src) nh = w;
+    }
+    out[(size_t)(out_row0 + s) * n_used + j] = nh;
+}
+
+__global__ void direct_next_hop(const uint32_t* __restrict__ used, uint32_t n_used, uint32_t rb, uint32_t rows,
+                                uint32_t* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < (uint64_t)rows * n_used) out[i] = used[i % n_used];   // the one edge's far end (graph/mod.rs:232-254)
+    (void)rb;
+}
+
 __global__ void arcs_q(const float* __restrict__ loss, float* __restrict__ q, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n) q[i] = one_minus(loss[i]);
@@ -885,7 +986,8 @@ static shd_status run_wide(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d_l
     const uint32_t V = R.V, n_used = P.n_used;
     const uint32_t batch = std::max<uint32_t>(
         1, std::min<uint32_t>(re - rb, (uint32_t)((1ull << 30) / (24ull * V))));
-    DevBuf la, pa, lb, pb, ch;
+    DevBuf la, pa, lb, pb, ch, pr;
+    if (ctx->nh_out) SHD_TRY(pr.ensure((size_t)batch * V * 4));
     SHD_TRY(la.ensure((size_t)batch * V * 8));
     SHD_TRY(lb.ensure((size_t)batch * V * 8));
     SHD_TRY(pa.ensure((size_t)batch * V * 4));
@@ -909,6 +1011,13 @@ static shd_status run_wide(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d_l
             if (!changed) break;
         }
         dim3 ge(div_up(n_used, 256), nb);
+        if (ctx->nh_out) {
+            wide_pred<<<gv, 256, 0, s>>>(w_off.as<uint32_t>(), w_src.as<uint32_t>(), w_lat.as<uint64_t>(),
+                                         w_q.as<float>(), V, la.as<uint64_t>(), pa.as<float>(),
+                                         ctx->g_used.as<uint32_t>(), r0, pr.as<uint32_t>());
+            wide_next_hop<<<ge, 256, 0, s>>>(pr.as<uint32_t>(), V, ctx->g_used.as<uint32_t>(), n_used, r0, r0 - rb,
+                                             ctx->nh_out);
+        }
         wide_emit<<<ge, 256, 0, s>>>(la.as<uint64_t>(), pa.as<float>(), V, ctx->g_used.as<uint32_t>(),
                                      n_used, r0, r0 - rb, ctx->g_diag_lat.as<uint64_t>(),
                                      ctx->g_diag_loss.as<float>(), d_lat, d_loss,
@@ -1000,6 +1109,9 @@ static shd_status run_direct(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d
     auto* bad_d = reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16);
     direct_check<<<div_up(nn, 256), 256, 0, s>>>(cnt.as<uint32_t>(), nn, bad_d);
     const size_t rows = re - rb;
+    if (ctx->nh_out && rows)
+        direct_next_hop<<<div_up((uint64_t)rows * n_used, 256), 256, 0, s>>>(ctx->g_used.as<uint32_t>(), n_used, rb,
+                                                                             (uint32_t)rows, ctx->nh_out);
     SHD_HIP(hipMemcpyAsync(d_lat, tl.as<uint64_t>() + (size_t)rb * n_used, rows * n_used * 8,
                            hipMemcpyDeviceToDevice, s));
     SHD_HIP(hipMemcpyAsync(d_loss, tp.as<float>() + (size_t)rb * n_used, rows * n_used * 4,
@@ -1035,7 +1147,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
         ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
         delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
-        seed, seed_stride);
+        seed, seed_stride, ctx->nh_out ? ctx->nh_out + (size_t)0 : nullptr);
 }
 
 static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
@@ -1048,7 +1160,8 @@ template <int BLOCK, bool CACHE>
 static void launch_by_degree(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint64_t* d_lat,
                              float* d_loss, uint32_t delta, uint32_t G, const uint32_t* seed,
                              uint32_t ss) {
-    const size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK, CACHE);
+    size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK, CACHE);
+    if (ctx->nh_out && !CACHE) lds = ((lds + 7) & ~(size_t)7) + (size_t)ctx->prep.V * 4;   // pred[V]
     switch (G) {
         case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
         case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
@@ -1121,7 +1234,8 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
         ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
         delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
-        ctx->g_glab.as<uint64_t>(), use_bkt, use_flat);
+        ctx->g_glab.as<uint64_t>(), use_bkt, use_flat, ctx->nh_out,
+        ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr);
 }
 
 // Kernel 1b driver: labels in global memory (graphs whose labels exceed the LDS).
@@ -1142,6 +1256,7 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     const uint32_t per_cu = std::max<uint32_t>(1, env_u32("SHD_SSSP_SLOTS", 2));
     const uint32_t grid = std::min<uint32_t>(re - rb, (uint32_t)ctx->n_cu * per_cu);
     SHD_TRY(ctx->g_glab.ensure((size_t)grid * P.V * 8));
+    if (ctx->nh_out) SHD_TRY(ctx->g_pred.ensure((size_t)grid * P.V * 4));
     const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
     const uint32_t G = env_u32("SHD_SSSP_G", deg >= 64 ? 16 : deg >= 24 ? 8 : 4);
     SHD_HIP(hipEventRecord(ctx->ev[2], s));
@@ -1280,7 +1395,8 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ctx->info.ms_total = ctx->info.ms_main = ms;
         return st;
     }
-    const size_t lds = sssp_lds_bytes(P.V, 1024, false);
+    // labels + bitmap + queues (+ next hops: pred[V]) must fit the LDS for the LDS-label kernels
+    const size_t lds = sssp_lds_bytes(P.V, 1024, false) + (ctx->nh_out ? (size_t)P.V * 4 + 8 : 0);
     if (algo == SHD_ALGO_BLOCKED && P.narrow_arcs && lds <= ctx->max_lds && P.V <= kBlockedMaxV) {
         bool ovf = false;
         SHD_TRY(run_blocked(ctx, rb, re, d_lat, d_loss, &ovf));

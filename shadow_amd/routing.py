@@ -137,6 +137,10 @@ class NetworkGraph:
             if N.STATUS_NAMES.get(st) == "LATENCY_OVERFLOW":
                 raise RoutingPanic(text)
             raise NetGraphError(text)
+        return cls._from_handle(lib, h)
+
+    @classmethod
+    def _from_handle(cls, lib, h) -> "NetworkGraph":
         try:
             v = N.Graph()
             N.check(lib.shd_gml_graph(h, C.byref(v)), "shd_gml_graph")
@@ -185,13 +189,7 @@ class NetworkGraph:
         g = self._cgraph()
         st = eng.lib.shd_routing_build(eng.ctx, C.byref(g), N.ptr(used), n, mode, algo, rb, re,
                                        N.ptr(lat), N.ptr(loss), C.byref(err))
-        if st in (1, 2):
-            what = "No edge connecting" if st == 1 else "More than one edge connecting"
-            raise NetGraphError(f"{what} node {err.node_a} to {err.node_b}")
-        if st == 3:
-            raise RoutingPanic(f"assertion failed: paths.len() == nodes.len().pow(2) "
-                               f"(no path from node {err.node_a} to {err.node_b})")
-        N.check(st, "shd_routing_build", err)
+        self._raise(st, err)
         return PathTable(self, list(used), lat, loss, rb)
 
     def compute_shortest_paths(self, nodes, engine: Engine | None = None,
@@ -202,6 +200,41 @@ class NetworkGraph:
     def get_direct_paths(self, nodes, engine: Engine | None = None, rows=None) -> PathTable:
         """``NetworkGraph::get_direct_paths`` (graph/mod.rs:232-254)."""
         return self._build(nodes, N.ROUTE_DIRECT, N.ALGO_AUTO, engine, rows)
+
+    def compute_next_hops(self, nodes, engine: Engine | None = None, algo: int = N.ALGO_AUTO, rows=None,
+                          shortest: bool = True):
+        """The table plus next hops (``shd_routing_run_next_hops``; the reference keeps none).
+        Returns (PathTable, next_hop[r, n] node indices): next_hop(s, d) is the node after s on
+        the lowest-index tight-predecessor chain of d; next_hop(s, s) = s."""
+        import torch
+        eng = engine or default_engine()
+        used = np.ascontiguousarray(nodes, np.uint32)
+        n = len(used)
+        rb, re = (0, n) if rows is None else rows
+        err = N.Error()
+        g = self._cgraph()
+        st = eng.lib.shd_routing_prepare(eng.ctx, C.byref(g), N.ptr(used), n,
+                                         N.ROUTE_SHORTEST if shortest else N.ROUTE_DIRECT, C.byref(err))
+        self._raise(st, err)
+        lat = torch.empty((re - rb, n), dtype=torch.int64, device="cuda")
+        loss = torch.empty((re - rb, n), dtype=torch.float32, device="cuda")
+        nh = torch.empty((re - rb, n), dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        st = eng.lib.shd_routing_run_next_hops(eng.ctx, algo, rb, re, N.ptr(lat), N.ptr(loss), N.ptr(nh),
+                                               C.byref(err))
+        self._raise(st, err)
+        t = PathTable(self, list(used), lat.cpu().numpy().view(np.uint64), loss.cpu().numpy(), rb)
+        return t, nh.cpu().numpy().view(np.uint32)
+
+    @staticmethod
+    def _raise(st, err):
+        if st in (1, 2):
+            what = "No edge connecting" if st == 1 else "More than one edge connecting"
+            raise NetGraphError(f"{what} node {err.node_a} to {err.node_b}")
+        if st == 3:
+            raise RoutingPanic(f"assertion failed: paths.len() == nodes.len().pow(2) "
+                               f"(no path from node {err.node_a} to {err.node_b})")
+        N.check(st, "routing", err)
 
 
 class RoutingInfo:
@@ -226,6 +259,47 @@ class RoutingInfo:
     def get_smallest_latency_ns(self):
         return int(self.table.lat.min()) if self.table.lat.size else None
 
+    def latency_ns(self, start: int, end: int):
+        """``WorkerShared::latency`` / ``worker_getLatency`` (worker.rs:529-536, 660-670)."""
+        p = self.path(start, end)
+        return None if p is None else p[0]
+
+    def reliability(self, start: int, end: int):
+        """``WorkerShared::reliability`` (worker.rs:538-543): ``1.0f32 - packet_loss``."""
+        p = self.path(start, end)
+        return None if p is None else np.float32(np.float32(1.0) - p[1])
+
+
+class IpAssignmentError(Exception):
+    """``IpPreviouslyAssignedError`` (graph/mod.rs:343-351) with the caller's context
+    (sim_config.rs:407-409)."""
+
+
+def assign_ips(node_gml_ids, ips=None):
+    """``assign_ips`` (sim_config.rs:399-420) over ``IpAssignment`` (graph/mod.rs:354-422), in the
+    native host code (``shd_assign_ips``).  ``node_gml_ids[h]`` is host h's network node id (hosts
+    in HostId order), ``ips[h]`` its configured IPv4 address as an int (0 / None = none).
+    Returns (ip per host, used node ids ascending = IpAssignment::get_nodes, each host's column
+    in that list = the relay's host -> node map)."""
+    lib = N.load()
+    ids = np.ascontiguousarray(node_gml_ids, np.uint32)
+    n = len(ids)
+    ip_in = None if ips is None else np.ascontiguousarray([int(x or 0) for x in ips], np.uint32)
+    ip_out = np.zeros(n, np.uint32)
+    used = np.zeros(max(n, 1), np.uint32)
+    col = np.zeros(max(n, 1), np.uint32)
+    n_used = C.c_uint32(0)
+    bad = C.c_uint32(0)
+    st = lib.shd_assign_ips(n, N.ptr(ids), N.ptr(ip_in), N.ptr(ip_out), N.ptr(used), C.byref(n_used),
+                            N.ptr(col), C.byref(bad))
+    if st == 5 and ip_in is not None and n:
+        h = bad.value
+        ip = ip_in[h]
+        raise IpAssignmentError(f"Failed to assign IP address {ip >> 24}.{(ip >> 16) & 255}.{(ip >> 8) & 255}."
+                                f"{ip & 255} for host {h} to node '{ids[h]}': IP address has already been assigned")
+    N.check(st, "shd_assign_ips")
+    return ip_out, used[:n_used.value].copy(), col[:n].copy()
+
 
 def generate_routing_info(graph: NetworkGraph, nodes, use_shortest_paths: bool = True,
                           engine: Engine | None = None) -> RoutingInfo:
@@ -236,18 +310,18 @@ def generate_routing_info(graph: NetworkGraph, nodes, use_shortest_paths: bool =
     return RoutingInfo(table)
 
 
-def load_network_graph(path: str) -> str:
-    """``load_network_graph`` (graph/mod.rs:481-520) for a GML file source: the text of `path`,
-    xz-decompressed when it ends in ``.xz`` (the reference's ``compression: xz``; Python's
-    lzma stands in for lzma-rs), decoded as strict UTF-8 like ``String::from_utf8``."""
-    import lzma
-    if path.endswith(".xz"):
-        with lzma.open(path, "rb") as f:
-            raw = f.read()
-    else:
-        with open(path, "rb") as f:
-            raw = f.read()
-    try:
-        return raw.decode("utf-8")
-    except UnicodeDecodeError as e:
-        raise NetGraphError(f"invalid utf-8: {e}") from None
+def load_network_graph(path: str, compression: str | None = None) -> NetworkGraph:
+    """``load_network_graph`` (graph/mod.rs:481-511) + ``NetworkGraph::parse`` for a GML file
+    source, natively (``shd_gml_load``): ``compression="xz"`` (the reference's
+    ``compression: xz``, read_xz :482-494) decompresses through the system liblzma; the text must
+    be strict UTF-8 (``String::from_utf8``)."""
+    lib = N.load()
+    h = C.c_void_p()
+    msg = C.create_string_buffer(1024)
+    st = lib.shd_gml_load(path.encode(), 1 if compression == "xz" else 0, C.byref(h), msg, len(msg))
+    if st != N.SHD_OK:
+        text = msg.value.decode("utf-8", "replace")
+        if N.STATUS_NAMES.get(st) == "LATENCY_OVERFLOW":
+            raise RoutingPanic(text)
+        raise NetGraphError(text)
+    return NetworkGraph._from_handle(lib, h)

@@ -104,3 +104,16 @@ def random_graph(rng, n, p_edge, directed, max_ms=20, loss_max=0.3, ties=True, s
     order = rng.permutation(m)
     return (np.arange(n, dtype=np.uint32), np.asarray(src, np.uint32)[order],
             np.asarray(dst, np.uint32)[order], lat[order], loss[order], directed)
+
+
+def gml_text(node_ids, src, dst, lat_ns, loss, directed=False):
+    """GML text of an edge list (node indices -> ids), one key per line as the reference's grammar
+    wants (a newline after every '[' and value); latencies in ns, losses as float literals."""
+    out = ["graph [\n", f"  directed {int(directed)}\n"]
+    for i in node_ids:
+        out.append(f"  node [\n    id {int(i)}\n  ]\n")
+    for a, b, lt, pl in zip(src, dst, lat_ns, loss):
+        out.append("  edge [\n    source %d\n    target %d\n    latency \"%d ns\"\n    packet_loss %r\n  ]\n"
+                   % (int(node_ids[a]), int(node_ids[b]), int(lt), float(pl)))
+    out.append("]\n")
+    return "".join(out)

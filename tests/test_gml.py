@@ -294,3 +294,85 @@ def test_native_parse_speed_vs_oracle():
     t2 = time.perf_counter()
     assert g is not None and len(g.edge_src) == len(o.edges)
     assert (t1 - t0) * 5 < (t2 - t1)
+
+
+# The reference's compressed-graph integration test (src/test/compressed-graph/): its graph
+# file, compressed with `xz --force` as its CMakeLists does, loaded with `compression: xz`.
+COMPRESSED_GRAPH = """graph [
+  node [
+    id 0
+    host_bandwidth_up "1 Gbit"
+    host_bandwidth_down "1 Gbit"
+  ]
+  edge [
+    source 0
+    target 0
+    latency "1 ms"
+  ]
+]
+"""
+
+
+def _xz_file(tmp_path, name, data: bytes):
+    import shutil
+    import subprocess
+    p = tmp_path / name
+    p.write_bytes(data)
+    if shutil.which("xz"):
+        subprocess.check_call(["xz", "--force", str(p)])
+    else:   # same container format (CRC64 check, xz's default)
+        import lzma
+        (tmp_path / (name + ".xz")).write_bytes(lzma.compress(data, format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64))
+    return str(p) + ".xz"
+
+
+def test_native_load_xz_reference_compressed_graph(tmp_path):
+    from shadow_amd.routing import NetGraphError, load_network_graph
+    path = _xz_file(tmp_path, "graph-compressed.gml", COMPRESSED_GRAPH.encode())
+    g = load_network_graph(path, compression="xz")
+    assert g.node_ids.tolist() == [0] and g.edge_latency_ns.tolist() == [1_000_000]
+    assert g.bandwidth_up_bps.tolist() == [10**9] and g.bandwidth_down_bps.tolist() == [10**9]
+    with pytest.raises(NetGraphError, match="Failed to read file"):   # read_to_string: not UTF-8
+        load_network_graph(path, compression=None)
+    with pytest.raises(NetGraphError, match="Failed to decompress"):
+        load_network_graph(_corrupt(tmp_path, path), compression="xz")
+    with pytest.raises(NetGraphError, match="Failed to"):
+        load_network_graph(str(tmp_path / "missing.gml.xz"), compression="xz")
+
+
+def _corrupt(tmp_path, path):
+    b = bytearray(open(path, "rb").read())
+    b[len(b) // 2] ^= 0x5A
+    q = tmp_path / "corrupt.gml.xz"
+    q.write_bytes(bytes(b))
+    return str(q)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_native_load_xz_random_graphs(tmp_path, seed):
+    """Random GML texts: plain file, xz file and in-memory parse give identical arrays."""
+    from shadow_amd.routing import NetworkGraph, load_network_graph
+    rng = np.random.default_rng(900 + seed)
+    text = _rand_gml(rng)
+    try:
+        want = NetworkGraph.parse(text)
+    except Exception:   # noqa: BLE001 -- invalid texts: the loaders must agree on the error too
+        want = None
+    plain = tmp_path / "g.gml"
+    plain.write_text(text)
+    for path, comp in ((str(plain), None), (_xz_file(tmp_path, "h.gml", text.encode()), "xz")):
+        if want is None:
+            with pytest.raises(Exception):
+                load_network_graph(path, compression=comp)
+            continue
+        g = load_network_graph(path, compression=comp)
+        for k in ("node_ids", "edge_src", "edge_dst", "edge_latency_ns"):
+            assert np.array_equal(getattr(g, k), getattr(want, k)), k
+        assert np.array_equal(g.edge_packet_loss.view(np.uint32), want.edge_packet_loss.view(np.uint32))
+
+
+def test_native_load_rejects_invalid_utf8(tmp_path):
+    from shadow_amd.routing import NetGraphError, load_network_graph
+    path = _xz_file(tmp_path, "bad.gml", COMPRESSED_GRAPH.encode().replace(b"Gbit", b"G\xffbit"))
+    with pytest.raises(NetGraphError, match="utf-8"):
+        load_network_graph(path, compression="xz")

@@ -312,3 +312,42 @@ def test_c_oracle_row_range_matches_full(seed):
             assert c2 == "OK"
             assert np.array_equal(l2, lat[rb:re])
             assert np.array_equal(p2.view(np.uint32), loss[rb:re].view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_native_assign_ips_matches_ip_assignment(seed):
+    """shd_assign_ips (host code) against the IpAssignment restatement (graph/mod.rs:354-422,
+    sim_config.rs:399-420): configured addresses first, then 11.0.0.1.. skipping .0/.255 and
+    every address already taken."""
+    from shadow_amd.routing import IpAssignmentError, assign_ips
+    rng = np.random.default_rng(40 + seed)
+    n = int(rng.integers(1, 700))
+    ids = rng.choice([3, 7, 11, 200, 4096, 99999], size=n).astype(np.uint32)
+    ips = [0] * n
+    k = n // 4
+    picks = rng.choice(np.arange(1, 600), size=k, replace=seed % 2 == 1)   # odd seeds: repeats
+    for h, a in zip(rng.choice(n, size=k, replace=False), picks):
+        ips[h] = (11 << 24) + int(a)      # inside the automatic range: assign() must skip them
+    o = R.IpAssignment()
+    want = [0] * n
+    dup = None
+    for h in range(n):
+        if ips[h]:
+            try:
+                o.assign_ip(int(ids[h]), ips[h])
+                want[h] = ips[h]
+            except R.RoutingError:
+                dup = h
+                break
+    if dup is not None:
+        with pytest.raises(IpAssignmentError, match="already been assigned"):
+            assign_ips(ids, ips)
+        return
+    for h in range(n):
+        if not ips[h]:
+            want[h] = o.assign(int(ids[h]))
+    ip_out, used, col = assign_ips(ids, ips)
+    assert ip_out.tolist() == want
+    assert all((ip & 0xFF) not in (0, 255) for ip in ip_out.tolist())
+    assert used.tolist() == sorted(o.get_nodes())
+    assert np.array_equal(used[col], ids)
