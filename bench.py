@@ -543,17 +543,18 @@ def codel_leg(eng, steps=5, cpu=True):
     out = {"workload": "C5 destinations: 100k CoDel queues x (100 pushes + 100 pops) per batch",
            "ops": n, "ms_per_batch": ms, "value": n / (ms * 1e-3), "unit": "queue ops/s",
            "dropped": dropped, "work": "one lane per host replays its ops in order (sequential state machine)"}
-    if cpu:   # oracle restatement (pure Python, one core) on 2,000 of the hosts
-        from oracle import codel as O
-        k = 2000
+    if cpu:   # the C restatement (oracle/c/queues.c) over the whole batch, all host cores
+        from oracle import corc
+        threads = corc.max_threads()
+        corc.codel_run(H, off, tarr, size, pkt, H * per, threads=threads)   # warm (page faults)
         s1 = time.perf_counter()
-        O.run_ops(k, off[: k + 1], tarr[: 2 * per * k], size[: 2 * per * k], pkt[: 2 * per * k])
+        pop_ref, fate_ref = corc.codel_run(H, off, tarr, size, pkt, H * per, threads=threads)
         dt = time.perf_counter() - s1
-        out["cpu_baseline"] = {"value": 2 * per * k / dt, "unit": "queue ops/s", "cores": 1, "kind": "port",
-                               "sample": "oracle/codel.py on 2,000 hosts of the same batch (400k ops)"}
-        _, pop_ref, _ = O.run_ops(k, off[: k + 1], tarr[: 2 * per * k], size[: 2 * per * k], pkt[: 2 * per * k])
-        out["cpu_baseline"]["bit_exact_vs_gpu"] = bool(
-            np.array_equal(np.asarray(pop_ref, np.uint32), pop_out.cpu().numpy().view(np.uint32)[: 2 * per * k]))
+        out["cpu_baseline"] = {"value": n / dt, "unit": "queue ops/s", "cores": threads, "kind": "port",
+                               "sample": "the whole batch (20M ops) through oracle/c/queues.c (CoDelQueue "
+                                         "restated, hosts over OpenMP threads)",
+                               "bit_exact_vs_gpu": bool(np.array_equal(pop_ref, pop_out.cpu().numpy().view(np.uint32))
+                                                        and np.array_equal(fate_ref, f))}
     return out
 
 
@@ -600,18 +601,18 @@ def tbucket_leg(eng, steps=5, cpu=True):
            "skipped": int(np.count_nonzero(st == 2)),
            "work": "one lane per relay replays its attempts in order (sequential state machine); "
                    "step includes shd_tb_setup (host -> device copy of 100k buckets)"}
-    if cpu:   # oracle restatement (pure Python, one core) on 2,000 of the relays
-        from oracle import token_bucket as O
-        k = 2000
-        bk = [O.TokenBucket(c, i, v, t0) for _ in range(k)]
+    if cpu:   # the C restatement (oracle/c/queues.c) over the whole batch, all host cores
+        from oracle import corc
+        threads = corc.max_threads()
+        corc.tb_run(caps, incs, itvs, last, off, tarr, size, flags, threads=threads)   # warm
         s1 = time.perf_counter()
-        ost, oval = O.relay_run(bk, [0] * k, off[: k + 1], tarr[: per * k], size[: per * k], flags[: per * k])
+        ost, oval, _ = corc.tb_run(caps, incs, itvs, last, off, tarr, size, flags, threads=threads)
         dt = time.perf_counter() - s1
-        out["cpu_baseline"] = {"value": per * k / dt, "unit": "relay attempts/s", "cores": 1, "kind": "port",
-                               "sample": "oracle/token_bucket.py on 2,000 relays of the same batch (200k attempts)",
-                               "bit_exact_vs_gpu": bool(
-                                   np.array_equal(np.asarray(ost, np.uint8), st[: per * k]) and np.array_equal(
-                                       np.asarray(oval, np.uint64), value.cpu().numpy().view(np.uint64)[: per * k]))}
+        out["cpu_baseline"] = {"value": n / dt, "unit": "relay attempts/s", "cores": threads, "kind": "port",
+                               "sample": "the whole batch (10M attempts) through oracle/c/queues.c (TokenBucket + "
+                                         "forward_until_blocked restated, relays over OpenMP threads)",
+                               "bit_exact_vs_gpu": bool(np.array_equal(ost, st) and np.array_equal(
+                                   oval, value.cpu().numpy().view(np.uint64)))}
     return out
 
 def main():

@@ -36,6 +36,10 @@ def lib():
         _lib.orc_next_hops.restype = C.c_int
         _lib.orc_next_hops.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P, C.c_uint32, C.c_uint32,
                                        C.c_uint32, P, P, C.c_int, P]
+        _lib.orc_codel_run.restype = None
+        _lib.orc_codel_run.argtypes = [C.c_uint32, P, P, P, P, P, P, C.c_uint32, C.c_int]
+        _lib.orc_tb_run.restype = C.c_int64
+        _lib.orc_tb_run.argtypes = [C.c_uint32, P, P, P, P, P, P, P, P, P, P, C.c_int]
         _lib.orc_direct_paths.restype = C.c_int
         _lib.orc_direct_paths.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, C.c_int, P,
                                           C.c_uint32, P, P, P, P]
@@ -120,3 +124,26 @@ def relay_round(src_off, send_time, dst_host, payload, host_node, lat, loss, rng
 
 def max_threads():
     return lib().orc_max_threads()
+
+
+def codel_run(n_hosts, off, time, size, pkt, n_ids, threads=0):
+    """C restatement of a CoDel batch on fresh queues -> (pop_out u32[n_ops], fate u64[n_ids])."""
+    n = len(time)
+    pop = np.zeros(n, np.uint32)
+    fate = np.zeros(n_ids, np.uint64)
+    lib().orc_codel_run(n_hosts, _p(np.ascontiguousarray(off, np.uint32)), _p(np.ascontiguousarray(time, np.uint64)),
+                        _p(np.ascontiguousarray(size, np.uint32)), _p(np.ascontiguousarray(pkt, np.uint32)),
+                        _p(pop), _p(fate), n_ids, threads)
+    return pop, fate
+
+
+def tb_run(capacity, increment, interval, last_refill, off, time, size, flags, threads=0):
+    """C restatement of a token-bucket batch on fresh buckets -> (status u8, value u64, panics)."""
+    n = len(time)
+    st = np.zeros(n, np.uint8)
+    val = np.zeros(n, np.uint64)
+    a = [np.ascontiguousarray(x, np.uint64) for x in (capacity, increment, interval, last_refill)]
+    k = lib().orc_tb_run(len(a[0]), *(_p(x) for x in a), _p(np.ascontiguousarray(off, np.uint32)),
+                         _p(np.ascontiguousarray(time, np.uint64)), _p(np.ascontiguousarray(size, np.uint32)),
+                         _p(np.ascontiguousarray(flags, np.uint8)), _p(st), _p(val), threads)
+    return st, val, int(k)

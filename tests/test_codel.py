@@ -176,3 +176,18 @@ def test_capacity_overflow_reported(engine):
     q2 = CoDelQueues(engine, 2, 8)
     pop, _ = q2.run(off, [START] * 5, [1500] * 5, list(range(5)))
     assert (pop == 0xFFFFFFFF).all()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_c_restatement_matches_python_oracle(seed):
+    """oracle/c/queues.c (the bench's multi-core CPU baseline) against oracle/codel.py on one
+    fresh batch: pop results and packet fates bit for bit."""
+    from oracle import corc
+    rng = np.random.default_rng(700 + seed)
+    n_hosts = int(rng.integers(1, 400))
+    off, t, sz, pk, pid = _random_ops(rng, n_hosts, 80)
+    n_ids = max(pid, 1)
+    _, pop_ref, fate_ref = O.run_ops(n_hosts, off, t, sz, pk)
+    pop, fate = corc.codel_run(n_hosts, off, t, sz, pk, n_ids)
+    assert pop.tolist() == [int(x) for x in pop_ref]
+    assert np.array_equal(fate, _oracle_fate(fate_ref, n_ids))

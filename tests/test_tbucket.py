@@ -153,3 +153,19 @@ def test_gpu_invalid_setup_and_time_before_refill(engine):
     tb = TokenBuckets(engine, [100], [10], [MS], [now])
     with pytest.raises(N.ShdError):
         tb.run([0, 1], [now - 1], [10])    # duration_since before last_refill: the reference panics
+
+
+@pytest.mark.parametrize("seed", [4, 5, 6])
+def test_c_restatement_matches_python_oracle(seed):
+    """oracle/c/queues.c (the bench's multi-core CPU baseline) against oracle/token_bucket.py."""
+    from oracle import corc
+    rng = np.random.default_rng(seed)
+    R = 900
+    t0 = O.SIM_START + 5 * 10**9
+    caps, incs, itvs = _setup(rng, R, t0)
+    buckets = [None if c == 0 else O.TokenBucket(int(c), int(i), int(v), t0) for c, i, v in zip(caps, incs, itvs)]
+    off, time, size, flags = _random_batch(rng, R, 40, t0, 30 * MS)
+    ost, oval = O.relay_run(buckets, [0] * R, off, time, size, flags)
+    st, val, panics = corc.tb_run(caps, incs, itvs, np.full(R, t0, np.uint64), off, time, size, flags)
+    assert panics == 0
+    assert st.tolist() == ost and val.tolist() == oval
