@@ -102,7 +102,7 @@ struct PreparedGraph {
     uint32_t mode = 0, V = 0, n_used = 0;
     bool directed = false, narrow_arcs = false;
     uint64_t arcs = 0, max_arc_lat = 0, pruned_arcs = 0, tight_arcs = 0;
-    uint32_t mean_arc_lat = 1;
+    uint32_t mean_arc_lat = 1, min_arc_lat = 1;
     std::vector<uint32_t> used, node_ids, es, ed;
     std::vector<uint64_t> el;
     std::vector<float> ep;

@@ -53,7 +53,7 @@ __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* la
                                            uint32_t scratch, const uint2* rng, const uint32_t* __restrict__ abeg,
                                            const uint32_t* __restrict__ aend,
                                            const uint4* __restrict__ arcs, bool& ovf, bool& dirty,
-                                           uint8_t* bkt, float inv_delta) {
+                                           uint8_t* bkt, float inv_delta, uint32_t& mnext) {
     const uint64_t ku = ld_lab<GLAB>(&lab[u]);
     const uint32_t lu = key_lat(ku);
     const float qu = one_minus(key_loss(ku));
@@ -109,6 +109,54 @@ __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* la
                 if ((imp >> i) & 1u) {
                     if (bkt) bkt[a[i].x] = bucket_of(key_lat(cand[i]), inv_delta);
                     atomicOr(&bits[a[i].x >> 5], 1u << (a[i].x & 31));
+                    mnext = min(mnext, key_lat(cand[i]));
+                }
+        }
+    }
+}
+
+// Padded arc lists (pruned dense graphs, prune_rows): every node's list is a multiple of
+// kArcPad slots, the tail filled with no-op arcs {scratch label V + i, lat 0, q 0} whose
+// candidate (lu, 1.0f) meets a scratch label holding 0.  The group then loads its G x R slots
+// at immediate offsets from one address, with no clamp, liveness test or per-arc select, and
+// the u32 overflow test is one compare per node: a label above lat_guard (2^32 - 2 - the
+// largest arc latency) flags the build for the wide rerun before any add can wrap.  The
+// kernel is issue-bound (C2 PMC: VALU pipe ~70% busy), so these per-arc instructions are the
+// cost that matters.
+constexpr uint32_t kArcPad = 64;
+template <int G, int R, bool CACHE>
+__device__ __forceinline__ void relax_node_pad(uint32_t u, uint32_t gl, uint64_t* lab, uint32_t* bits,
+                                               const uint2* rng, const uint32_t* __restrict__ abeg,
+                                               const uint32_t* __restrict__ aend,
+                                               const uint4* __restrict__ arcs, uint32_t lat_guard,
+                                               bool& ovf, bool& dirty, uint32_t& mnext) {
+    static_assert(kArcPad % (G * R) == 0, "a padded list holds whole G x R steps");
+    const uint64_t ku = lab[u];
+    const uint32_t lu = key_lat(ku);
+    if (lu > lat_guard) ovf = true;
+    const float qu = one_minus(key_loss(ku));
+    const uint2 r = CACHE ? rng[u] : make_uint2(abeg[u], aend[u]);
+    for (uint32_t k0 = r.x; k0 < r.y; k0 += G * R) {
+        const uint4* ap = arcs + k0 + gl;
+        uint4 a[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) a[i] = ap[i * G];
+        uint64_t cand[R], old[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) cand[i] = pack_key(lu + a[i].y, fold_q(qu, __uint_as_float(a[i].z)));
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+            old[i] = atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[i].x]), (unsigned long long)cand[i]);
+        uint32_t imp = 0;
+#pragma unroll
+        for (int i = 0; i < R; ++i) imp |= (cand[i] < old[i] ? 1u : 0u) << i;
+        if (imp) {
+            dirty = true;
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+                if ((imp >> i) & 1u) {
+                    atomicOr(&bits[a[i].x >> 5], 1u << (a[i].x & 31));
+                    mnext = min(mnext, key_lat(cand[i]));
                 }
         }
     }
@@ -124,10 +172,12 @@ constexpr int kFlatR = 8;              // arcs per lane per round of expand_flat
 // reads and atomics -- one chain of global round trips per ~512 relaxations instead of one per
 // node group.  The owner of an arc is the last node whose prefix is <= its position.  BA and
 // internet-like graphs mix hubs and low-degree nodes; this keeps every lane busy on both.
+template <bool GLAB>
 __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint32_t lane, uint64_t* lab,
-                                            uint32_t* bits, const uint32_t* __restrict__ abeg,
+                                            uint32_t* bits, const uint2* rng, const uint32_t* __restrict__ abeg,
                                             const uint32_t* __restrict__ aend, const uint4* __restrict__ arcs,
-                                            uint32_t* fx, bool& ovf, bool& dirty, uint8_t* bkt, float inv_delta) {
+                                            uint32_t* fx, bool& ovf, bool& dirty, uint8_t* bkt, float inv_delta,
+                                            uint32_t scratch) {
     uint32_t* pre = fx;          // [65]
     uint32_t* beg = fx + 65;     // [64]
     uint32_t* nl = fx + 129;     // [64] latency of the node's label
@@ -138,9 +188,10 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
         uint64_t ku = kKeyInf;
         if (lane < cn) {
             const uint32_t u = q[c0 + lane];
-            b = abeg[u];
-            deg = aend[u] - b;
-            ku = ld_lab<true>(&lab[u]);
+            const uint2 r = rng ? rng[u] : make_uint2(abeg[u], aend[u]);
+            b = r.x;
+            deg = r.y - b;
+            ku = ld_lab<GLAB>(&lab[u]);
         }
         uint32_t incl = deg;
 #pragma unroll
@@ -185,19 +236,35 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
                 if (live[r] && a[r].y != kLat32Inf && !ok) ovf = true;   // leaves u32: wide rerun
                 cand[r] = ok ? pack_key(cl, fold_q(qu[r], __uint_as_float(a[r].z))) : kKeyInf;
             }
+            if constexpr (GLAB) {
 #pragma unroll
-            for (int r = 0; r < kFlatR; ++r) cur[r] = cand[r] != kKeyInf ? ld_lab<true>(&lab[a[r].x]) : 0ull;
+                for (int r = 0; r < kFlatR; ++r) cur[r] = cand[r] != kKeyInf ? ld_lab<true>(&lab[a[r].x]) : 0ull;
 #pragma unroll
-            for (int r = 0; r < kFlatR; ++r) {
-                // labels only decrease: a candidate not below the label read now cannot improve it
-                if (cand[r] < cur[r]) {
-                    const uint64_t old =
-                        atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[r].x]), (unsigned long long)cand[r]);
-                    if (cand[r] < old) {
-                        dirty = true;
-                        if (bkt) bkt[a[r].x] = bucket_of(key_lat(cand[r]), inv_delta);
-                        atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
+                for (int r = 0; r < kFlatR; ++r) {
+                    // labels only decrease: a candidate not below the label read now cannot improve it
+                    if (cand[r] < cur[r]) {
+                        const uint64_t old =
+                            atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[r].x]), (unsigned long long)cand[r]);
+                        if (cand[r] < old) {
+                            dirty = true;
+                            if (bkt) bkt[a[r].x] = bucket_of(key_lat(cand[r]), inv_delta);
+                            atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
+                        }
                     }
+                }
+            } else {   // LDS labels: unconditional atomics (dead slots hit the lane's scratch label)
+#pragma unroll
+                for (int r = 0; r < kFlatR; ++r)
+                    cur[r] = atomicMin(reinterpret_cast<unsigned long long*>(&lab[cand[r] != kKeyInf ? a[r].x : scratch]),
+                                       (unsigned long long)cand[r]);
+                uint32_t imp = 0;
+#pragma unroll
+                for (int r = 0; r < kFlatR; ++r) imp |= (cand[r] < cur[r] ? 1u : 0u) << r;
+                if (imp) {
+                    dirty = true;
+#pragma unroll
+                    for (int r = 0; r < kFlatR; ++r)
+                        if ((imp >> r) & 1u) atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
                 }
             }
         }
@@ -216,7 +283,8 @@ __device__ __forceinline__ void sssp_row(
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
-    uint32_t seed_stride, uint8_t* bkt, uint32_t* flat, uint32_t* nh_out, uint32_t* pred) {
+    uint32_t seed_stride, uint8_t* bkt, uint32_t* flat, uint32_t* nh_out, uint32_t* pred,
+    uint32_t lat_guard, uint32_t pad_r) {
     // bkt (global labels + delta-stepping): per node, the bucket of the latency that last
     // activated it, in LDS, so choosing a sweep's nodes reads no global label
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
@@ -250,25 +318,45 @@ __device__ __forceinline__ void sssp_row(
         if (CACHE) rng[v] = make_uint2(abeg[v], aend[v]);
     }
     for (uint32_t w = tid; w < W; w += BLOCK) bits[w] = 0;
+    if (!GLAB && tid < 64) lab[V + tid] = 0;   // scratch labels: no candidate improves them
     // global labels: every storing wave drains its stores before the barrier, so the L2 holds
     // them before any wave's atomics
     if (GLAB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // One-barrier sweeps (LDS labels + delta-stepping): the next sweep's bucket floor is the
+    // minimum over the nodes still active after this one -- those the selection skipped, and
+    // those a relaxation just improved -- gathered while the sweep runs, so no separate scan
+    // and only one barrier per sweep.  Three rotating accumulators ctl[1..3]: sweep k writes
+    // slot k%3, all read it after the barrier, and sweep k resets slot (k+1)%3, whose last
+    // readers passed the barrier of sweep k-1.  A floor taken from a node that the same sweep
+    // then expands is only lower than needed: the next sweep selects less, never wrongly.
+    const bool fused = !GLAB && use_delta && flat == nullptr;
     if (tid == 0) {
         if (!GLAB) lab[src] = 0;  // PathProperties::default() = (0 ns, 0.0)
         bits[src >> 5] = 1u << (src & 31);
         if (bkt) bkt[src] = 0;
+        if (fused) ctl[1] = ctl[2] = ctl[3] = kLat32Inf;
     }
+    if (fused) __syncthreads();
     bool ovf = false;
     uint32_t expanded = 0, sweeps = 0;
+    uint32_t slot = 0;   // fused: this sweep's accumulator, ctl[1 + slot]
     for (;;) {
-        if (tid == 0) {
-            ctl[0] = 0;
-            ctl[1] = kLat32Inf;
-        }
-        __syncthreads();
         uint32_t thr = kLat32Inf;
-        if (use_delta) {
+        uint32_t mnext = kLat32Inf;   // fused: lowest latency active after this sweep (this lane)
+        if (fused) {
+            const uint32_t lo = sweeps == 0 ? 0u : ctl[1 + (slot + 2) % 3];
+            if (lo == kLat32Inf) break;  // no active node anywhere
+            if (tid == 0) ctl[1 + (slot + 1) % 3] = kLat32Inf;
+            thr = lo + delta < lo ? kLat32Inf - 1 : lo + delta;
+        } else {
+            if (tid == 0) {
+                ctl[0] = 0;
+                ctl[1] = kLat32Inf;
+            }
+            __syncthreads();
+        }
+        if (use_delta && !fused) {
             uint32_t m = kLat32Inf;
             for (uint32_t widx = wave; widx < W; widx += NW) {
                 const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -290,7 +378,11 @@ __device__ __forceinline__ void sssp_row(
                 const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (word != 0) {  // wave-uniform
                     bool sel = lane < 32 && ((word >> lane) & 1u);
-                    if (use_delta && sel) sel = act_key(widx * 32 + lane) <= thr;
+                    if (use_delta && sel) {
+                        const uint32_t key = act_key(widx * 32 + lane);
+                        sel = key <= thr;
+                        if (!sel) mnext = min(mnext, key);
+                    }
                     const uint32_t mask = (uint32_t)__ballot(sel);
                     if (mask) {
                         // words are owned by one wave; other waves only set bits: clearing is exact
@@ -305,15 +397,29 @@ __device__ __forceinline__ void sssp_row(
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 expanded += qn;
-                if (GLAB && flat) {
-                    expand_flat(q, qn, lane, lab, bits, abeg, aend, arcs, flat + wave * kFlatWords, ovf, dirty,
-                                bkt, inv_delta);
+                if (flat) {
+                    expand_flat<GLAB>(q, qn, lane, lab, bits, CACHE ? rng : nullptr, abeg, aend, arcs,
+                                      flat + wave * kFlatWords, ovf, dirty, bkt, inv_delta, V + lane);
                 } else {
                     for (uint32_t t = 0; t < qn; t += NG) {
                         const uint32_t qi = t + grp;
-                        if (qi < qn)
-                            relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
-                                                          ovf, dirty, bkt, inv_delta);
+                        if (qi >= qn) continue;
+                        if constexpr (!GLAB && kArcPad % (G * 8) == 0) {
+                            if (lat_guard && pad_r == 8) {   // a whole 64-slot list per group step
+                                relax_node_pad<G, 8, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, lat_guard,
+                                                            ovf, dirty, mnext);
+                                continue;
+                            }
+                        }
+                        if constexpr (!GLAB && kArcPad % (G * R) == 0) {
+                            if (lat_guard) {
+                                relax_node_pad<G, R, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, lat_guard,
+                                                            ovf, dirty, mnext);
+                                continue;
+                            }
+                        }
+                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
+                                                      ovf, dirty, bkt, inv_delta, mnext);
                     }
                 }
                 qn = 0;
@@ -322,7 +428,12 @@ __device__ __forceinline__ void sssp_row(
             if (!more) break;
         }
         ++sweeps;
-        if (!use_delta) {
+        if (fused) {
+            for (int o = 32; o > 0; o >>= 1) mnext = min(mnext, (uint32_t)__shfl_xor((int)mnext, o));
+            if (lane == 0 && mnext != kLat32Inf) atomicMin(&ctl[1 + slot], mnext);
+            __syncthreads();
+            slot = slot == 2 ? 0 : slot + 1;
+        } else if (!use_delta) {
             if (dirty) ctl[0] = 1;
             __syncthreads();
             const bool again = ctl[0] != 0;
@@ -412,7 +523,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
-    uint32_t seed_stride, uint32_t* __restrict__ nh_out) {
+    uint32_t seed_stride, uint32_t* __restrict__ nh_out, uint32_t use_flat, uint32_t lat_guard, uint32_t pad_r) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr uint32_t NW = BLOCK / 64;
     uint64_t* lab = reinterpret_cast<uint64_t*>(smem);   // V labels + 64 per-lane scratch labels
@@ -420,15 +531,17 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V + 64);
     uint32_t* ctl = bits + W;            // [0] dirty  [1] min active latency
     uint32_t* wq = ctl + 4;              // per-wave queue (kQCap + 32 node ids)
-    // [V] arc range {beg, end}, 8-byte aligned after the queues
+    uint32_t* flat = use_flat ? wq + NW * (kQCap + 32) : nullptr;   // per-wave expand_flat scratch
+    // [V] arc range {beg, end}, 8-byte aligned after the queues (and the flat scratch)
     const uint32_t rng_off =
-        (((uint32_t)((wq + NW * (kQCap + 32)) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
+        (((uint32_t)((wq + NW * (kQCap + 32 + (use_flat ? kFlatWords : 0))) - reinterpret_cast<uint32_t*>(smem)) * 4u) +
+         7u) & ~7u;
     uint2* rng = reinterpret_cast<uint2*>(smem + rng_off);
     sssp_row<BLOCK, G, R, CACHE, false>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
                                         row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
                                         diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
-                                        delta, stats, seed_lat, seed_stride, nullptr, nullptr, nh_out,
-                                        reinterpret_cast<uint32_t*>(smem + rng_off));
+                                        delta, stats, seed_lat, seed_stride, nullptr, flat, nh_out,
+                                        reinterpret_cast<uint32_t*>(smem + rng_off), lat_guard, pad_r);
 }
 
 // Kernel 1b: labels in global memory, for graphs whose labels do not fit the LDS (C4: 50k
@@ -459,7 +572,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
                                            n_used, row, (size_t)(row - row_begin) * n_used,
                                            diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
                                            delta, stats, nullptr, 0, bkt, flat, nh_out,
-                                           gpred ? gpred + (size_t)blockIdx.x * V : nullptr);
+                                           gpred ? gpred + (size_t)blockIdx.x * V : nullptr, 0u, 0u);
         __syncthreads();   // the next row re-initialises labels and bitmap
     }
 }
@@ -480,13 +593,6 @@ __global__ __launch_bounds__(256) void arcs_pack(const uint32_t* __restrict__ ds
 // over the K lowest-latency neighbours of u (any subset is sound; the nearest catch almost
 // all: C2 keeps ~49 of 999 arcs per node with K = 32).  Ties (detour == arc) are kept.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void dense_init(uint64_t* __restrict__ Wk, uint64_t nn,
-                                                  uint32_t* __restrict__ cursor) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < nn) Wk[i] = kKeyInf;
-    if (i == 0) *cursor = 0;   // prune_rows' output cursor
-}
-
 // per-build flags (one launch instead of three memsets): [0,16) overflow / misc = 0,
 // [16,24) first unreachable pair = ~0, [24,64) = 0 (stats counters at 32)
 __global__ __launch_bounds__(64) void flags_init(uint32_t* __restrict__ f) {
@@ -494,27 +600,37 @@ __global__ __launch_bounds__(64) void flags_init(uint32_t* __restrict__ f) {
     if (t < 16) f[t] = (t == 4 || t == 5) ? 0xFFFFFFFFu : 0u;
 }
 
-// one workgroup per row u: lexicographic min over parallel arcs into the dense key matrix
-__global__ __launch_bounds__(256) void dense_scatter(const uint32_t* __restrict__ off,
-                                                     const uint32_t* __restrict__ adst,
-                                                     const uint32_t* __restrict__ alat,
-                                                     const float* __restrict__ aloss, uint32_t V,
-                                                     uint64_t* __restrict__ Wk) {
-    const uint32_t u = blockIdx.x;
-    for (uint32_t k = off[u] + threadIdx.x; k < off[u + 1]; k += 256)
-        atomicMin(reinterpret_cast<unsigned long long*>(&Wk[(size_t)u * V + adst[k]]),
-                  (unsigned long long)pack_key(alat[k], aloss[k]));
-}
-
-__global__ __launch_bounds__(256) void dense_lat(const uint64_t* __restrict__ Wk,
-                                                 uint32_t* __restrict__ Wl, uint64_t nn) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < nn) Wl[i] = key_lat(Wk[i]);
+// One workgroup per row u: the row's arc keys (parallel arcs folded by a lexicographic LDS
+// atomicMin) built in LDS and written once as the key row Wk and the latency row Wl -- one
+// pass instead of init + global-atomic scatter + a latency-extract pass (C2: 16 -> 7 us).
+// (A u16 latency row rounded up -- sound for the prune, half the gathered bytes -- measured
+// slower: prune_rows 32 -> 57 us, the decode outweighing the bytes.)
+__global__ __launch_bounds__(256) void dense_build(const uint32_t* __restrict__ off,
+                                                   const uint32_t* __restrict__ adst,
+                                                   const uint32_t* __restrict__ alat,
+                                                   const float* __restrict__ aloss, uint32_t V,
+                                                   uint64_t* __restrict__ Wk, uint32_t* __restrict__ Wl,
+                                                   uint32_t* __restrict__ cursor) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t* rowk = reinterpret_cast<uint64_t*>(smem);
+    const uint32_t u = blockIdx.x, tid = threadIdx.x;
+    for (uint32_t v = tid; v < V; v += 256) rowk[v] = kKeyInf;
+    if (u == 0 && tid == 0) *cursor = 0;   // prune_rows' output cursor
+    __syncthreads();
+    for (uint32_t k = off[u] + tid; k < off[u + 1]; k += 256)
+        atomicMin(reinterpret_cast<unsigned long long*>(&rowk[adst[k]]), (unsigned long long)pack_key(alat[k], aloss[k]));
+    __syncthreads();
+    const size_t base = (size_t)u * V;
+    for (uint32_t v = tid; v < V; v += 256) {
+        const uint64_t k = rowk[v];
+        Wk[base + v] = k;
+        Wl[base + v] = key_lat(k);
+    }
 }
 
 template <int BLOCK, int K>
 __global__ __launch_bounds__(BLOCK) void prune_rows(
-    const uint32_t* __restrict__ Wl, const uint64_t* __restrict__ Wk, uint32_t V, uint32_t P,
+    const uint32_t* __restrict__ Wl, const uint64_t* __restrict__ Wk, uint32_t V,
     uint32_t* __restrict__ pbeg, uint32_t* __restrict__ pend, uint4* __restrict__ parcs,
     uint32_t* __restrict__ cursor) {
     // Detour nodes x: ~K of u's lowest-latency neighbours, chosen by a 256-bin latency histogram
@@ -528,10 +644,11 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
     uint32_t* hist = cnt + 8;                          // 256 bins
     uint32_t* selx = hist + 256;                       // K detour nodes
     uint32_t* sela = selx + K;                         // their latencies
-    uint16_t* binv = reinterpret_cast<uint16_t*>(sela + K);   // bin per node (0xFFFF: no arc)
+    uint32_t* row = sela + K;                          // u's exact arc latencies
+    uint16_t* binv = reinterpret_cast<uint16_t*>(row + V);   // bin per node (0xFFFF: no arc)
     const uint32_t u = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const uint32_t* row = Wl + (size_t)u * V;
-    (void)P;
+    const size_t base = (size_t)u * V;
+    for (uint32_t v = tid; v < V; v += BLOCK) row[v] = key_lat(Wk[base + v]);
     for (uint32_t i = tid; i < 256; i += BLOCK) hist[i] = 0;
     if (tid < 8) cnt[tid] = 0;
     uint32_t mx = 0;
@@ -624,37 +741,64 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
     }
     if (tid == 0) cnt[0] = 0;
     __syncthreads();
-    const size_t base = (size_t)u * V;
-    constexpr int KC = K < 32 ? K : 32;   // detours per batch of loads in flight
-    for (uint32_t v = tid; v < V; v += BLOCK) {  // 2-hop test of every arc of u
-        const uint32_t w = row[v];
-        if (w == kLat32Inf) continue;
-        uint32_t z = kLat32Inf;
-        for (int j0 = 0; j0 < K && w <= z; j0 += KC) {   // stop once a strict detour is found
-            uint32_t bv[KC], as[KC];
+    // 2-hop test of every arc of u: each thread tests VB arcs at once against batches of KB
+    // detours (VB x KB loads in flight), and a lane stops loading for an arc as soon as a
+    // strictly shorter detour is found -- most arcs of a dense row fall to the first batch
+    constexpr int VB = 4, KB = 8;
+    for (uint32_t v0 = tid; v0 < V; v0 += BLOCK * VB) {
+        uint32_t w[VB], z[VB];
 #pragma unroll
-            for (int j = 0; j < KC; ++j) {   // the batch's detour loads in flight together
-                as[j] = sela[j0 + j];
-                bv[j] = as[j] != kLat32Inf ? Wl[(size_t)selx[j0 + j] * V + v] : kLat32Inf;
-            }
-#pragma unroll
-            for (int j = 0; j < KC; ++j) {
-                const uint32_t t = as[j] + bv[j];
-                if (as[j] != kLat32Inf && bv[j] != kLat32Inf && t >= as[j]) z = min(z, t);
-            }
+        for (int i = 0; i < VB; ++i) {
+            const uint32_t v = v0 + i * BLOCK;
+            w[i] = v < V ? row[v] : kLat32Inf;
+            z[i] = kLat32Inf;
         }
-        if (w <= z) {
+        for (int j0 = 0; j0 < K; j0 += KB) {
+            bool any = false;
+#pragma unroll
+            for (int i = 0; i < VB; ++i) any |= w[i] != kLat32Inf && w[i] <= z[i];
+            if (!any) break;
+            uint32_t as[KB], bv[VB][KB];
+            size_t xb[KB];
+#pragma unroll
+            for (int j = 0; j < KB; ++j) {
+                as[j] = sela[j0 + j];
+                xb[j] = (size_t)selx[j0 + j] * V;
+            }
+#pragma unroll
+            for (int i = 0; i < VB; ++i) {
+                const bool live = w[i] != kLat32Inf && w[i] <= z[i];
+#pragma unroll
+                for (int j = 0; j < KB; ++j)
+                    bv[i][j] = live && as[j] != kLat32Inf ? Wl[xb[j] + v0 + i * BLOCK] : kLat32Inf;
+            }
+#pragma unroll
+            for (int i = 0; i < VB; ++i)
+#pragma unroll
+                for (int j = 0; j < KB; ++j) {
+                    const uint32_t t = as[j] + bv[i][j];
+                    if (as[j] != kLat32Inf && bv[i][j] != kLat32Inf && t >= as[j]) z[i] = min(z[i], t);
+                }
+        }
+#pragma unroll
+        for (int i = 0; i < VB; ++i) {
+            if (w[i] == kLat32Inf || w[i] > z[i]) continue;
+            const uint32_t v = v0 + i * BLOCK;
             const uint32_t slot = atomicAdd(&cnt[0], 1u);
             const uint64_t key = Wk[base + v];
-            kept[slot] = make_uint4(v, w, __float_as_uint(one_minus(key_loss(key))), 0u);
+            kept[slot] = make_uint4(v, w[i], __float_as_uint(one_minus(key_loss(key))), 0u);
         }
     }
     __syncthreads();
-    // rows land contiguously (in any row order) so the kept arcs stay dense in L2
-    if (tid == 0) cnt[1] = atomicAdd(cursor, cnt[0]);
+    // rows land contiguously (in any row order) so the kept arcs stay dense in L2; each list is
+    // padded to kArcPad slots with no-op arcs for relax_node_pad (scratch label V + i, lat 0,
+    // q 0: candidate (lu, 1.0f) against a scratch label holding 0)
+    const uint32_t n = cnt[0], np = (n + kArcPad - 1) / kArcPad * kArcPad;
+    if (tid == 0) cnt[1] = atomicAdd(cursor, np);
     __syncthreads();
-    const uint32_t n = cnt[0], at = cnt[1];
-    for (uint32_t i = tid; i < n; i += BLOCK) parcs[at + i] = kept[i];
+    const uint32_t at = cnt[1];
+    for (uint32_t i = tid; i < np; i += BLOCK)
+        parcs[at + i] = i < n ? kept[i] : make_uint4(V + (i & 63u), 0u, 0u, 0u);
     if (tid == 0) {
         pbeg[u] = at;
         pend[u] = at + n;
@@ -836,7 +980,7 @@ struct HostGraph {
     std::vector<float> loss;
     std::vector<uint64_t> diag_lat;      // per used index
     std::vector<float> diag_loss;
-    uint64_t max_arc_lat = 0;
+    uint64_t max_arc_lat = 0, min_arc_lat = 0;
     double sum_arc_lat = 0;
 };
 
@@ -912,12 +1056,14 @@ static void build_csr(const shd_graph* g, bool reverse, HostGraph& H) {
     H.loss.resize(A);
     std::vector<uint32_t> fill(H.off.begin(), H.off.end() - 1);
     H.max_arc_lat = 0;
+    H.min_arc_lat = ~0ull;
     for (uint32_t i = 0; i < g->n_edges; i++) {
         const uint32_t a = g->edge_src[i], b = g->edge_dst[i];
         if (a == b) continue;
         const uint64_t l = g->edge_latency_ns[i];
         const float p = g->edge_packet_loss[i] + 0.0f;  // -0.0 -> +0.0: same fold, ordered bits
         H.max_arc_lat = std::max(H.max_arc_lat, l);
+        H.min_arc_lat = std::min(H.min_arc_lat, l);
         H.sum_arc_lat += l;
         auto put = [&](uint32_t from, uint32_t to) {
             const uint32_t k = fill[from]++;
@@ -1068,6 +1214,7 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
         P.narrow_arcs = H.max_arc_lat < kLat32Inf;
         P.mean_arc_lat = H.dst.empty() ? 1u
                          : (uint32_t)std::min<double>(kLat32Inf - 1, H.sum_arc_lat / H.dst.size());
+        P.min_arc_lat = H.dst.empty() ? 1u : (uint32_t)std::min<uint64_t>(kLat32Inf - 1, std::max<uint64_t>(H.min_arc_lat, 1));
         if (P.narrow_arcs) {
             std::vector<uint32_t> l32(H.lat.begin(), H.lat.end());
             SHD_TRY(upload(ctx->g_off, H.off, s));
@@ -1130,51 +1277,61 @@ static shd_status run_direct(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d
     return SHD_OK;
 }
 
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+    const char* v = std::getenv(name);
+    return v && *v ? (uint32_t)std::strtoul(v, nullptr, 10) : dflt;
+}
+
 struct ArcView {
     const uint32_t *beg, *end;
     const uint4* arcs;
     uint64_t n_arcs;
+    bool padded = false;   // lists padded to kArcPad slots with no-op arcs (prune_rows)
 };
 
 template <int BLOCK, int G, bool CACHE>
 static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, size_t lds,
                          uint64_t* d_lat, float* d_loss, uint32_t delta, const uint32_t* seed,
-                         uint32_t seed_stride) {
+                         uint32_t seed_stride, uint32_t flat) {
     PreparedGraph& P = ctx->prep;
     constexpr int R = G >= 32 ? 2 : G == 4 ? 2 : 4;   // arcs in flight per lane (R = 6, 8 at G = 8 measured slower on C2)
+    // padded lists: labels stay below 2^32 - 1 while lu <= guard (0 = unpadded path)
+    const uint64_t guard = (uint64_t)kLat32Inf - 1 - P.max_arc_lat;
+    const uint32_t lat_guard =
+        A.padded && kArcPad % (G * R) == 0 && P.max_arc_lat < kLat32Inf - 1 && env_u32("SHD_SSSP_NO_PAD", 0) != 1
+            ? (uint32_t)std::max<uint64_t>(guard, 1)
+            : 0u;
     sssp_lds_group<BLOCK, G, R, CACHE><<<re - rb, BLOCK, lds, ctx->stream>>>(
         A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
         ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
         delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
-        seed, seed_stride, ctx->nh_out ? ctx->nh_out + (size_t)0 : nullptr);
+        seed, seed_stride, ctx->nh_out ? ctx->nh_out + (size_t)0 : nullptr, flat, lat_guard,
+        env_u32("SHD_SSSP_PAD_R", 8));
 }
 
-static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
-    // labels + bitmap + control + per-wave queues (+ arc ranges, 8-byte aligned)
-    const size_t head = (size_t)(V + 64) * 8 + (size_t)((V + 31) / 32) * 4 + 16 + (block / 64) * 96 * 4;
+static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache, bool flat = false) {
+    // labels + bitmap + control + per-wave queues (+ flat scratch) (+ arc ranges, 8-byte aligned)
+    const size_t head = (size_t)(V + 64) * 8 + (size_t)((V + 31) / 32) * 4 + 16 +
+                        (block / 64) * (kQCap + 32 + (flat ? kFlatWords : 0)) * 4;
     return cache ? ((head + 7) & ~(size_t)7) + (size_t)V * 8 : head;
 }
 
 template <int BLOCK, bool CACHE>
 static void launch_by_degree(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint64_t* d_lat,
                              float* d_loss, uint32_t delta, uint32_t G, const uint32_t* seed,
-                             uint32_t ss) {
-    size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK, CACHE);
+                             uint32_t ss, uint32_t flat) {
+    size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK, CACHE, flat != 0);
     if (ctx->nh_out && !CACHE) lds = ((lds + 7) & ~(size_t)7) + (size_t)ctx->prep.V * 4;   // pred[V]
     switch (G) {
-        case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
-        case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
-        case 16: launch_group<BLOCK, 16, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
-        case 8: launch_group<BLOCK, 8, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
-        default: launch_group<BLOCK, 4, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
+        case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
+        case 16: launch_group<BLOCK, 16, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
+        case 8: launch_group<BLOCK, 8, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
+        default: launch_group<BLOCK, 4, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
     }
 }
 
-static uint32_t env_u32(const char* name, uint32_t dflt) {
-    const char* v = std::getenv(name);
-    return v && *v ? (uint32_t)std::strtoul(v, nullptr, 10) : dflt;
-}
 
 static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re,
                            uint64_t* d_lat, float* d_loss, uint32_t delta, bool* ovf,
@@ -1197,24 +1354,31 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
                      : rows_per_cu <= 1 ? 1024 : rows_per_cu <= 2 ? 512 : 256;
     block = env_u32("SHD_SSSP_BLOCK", block);
     if (block != 256 && block != 512 && block != 1024) block = 256;
-    const bool cache = sssp_lds_bytes(P.V, block, true) <= ctx->max_lds;
+    // edge-parallel expansion (expand_flat) when its per-wave scratch fits beside the labels:
+    // off by default here -- with LDS labels the kernel is issue-bound, and the owner search
+    // of expand_flat costs more instructions than the dead group slots it removes
+    uint32_t flat = env_u32("SHD_SSSP_FLAT_LDS", 0) != 0;
+    const size_t nh_extra = ctx->nh_out ? (size_t)P.V * 4 + 8 : 0;
+    if (flat && sssp_lds_bytes(P.V, block, false, true) + nh_extra > ctx->max_lds) flat = 0;
+    const bool cache = sssp_lds_bytes(P.V, block, true, flat != 0) <= ctx->max_lds;
     SHD_HIP(hipEventRecord(ctx->ev[2], s));
     if (block == 1024) {
-        if (cache) launch_by_degree<1024, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
-        else launch_by_degree<1024, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
+        if (cache) launch_by_degree<1024, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
+        else launch_by_degree<1024, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
     } else if (block == 512) {
-        if (cache) launch_by_degree<512, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
-        else launch_by_degree<512, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
+        if (cache) launch_by_degree<512, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
+        else launch_by_degree<512, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
     } else {
-        if (cache) launch_by_degree<256, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
-        else launch_by_degree<256, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
+        if (cache) launch_by_degree<256, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
+        else launch_by_degree<256, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
     }
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(ctx->ev[3], s));
     (void)ovf;   // the caller reads the overflow flag with read_flags()
     if (ctx->stats_on) {
         unsigned long long st[2];
-        SHD_HIP(hipMemcpy(st, ctx->g_flags.as<char>() + 32, 16, hipMemcpyDeviceToHost));
+        SHD_HIP(hipMemcpyAsync(st, ctx->g_flags.as<char>() + 32, 16, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipStreamSynchronize(s));
         std::fprintf(stderr, "shd_sssp: rows=%u G=%u block=%u delta=%u expanded=%llu (%.2f per node) "
                      "sweeps=%llu (%.1f per row) arcs=%llu\n", re - rb, G, block, delta, st[0],
                      (double)st[0] / ((double)(re - rb) * P.V), st[1], (double)st[1] / (re - rb),
@@ -1328,33 +1492,27 @@ static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
     hipStream_t s = ctx->stream;
     const uint32_t V = P.V;
     const uint64_t nn = (uint64_t)V * V;
-    uint32_t Pw = 1;
-    while (Pw < V) Pw <<= 1;
     SHD_TRY(ctx->g_dense.ensure(nn * 8));
     SHD_TRY(ctx->g_labels.ensure(nn * 4));
-    SHD_TRY(ctx->g_prune_dst.ensure(nn * 16));
+    SHD_TRY(ctx->g_prune_dst.ensure((nn + (uint64_t)V * kArcPad) * 16));   // + list padding
     SHD_TRY(ctx->g_prune_cnt.ensure((size_t)V * 8 + 16));
     uint64_t* Wk = ctx->g_dense.as<uint64_t>();
     uint32_t* Wl = ctx->g_labels.as<uint32_t>();
     uint32_t* pbeg = ctx->g_prune_cnt.as<uint32_t>();
     uint32_t* pend = pbeg + V;
     uint32_t* cursor = pend + V;
-    dense_init<<<div_up(nn, 256), 256, 0, s>>>(Wk, nn, cursor);
-    dense_scatter<<<V, 256, 0, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
-                                    ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wk);
-    dense_lat<<<div_up(nn, 256), 256, 0, s>>>(Wk, Wl, nn);
+    uint4* pa = ctx->g_prune_dst.as<uint4>();
+    dense_build<<<V, 256, (size_t)V * 8, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
+                                              ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wk, Wl, cursor);
     const char* pk = std::getenv("SHD_PRUNE_K");   // tuning: detour nodes per row (same output tables)
     const uint32_t Kr = pk && *pk ? (uint32_t)std::atoi(pk) : kPruneK;
     const uint32_t K = Kr >= 128 ? 128u : Kr >= 64 ? 64u : 32u;
-    const size_t plds = (size_t)V * 18 + (8 + 256 + 2 * (size_t)K) * 4;
-    if (K >= 128)
-        prune_rows<256, 128><<<V, 256, plds, s>>>(Wl, Wk, V, Pw, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor);
-    else if (K >= 64)
-        prune_rows<256, 64><<<V, 256, plds, s>>>(Wl, Wk, V, Pw, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor);
-    else
-        prune_rows<256, 32><<<V, 256, plds, s>>>(Wl, Wk, V, Pw, pbeg, pend, ctx->g_prune_dst.as<uint4>(), cursor);
+    const size_t plds = (size_t)V * 22 + (8 + 256 + 2 * (size_t)K) * 4;
+    if (K >= 128) prune_rows<256, 128><<<V, 256, plds, s>>>(Wl, Wk, V, pbeg, pend, pa, cursor);
+    else if (K >= 64) prune_rows<256, 64><<<V, 256, plds, s>>>(Wl, Wk, V, pbeg, pend, pa, cursor);
+    else prune_rows<256, 32><<<V, 256, plds, s>>>(Wl, Wk, V, pbeg, pend, pa, cursor);
     SHD_HIP(hipGetLastError());
-    *out = ArcView{pbeg, pend, ctx->g_prune_dst.as<uint4>(), 0};
+    *out = ArcView{pbeg, pend, ctx->g_prune_dst.as<uint4>(), 0, true};
     return SHD_OK;
 }
 
@@ -1377,7 +1535,6 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
     if (!P.ready) return SHD_ERR_STATE;
     if (re == 0) re = P.n_used;
     if (rb >= re || re > P.n_used) return SHD_ERR_INVALID;
-    hipStream_t s = ctx->stream;
     ctx->info = shd_routing_info{};
     ctx->info.arcs = P.arcs;
     ctx->info.arcs_kept = P.arcs;
@@ -1401,7 +1558,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         bool ovf = false;
         SHD_TRY(run_blocked(ctx, rb, re, d_lat, d_loss, &ovf));
         ctx->info.algo_used = SHD_ALGO_BLOCKED;
-                SHD_TRY(read_flags(ctx));
+        SHD_TRY(read_flags(ctx));
         ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;
         ms = call_ms();
@@ -1430,13 +1587,20 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
             A.n_arcs = P.pruned_arcs ? P.pruned_arcs : (uint64_t)P.V * 64;
         }
         bool ovf = false;
-        // delta-stepping bucket width: the mean kept-arc latency (env override for tuning)
+        // delta-stepping bucket width (env override for tuning).  SHD_ALGO_DELTA: the mean arc
+        // latency.  AUTO on a pruned dense graph: the smallest arc latency (never pruned: every
+        // detour has two arcs), floored at mean/256 so that a stray tiny arc cannot make the
+        // sweep count explode -- a bucket no wider than every arc settles in one sweep, so each
+        // node is expanded once (Dial order); the sweep jumps to the smallest active label, so
+        // empty buckets cost nothing.  C2: 1 ms -> main kernel 172 -> 120 us, tables identical.
         uint32_t delta = kLat32Inf;
         if (algo == SHD_ALGO_DELTA) delta = env_u32("SHD_SSSP_DELTA", P.mean_arc_lat);
+        else if (algo == SHD_ALGO_AUTO && prune && env_u32("SHD_SSSP_NO_DELTA", 0) != 1)
+            delta = env_u32("SHD_SSSP_DELTA", std::max(P.min_arc_lat, P.mean_arc_lat / 256));
         SHD_TRY(run_sssp(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
         ctx->info.algo_used = algo == SHD_ALGO_DELTA ? SHD_ALGO_DELTA
                               : prune ? SHD_ALGO_PRUNED : SHD_ALGO_SSSP;
-                SHD_TRY(read_flags(ctx));
+        SHD_TRY(read_flags(ctx));
         ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;
         ms = call_ms();
@@ -1457,7 +1621,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
                   P.arcs};
         SHD_TRY(run_sssp_global(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
         ctx->info.algo_used = algo == SHD_ALGO_DELTA ? SHD_ALGO_DELTA : SHD_ALGO_SSSP;
-                SHD_TRY(read_flags(ctx));
+        SHD_TRY(read_flags(ctx));
         ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;
         ms = call_ms();

@@ -1,0 +1,36 @@
+"""Tuning probe for the C2 build: time every engine / knob combination on the 1k-node complete
+graph (tables checked identical).  SHD_SSSP_STATS=1 prints sweeps and expansions."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import prepare, run_rows  # noqa: E402
+from shadow_amd import synth  # noqa: E402
+from shadow_amd.routing import Engine  # noqa: E402
+
+eng = Engine(0)
+el = synth.complete_graph(1000, 1)
+n = prepare(eng, el)
+lat = torch.empty((n, n), dtype=torch.int64, device="cuda")
+loss = torch.empty((n, n), dtype=torch.float32, device="cuda")
+ref = None
+for spec in sys.argv[1:]:           # "algo[:ENV=val,ENV=val]"
+    algo, _, envs = spec.partition(":")
+    for kv in filter(None, envs.split(",")):
+        k, v = kv.split("=")
+        os.environ[k] = v
+    ms = []
+    for rep in range(8):
+        run_rows(eng, int(algo), 0, n, lat, loss)
+        ms.append(eng.last_info()["ms_main"])
+    h = (int(lat.sum().item()), int(loss.view(torch.int32).to(torch.int64).sum().item()))
+    ref = ref or h
+    i = eng.last_info()
+    print(f"{spec:40s} main_us={np.median(ms) * 1e3:7.1f} total_us={i['ms_total'] * 1e3:7.1f} kept={i['arcs_kept']} "
+          f"same={h == ref}", flush=True)
+    for kv in filter(None, envs.split(",")):
+        os.environ.pop(kv.split("=")[0])
