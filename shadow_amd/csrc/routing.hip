@@ -273,7 +273,7 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
 }
 
 // One source row: init, sweeps until nothing improves, emit the used columns.
-template <int BLOCK, int G, int R, bool CACHE, bool GLAB>
+template <int BLOCK, int G, int R, bool CACHE, bool GLAB, int PADR = 0>
 __device__ __forceinline__ void sssp_row(
     uint64_t* lab, uint32_t* bits, uint32_t* ctl, uint32_t* wq, uint2* rng,
     const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
@@ -284,7 +284,7 @@ __device__ __forceinline__ void sssp_row(
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
     uint32_t seed_stride, uint8_t* bkt, uint32_t* flat, uint32_t* nh_out, uint32_t* pred,
-    uint32_t lat_guard, uint32_t pad_r) {
+    uint32_t lat_guard) {
     // bkt (global labels + delta-stepping): per node, the bucket of the latency that last
     // activated it, in LDS, so choosing a sweep's nodes reads no global label
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
@@ -397,29 +397,28 @@ __device__ __forceinline__ void sssp_row(
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 expanded += qn;
-                if (flat) {
-                    expand_flat<GLAB>(q, qn, lane, lab, bits, CACHE ? rng : nullptr, abeg, aend, arcs,
-                                      flat + wave * kFlatWords, ovf, dirty, bkt, inv_delta, V + lane);
+                if constexpr (GLAB) {
+                    if (flat) {
+                        expand_flat<GLAB>(q, qn, lane, lab, bits, nullptr, abeg, aend, arcs, flat + wave * kFlatWords,
+                                          ovf, dirty, bkt, inv_delta, V + lane);
+                    } else {
+                        for (uint32_t t = 0; t < qn; t += NG) {
+                            const uint32_t qi = t + grp;
+                            if (qi < qn)
+                                relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
+                                                              ovf, dirty, bkt, inv_delta, mnext);
+                        }
+                    }
                 } else {
                     for (uint32_t t = 0; t < qn; t += NG) {
                         const uint32_t qi = t + grp;
                         if (qi >= qn) continue;
-                        if constexpr (!GLAB && kArcPad % (G * 8) == 0) {
-                            if (lat_guard && pad_r == 8) {   // a whole 64-slot list per group step
-                                relax_node_pad<G, 8, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, lat_guard,
-                                                            ovf, dirty, mnext);
-                                continue;
-                            }
-                        }
-                        if constexpr (!GLAB && kArcPad % (G * R) == 0) {
-                            if (lat_guard) {
-                                relax_node_pad<G, R, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, lat_guard,
-                                                            ovf, dirty, mnext);
-                                continue;
-                            }
-                        }
-                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
-                                                      ovf, dirty, bkt, inv_delta, mnext);
+                        if constexpr (PADR != 0)   // padded lists: a whole 64-slot list per group step
+                            relax_node_pad<G, PADR, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, lat_guard,
+                                                           ovf, dirty, mnext);
+                        else
+                            relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
+                                                          ovf, dirty, bkt, inv_delta, mnext);
                     }
                 }
                 qn = 0;
@@ -514,7 +513,8 @@ __device__ __forceinline__ void sssp_row(
 }
 
 // Kernel 1: one workgroup per source row, labels (8 B/node) and the arc ranges in LDS.
-template <int BLOCK, int G, int R, bool CACHE>
+// PADR = 8: padded arc lists (prune_rows), relax_node_pad with 8 arcs per lane per step.
+template <int BLOCK, int G, int R, bool CACHE, int PADR>
 __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
     const uint4* __restrict__ arcs, uint32_t V, const uint32_t* __restrict__ used,
@@ -523,25 +523,23 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
-    uint32_t seed_stride, uint32_t* __restrict__ nh_out, uint32_t use_flat, uint32_t lat_guard, uint32_t pad_r) {
+    uint32_t seed_stride, uint32_t* __restrict__ nh_out, uint32_t lat_guard) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr uint32_t NW = BLOCK / 64;
     uint64_t* lab = reinterpret_cast<uint64_t*>(smem);   // V labels + 64 per-lane scratch labels
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V + 64);
-    uint32_t* ctl = bits + W;            // [0] dirty  [1] min active latency
+    uint32_t* ctl = bits + W;            // [0] dirty  [1..3] min active latency
     uint32_t* wq = ctl + 4;              // per-wave queue (kQCap + 32 node ids)
-    uint32_t* flat = use_flat ? wq + NW * (kQCap + 32) : nullptr;   // per-wave expand_flat scratch
-    // [V] arc range {beg, end}, 8-byte aligned after the queues (and the flat scratch)
+    // [V] arc range {beg, end}, 8-byte aligned after the queues
     const uint32_t rng_off =
-        (((uint32_t)((wq + NW * (kQCap + 32 + (use_flat ? kFlatWords : 0))) - reinterpret_cast<uint32_t*>(smem)) * 4u) +
-         7u) & ~7u;
+        (((uint32_t)((wq + NW * (kQCap + 32)) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
     uint2* rng = reinterpret_cast<uint2*>(smem + rng_off);
-    sssp_row<BLOCK, G, R, CACHE, false>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
-                                        row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
-                                        diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
-                                        delta, stats, seed_lat, seed_stride, nullptr, flat, nh_out,
-                                        reinterpret_cast<uint32_t*>(smem + rng_off), lat_guard, pad_r);
+    sssp_row<BLOCK, G, R, CACHE, false, PADR>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
+                                              row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
+                                              diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
+                                              delta, stats, seed_lat, seed_stride, nullptr, nullptr, nh_out,
+                                              reinterpret_cast<uint32_t*>(smem + rng_off), lat_guard);
 }
 
 // Kernel 1b: labels in global memory, for graphs whose labels do not fit the LDS (C4: 50k
@@ -572,7 +570,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
                                            n_used, row, (size_t)(row - row_begin) * n_used,
                                            diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
                                            delta, stats, nullptr, 0, bkt, flat, nh_out,
-                                           gpred ? gpred + (size_t)blockIdx.x * V : nullptr, 0u, 0u);
+                                           gpred ? gpred + (size_t)blockIdx.x * V : nullptr, 0u);
         __syncthreads();   // the next row re-initialises labels and bitmap
     }
 }
@@ -1292,46 +1290,53 @@ struct ArcView {
 template <int BLOCK, int G, bool CACHE>
 static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, size_t lds,
                          uint64_t* d_lat, float* d_loss, uint32_t delta, const uint32_t* seed,
-                         uint32_t seed_stride, uint32_t flat) {
+                         uint32_t seed_stride) {
     PreparedGraph& P = ctx->prep;
     constexpr int R = G >= 32 ? 2 : G == 4 ? 2 : 4;   // arcs in flight per lane (R = 6, 8 at G = 8 measured slower on C2)
     // padded lists: labels stay below 2^32 - 1 while lu <= guard (0 = unpadded path)
     const uint64_t guard = (uint64_t)kLat32Inf - 1 - P.max_arc_lat;
     const uint32_t lat_guard =
-        A.padded && kArcPad % (G * R) == 0 && P.max_arc_lat < kLat32Inf - 1 && env_u32("SHD_SSSP_NO_PAD", 0) != 1
+        A.padded && P.max_arc_lat < kLat32Inf - 1 && env_u32("SHD_SSSP_NO_PAD", 0) != 1
             ? (uint32_t)std::max<uint64_t>(guard, 1)
             : 0u;
-    sssp_lds_group<BLOCK, G, R, CACHE><<<re - rb, BLOCK, lds, ctx->stream>>>(
+    uint32_t* flags = ctx->g_flags.as<uint32_t>();
+    auto* unreach = reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16);
+    auto* stats = ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr;
+    if constexpr (kArcPad % (G * 8) == 0) {
+        if (lat_guard) {
+            sssp_lds_group<BLOCK, G, R, CACHE, 8><<<re - rb, BLOCK, lds, ctx->stream>>>(
+                A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
+                ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss, flags, unreach, delta,
+                stats, seed, seed_stride, ctx->nh_out, lat_guard);
+            return;
+        }
+    }
+    sssp_lds_group<BLOCK, G, R, CACHE, 0><<<re - rb, BLOCK, lds, ctx->stream>>>(
         A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
-        ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
-        ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
-        delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
-        seed, seed_stride, ctx->nh_out ? ctx->nh_out + (size_t)0 : nullptr, flat, lat_guard,
-        env_u32("SHD_SSSP_PAD_R", 8));
+        ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss, flags, unreach, delta,
+        stats, seed, seed_stride, ctx->nh_out, 0u);
 }
 
-static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache, bool flat = false) {
-    // labels + bitmap + control + per-wave queues (+ flat scratch) (+ arc ranges, 8-byte aligned)
-    const size_t head = (size_t)(V + 64) * 8 + (size_t)((V + 31) / 32) * 4 + 16 +
-                        (block / 64) * (kQCap + 32 + (flat ? kFlatWords : 0)) * 4;
+static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
+    // labels + bitmap + control + per-wave queues (+ arc ranges, 8-byte aligned)
+    const size_t head = (size_t)(V + 64) * 8 + (size_t)((V + 31) / 32) * 4 + 16 + (block / 64) * (kQCap + 32) * 4;
     return cache ? ((head + 7) & ~(size_t)7) + (size_t)V * 8 : head;
 }
 
 template <int BLOCK, bool CACHE>
 static void launch_by_degree(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint64_t* d_lat,
                              float* d_loss, uint32_t delta, uint32_t G, const uint32_t* seed,
-                             uint32_t ss, uint32_t flat) {
-    size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK, CACHE, flat != 0);
+                             uint32_t ss) {
+    size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK, CACHE);
     if (ctx->nh_out && !CACHE) lds = ((lds + 7) & ~(size_t)7) + (size_t)ctx->prep.V * 4;   // pred[V]
     switch (G) {
-        case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
-        case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
-        case 16: launch_group<BLOCK, 16, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
-        case 8: launch_group<BLOCK, 8, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
-        default: launch_group<BLOCK, 4, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, flat); break;
+        case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        case 16: launch_group<BLOCK, 16, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        case 8: launch_group<BLOCK, 8, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        default: launch_group<BLOCK, 4, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
     }
 }
-
 
 static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re,
                            uint64_t* d_lat, float* d_loss, uint32_t delta, bool* ovf,
@@ -1354,23 +1359,20 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
                      : rows_per_cu <= 1 ? 1024 : rows_per_cu <= 2 ? 512 : 256;
     block = env_u32("SHD_SSSP_BLOCK", block);
     if (block != 256 && block != 512 && block != 1024) block = 256;
-    // edge-parallel expansion (expand_flat) when its per-wave scratch fits beside the labels:
-    // off by default here -- with LDS labels the kernel is issue-bound, and the owner search
-    // of expand_flat costs more instructions than the dead group slots it removes
-    uint32_t flat = env_u32("SHD_SSSP_FLAT_LDS", 0) != 0;
-    const size_t nh_extra = ctx->nh_out ? (size_t)P.V * 4 + 8 : 0;
-    if (flat && sssp_lds_bytes(P.V, block, false, true) + nh_extra > ctx->max_lds) flat = 0;
-    const bool cache = sssp_lds_bytes(P.V, block, true, flat != 0) <= ctx->max_lds;
+    // (edge-parallel expand_flat, as in the global-label kernel, measured slower here: the
+    // kernel is issue-bound and the owner search costs more than the dead group slots; C2
+    // 132 -> 197 us, so the LDS kernels keep node groups)
+    const bool cache = sssp_lds_bytes(P.V, block, true) <= ctx->max_lds;
     SHD_HIP(hipEventRecord(ctx->ev[2], s));
     if (block == 1024) {
-        if (cache) launch_by_degree<1024, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
-        else launch_by_degree<1024, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
+        if (cache) launch_by_degree<1024, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
+        else launch_by_degree<1024, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
     } else if (block == 512) {
-        if (cache) launch_by_degree<512, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
-        else launch_by_degree<512, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
+        if (cache) launch_by_degree<512, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
+        else launch_by_degree<512, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
     } else {
-        if (cache) launch_by_degree<256, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
-        else launch_by_degree<256, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss, flat);
+        if (cache) launch_by_degree<256, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
+        else launch_by_degree<256, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
     }
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(ctx->ev[3], s));
