@@ -92,6 +92,9 @@ def load_pmc(name):
     return None
 
 
+TIME_EVERY = 4   # routing builds per timed one (shd_routing_set_timing)
+
+
 def prepare(eng, el):
     from shadow_amd import _native as N
     from shadow_amd.routing import NetworkGraph
@@ -136,13 +139,18 @@ def sharded_build(eng, world, rank, n, algo, steps, warmup, keep=False, gather=T
         step()
     barrier_sync(world)
     infos = []
+    # the dominant kernel is timed (HIP events on its dispatch) on every 4th step of the timed
+    # region: each timed build pays a few microseconds of queue gap for its events
+    eng.lib.shd_routing_set_timing(eng.ctx, TIME_EVERY)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
         infos.append(eng.last_info())
     barrier_sync(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
-    out = dict(dt=dt, ms_per_step=dt / steps * 1e3, rows=re - rb, rb=rb, infos=infos)
+    eng.lib.shd_routing_set_timing(eng.ctx, 1)
+    out = dict(dt=dt, ms_per_step=dt / steps * 1e3, rows=re - rb, rb=rb, infos=infos,
+               kernel_ms=float(np.mean([i["ms_main"] for i in infos if i["ms_main"] >= 0] or [0.0])))
     if keep:
         k = n if (world == 1 or gather) else 0
         out["lat"] = lat[:k].cpu().numpy().view(np.uint64)
@@ -159,7 +167,7 @@ def routing_leg(eng, world, rank, steps, warmup):
     r = sharded_build(eng, world, rank, n, N.ALGO_AUTO, steps, warmup, keep=True)
     del r["lat_dev"], r["loss_dev"]
     info = r["infos"][-1]
-    kernel_ms = max_over_ranks(float(np.mean([i["ms_main"] for i in r["infos"]])), world)
+    kernel_ms = max_over_ranks(r["kernel_ms"], world)
     ops_per_launch = 2.0 * r["rows"] * info["arcs"]      # one add + one min per arc per source row
     achieved = ops_per_launch / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
     r.update(n=n, arcs=info["arcs"], kernel_ms=kernel_ms, achieved=achieved, algo=info["algo_used"],
@@ -276,7 +284,7 @@ def c4_leg(eng, world, rank, steps, gather=True, cpu=True):
     n = prepare(eng, el)
     gather = gather and world > 1
     r = sharded_build(eng, world, rank, n, N.ALGO_DELTA, steps, 0 if steps > 1 else 1, gather=gather)
-    kernel_ms = max_over_ranks(float(np.mean([i["ms_main"] for i in r["infos"]])), world)
+    kernel_ms = max_over_ranks(r["kernel_ms"], world)
     how = ("source rows sharded + RCCL all-gather of the table" if gather else
            "source rows sharded, shards resident (no all-gather)" if world > 1 else "1 GPU, whole table")
     arcs = int(r["infos"][-1]["arcs"])

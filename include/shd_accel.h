@@ -96,7 +96,8 @@ typedef struct shd_routing_info {
     uint64_t arcs;             /* arcs after parallel-edge reduction */
     uint64_t arcs_kept;        /* arcs after pruning (== arcs when no prune ran) */
     double ms_total;           /* device time of the last build (HIP events) */
-    double ms_main;            /* device time of the dominant kernel */
+    double ms_main;            /* device time of the dominant kernel; -1 when this call was not
+                                  timed (shd_routing_set_timing) */
     double ms_minplus;         /* SHD_ALGO_BLOCKED: device time of the min-plus closure */
 } shd_routing_info;
 
@@ -156,6 +157,12 @@ shd_status shd_routing_build_device(shd_ctx* ctx, const shd_graph* g, const uint
                                     uint64_t* d_lat_out, float* d_loss_out, shd_error* err);
 
 shd_status shd_routing_last_info(const shd_ctx* ctx, shd_routing_info* info);
+
+/* Time the dominant kernel on every `every`-th build (default 1 = every build; 0 = never).
+ * The duration comes from HIP events recorded with that kernel's dispatch on the context's
+ * stream; they cost a few microseconds of queue gap, which a caller timing many builds can
+ * spread by sampling. */
+shd_status shd_routing_set_timing(shd_ctx* ctx, uint32_t every);
 
 /* Look up one pair of the resident table (row index relative to row_begin of the last build). */
 shd_status shd_routing_lookup(shd_ctx* ctx, uint32_t src_row, uint32_t dst_col,

@@ -23,7 +23,7 @@ PKT_SKIPPED, PKT_DROPPED, PKT_SENT = 0, 1, 2
 EXPORTED = [
     "shd_version", "shd_status_str", "shd_open", "shd_close", "shd_set_stream",
     "shd_routing_build", "shd_routing_prepare", "shd_routing_run", "shd_routing_build_device",
-    "shd_routing_last_info",
+    "shd_routing_last_info", "shd_routing_set_timing",
     "shd_routing_lookup", "shd_routing_smallest_latency", "shd_relay_setup", "shd_relay_round",
     "shd_relay_round_device", "shd_events_merge_device", "shd_relay_get_host_state",
     "shd_relay_set_counters", "shd_relay_last_pipeline",
@@ -138,6 +138,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_routing_prepare": (I32, [P, P, P, U32, U32, P]),
         "shd_routing_run": (I32, [P, U32, U32, U32, P, P, P]),
         "shd_routing_last_info": (I32, [P, P]),
+        "shd_routing_set_timing": (I32, [P, U32]),
         "shd_routing_lookup": (I32, [P, U32, U32, P, P]),
         "shd_routing_smallest_latency": (I32, [P, P]),
         "shd_relay_setup": (I32, [P, U32, P, U32, P, P, P, P]),

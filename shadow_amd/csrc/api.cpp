@@ -80,8 +80,10 @@ shd_ctx* shd_open(int device_ordinal, shd_status* st) {
         shd_close(ctx);
         return fail(SHD_ERR_HIP);
     }
+    // timing-only events: no system-scope fence (cache writeback + invalidate) when recorded --
+    // with it each event cost ~5 us of queue gap beside C2's ~80 us kernel
     for (auto& e : ctx->ev)
-        if (hipEventCreate(&e) != hipSuccess) {
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
             shd_close(ctx);
             return fail(SHD_ERR_HIP);
         }
@@ -255,6 +257,13 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
     SHD_TRY(C.all_gather(d_lat_full + (size_t)C.rank * per * n, d_lat_full, per * n * 8, s));
     SHD_TRY(C.all_gather(d_loss_full + (size_t)C.rank * per * n, d_loss_full, per * n * 4, s));
     SHD_HIP(hipStreamSynchronize(s));
+    return SHD_OK;
+}
+
+shd_status shd_routing_set_timing(shd_ctx* ctx, uint32_t every) {
+    if (!ctx) return SHD_ERR_INVALID;
+    ctx->time_every = every;
+    ctx->time_calls = 0;
     return SHD_OK;
 }
 

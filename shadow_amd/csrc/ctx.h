@@ -138,6 +138,8 @@ struct shd_ctx {
     uint32_t t_rows = 0, t_cols = 0, t_row_begin = 0;
     bool t_full = false;
     shd_routing_info info{};
+    uint32_t time_every = 1, time_calls = 0;   // shd_routing_set_timing
+    bool time_now = true;                      // this build records ev[2] / ev[3]
     bool stats_on = false;   // SHD_SSSP_STATS=1: count expansions / sweeps (tuning only)
 
     shd::PreparedGraph prep;

@@ -17,6 +17,8 @@
 #include <cstring>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "ctx.h"
 
 namespace shd {
@@ -293,7 +295,8 @@ __device__ __forceinline__ void sssp_row(
     const uint32_t grp = lane / G, gl = lane % G;
     uint32_t* q = wq + wave * (kQCap + 32);
     const uint32_t src = used[row];
-    const bool use_delta = delta != kLat32Inf;
+    // PADR kernels run only delta-stepping with one-barrier sweeps and no seed (launch_group)
+    const bool use_delta = PADR != 0 || delta != kLat32Inf;
     const float inv_delta = use_delta ? 1.0f / (float)delta : 0.0f;
     // the ordering key of an active node: its bucket byte, or its label's latency
     auto act_key = [&](uint32_t v) -> uint32_t {
@@ -302,7 +305,7 @@ __device__ __forceinline__ void sssp_row(
 
     // seed_lat (blocked path): labels start at (final latency, +inf loss) so only the loss
     // part can still improve, and only through tight arcs
-    const uint32_t* seed = seed_lat ? seed_lat + (size_t)src * seed_stride : nullptr;
+    const uint32_t* seed = PADR == 0 && seed_lat ? seed_lat + (size_t)src * seed_stride : nullptr;
     for (uint32_t v = tid; v < V; v += BLOCK) {
         uint64_t l0 = kKeyInf;
         if (seed) {
@@ -330,7 +333,7 @@ __device__ __forceinline__ void sssp_row(
     // slot k%3, all read it after the barrier, and sweep k resets slot (k+1)%3, whose last
     // readers passed the barrier of sweep k-1.  A floor taken from a node that the same sweep
     // then expands is only lower than needed: the next sweep selects less, never wrongly.
-    const bool fused = !GLAB && use_delta && flat == nullptr;
+    const bool fused = PADR != 0 || (!GLAB && use_delta && flat == nullptr);
     if (tid == 0) {
         if (!GLAB) lab[src] = 0;  // PathProperties::default() = (0 ns, 0.0)
         bits[src >> 5] = 1u << (src & 31);
@@ -608,12 +611,13 @@ __global__ __launch_bounds__(256) void dense_build(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ alat,
                                                    const float* __restrict__ aloss, uint32_t V,
                                                    uint64_t* __restrict__ Wk, uint32_t* __restrict__ Wl,
-                                                   uint32_t* __restrict__ cursor) {
+                                                   uint32_t* __restrict__ cursor, uint32_t* __restrict__ flags) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t* rowk = reinterpret_cast<uint64_t*>(smem);
     const uint32_t u = blockIdx.x, tid = threadIdx.x;
     for (uint32_t v = tid; v < V; v += 256) rowk[v] = kKeyInf;
     if (u == 0 && tid == 0) *cursor = 0;   // prune_rows' output cursor
+    if (u == 0 && tid < 16) flags[tid] = (tid == 4 || tid == 5) ? 0xFFFFFFFFu : 0u;   // as flags_init
     __syncthreads();
     for (uint32_t k = off[u] + tid; k < off[u + 1]; k += 256)
         atomicMin(reinterpret_cast<unsigned long long*>(&rowk[adst[k]]), (unsigned long long)pack_key(alat[k], aloss[k]));
@@ -1296,25 +1300,30 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
     // padded lists: labels stay below 2^32 - 1 while lu <= guard (0 = unpadded path)
     const uint64_t guard = (uint64_t)kLat32Inf - 1 - P.max_arc_lat;
     const uint32_t lat_guard =
-        A.padded && P.max_arc_lat < kLat32Inf - 1 && env_u32("SHD_SSSP_NO_PAD", 0) != 1
+        A.padded && delta != kLat32Inf && !seed && P.max_arc_lat < kLat32Inf - 1 &&
+                env_u32("SHD_SSSP_NO_PAD", 0) != 1
             ? (uint32_t)std::max<uint64_t>(guard, 1)
             : 0u;
     uint32_t* flags = ctx->g_flags.as<uint32_t>();
     auto* unreach = reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16);
     auto* stats = ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr;
+    hipEvent_t e0 = ctx->time_now ? ctx->ev[2] : nullptr, e1 = ctx->time_now ? ctx->ev[3] : nullptr;
     if constexpr (kArcPad % (G * 8) == 0) {
         if (lat_guard) {
-            sssp_lds_group<BLOCK, G, R, CACHE, 8><<<re - rb, BLOCK, lds, ctx->stream>>>(
-                A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
-                ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss, flags, unreach, delta,
-                stats, seed, seed_stride, ctx->nh_out, lat_guard);
+            hipExtLaunchKernelGGL(sssp_lds_group<BLOCK, G, R, CACHE, 8>, dim3(re - rb), dim3(BLOCK), (uint32_t)lds,
+                                  ctx->stream, e0, e1, 0u, A.beg, A.end, A.arcs, P.V,
+                                  (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
+                                  (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(),
+                                  (const float*)ctx->g_diag_loss.as<float>(), d_lat, d_loss, flags, unreach, delta,
+                                  stats, seed, seed_stride, ctx->nh_out, lat_guard);
             return;
         }
     }
-    sssp_lds_group<BLOCK, G, R, CACHE, 0><<<re - rb, BLOCK, lds, ctx->stream>>>(
-        A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb,
-        ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss, flags, unreach, delta,
-        stats, seed, seed_stride, ctx->nh_out, 0u);
+    hipExtLaunchKernelGGL(sssp_lds_group<BLOCK, G, R, CACHE, 0>, dim3(re - rb), dim3(BLOCK), (uint32_t)lds,
+                          ctx->stream, e0, e1, 0u, A.beg, A.end, A.arcs, P.V,
+                          (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
+                          (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(), (const float*)ctx->g_diag_loss.as<float>(),
+                          d_lat, d_loss, flags, unreach, delta, stats, seed, seed_stride, ctx->nh_out, 0u);
 }
 
 static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
@@ -1363,7 +1372,8 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
     // kernel is issue-bound and the owner search costs more than the dead group slots; C2
     // 132 -> 197 us, so the LDS kernels keep node groups)
     const bool cache = sssp_lds_bytes(P.V, block, true) <= ctx->max_lds;
-    SHD_HIP(hipEventRecord(ctx->ev[2], s));
+    // launch_group records ev[2] / ev[3] on the kernel's dispatch packet (hipExtLaunchKernel):
+    // separate event markers around it cost ~6 us of queue gap each on C2
     if (block == 1024) {
         if (cache) launch_by_degree<1024, true>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
         else launch_by_degree<1024, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
@@ -1375,7 +1385,6 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
         else launch_by_degree<256, false>(ctx, A, rb, re, d_lat, d_loss, delta, G, seed, ss);
     }
     SHD_HIP(hipGetLastError());
-    SHD_HIP(hipEventRecord(ctx->ev[3], s));
     (void)ovf;   // the caller reads the overflow flag with read_flags()
     if (ctx->stats_on) {
         unsigned long long st[2];
@@ -1395,11 +1404,14 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
                           uint32_t use_flat) {
     PreparedGraph& P = ctx->prep;
     constexpr int R = G >= 32 ? 2 : 4;
-    sssp_global_group<BLOCK, G, R><<<grid, BLOCK, lds, ctx->stream>>>(
-        A.beg, A.end, A.arcs, P.V, ctx->g_used.as<uint32_t>(), P.n_used, rb, re,
-        ctx->g_diag_lat.as<uint64_t>(), ctx->g_diag_loss.as<float>(), d_lat, d_loss,
-        ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16),
-        delta, ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
+    // the events ride on the dispatch packet: the kernel's own duration, no marker gaps
+    hipExtLaunchKernelGGL(
+        sssp_global_group<BLOCK, G, R>, dim3(grid), dim3(BLOCK), (uint32_t)lds, ctx->stream,
+        ctx->time_now ? ctx->ev[2] : nullptr, ctx->time_now ? ctx->ev[3] : nullptr, 0u,
+        A.beg, A.end, A.arcs, P.V, (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb, re,
+        (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(), (const float*)ctx->g_diag_loss.as<float>(), d_lat, d_loss,
+        ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16), delta,
+        ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
         ctx->g_glab.as<uint64_t>(), use_bkt, use_flat, ctx->nh_out,
         ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr);
 }
@@ -1408,7 +1420,6 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
 static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re,
                                   uint64_t* d_lat, float* d_loss, uint32_t delta, bool* ovf) {
     PreparedGraph& P = ctx->prep;
-    hipStream_t s = ctx->stream;
     constexpr uint32_t BLOCK = 512;
     const uint32_t W = (P.V + 31) / 32;
     // bitmap + control + per-wave queues (+ delta-stepping: one bucket byte per node, when it
@@ -1425,14 +1436,12 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     if (ctx->nh_out) SHD_TRY(ctx->g_pred.ensure((size_t)grid * P.V * 4));
     const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
     const uint32_t G = env_u32("SHD_SSSP_G", deg >= 64 ? 16 : deg >= 24 ? 8 : 4);
-    SHD_HIP(hipEventRecord(ctx->ev[2], s));
     switch (G) {
         case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat); break;
         case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat); break;
         default: launch_global<BLOCK, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat); break;
     }
     SHD_HIP(hipGetLastError());
-    SHD_HIP(hipEventRecord(ctx->ev[3], s));
     (void)ovf;   // the caller reads the overflow flag with read_flags()
     if (ctx->stats_on) {
         unsigned long long st[2];
@@ -1505,7 +1514,8 @@ static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
     uint32_t* cursor = pend + V;
     uint4* pa = ctx->g_prune_dst.as<uint4>();
     dense_build<<<V, 256, (size_t)V * 8, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
-                                              ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wk, Wl, cursor);
+                                              ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wk, Wl, cursor,
+                                              ctx->g_flags.as<uint32_t>());
     const char* pk = std::getenv("SHD_PRUNE_K");   // tuning: detour nodes per row (same output tables)
     const uint32_t Kr = pk && *pk ? (uint32_t)std::atoi(pk) : kPruneK;
     const uint32_t K = Kr >= 128 ? 128u : Kr >= 64 ? 64u : 32u;
@@ -1530,6 +1540,13 @@ static shd_status count_kept(shd_ctx* ctx, const ArcView& A) {
     return SHD_OK;
 }
 
+// the dominant kernel's device time, when this build was timed (shd_routing_set_timing)
+static float main_ms(shd_ctx* ctx) {
+    float ms = -1.0f;
+    if (ctx->time_now && hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]) != hipSuccess) ms = -1.0f;
+    return ms;
+}
+
 shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t re,
                             uint64_t* d_lat, float* d_loss, shd_error* err) {
     if (err) *err = shd_error{SHD_OK, 0, 0};
@@ -1540,7 +1557,17 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
     ctx->info = shd_routing_info{};
     ctx->info.arcs = P.arcs;
     ctx->info.arcs_kept = P.arcs;
-    SHD_TRY(reset_flags(ctx));
+    ctx->time_now = ctx->time_every != 0 && ctx->time_calls++ % ctx->time_every == 0;
+    // labels + bitmap + queues (+ next hops: pred[V]) must fit the LDS for the LDS-label kernels
+    const size_t lds = sssp_lds_bytes(P.V, 1024, false) + (ctx->nh_out ? (size_t)P.V * 4 + 8 : 0);
+    const bool blocked = algo == SHD_ALGO_BLOCKED && P.narrow_arcs && lds <= ctx->max_lds && P.V <= kBlockedMaxV;
+    const bool lds_path = !blocked && P.narrow_arcs && lds <= ctx->max_lds && env_u32("SHD_SSSP_GLOBAL", 0) != 1;
+    const bool dense = P.V <= kPruneMaxV && P.arcs * 8 >= (uint64_t)P.V * P.V;
+    const bool prune = lds_path && P.mode != SHD_ROUTE_DIRECT &&
+                       (algo == SHD_ALGO_PRUNED || ((algo == SHD_ALGO_AUTO || algo == SHD_ALGO_DELTA) && dense)) &&
+                       P.V <= kPruneMaxV;
+    SHD_TRY(ctx->g_flags.ensure(64));
+    if (!prune) SHD_TRY(reset_flags(ctx));   // the prune path's dense_build resets them
     // wall time of the call (host clock): timing events between the build's kernels cost a
     // few microseconds of queue bubble each, so only the main kernel is bracketed by events
     const auto t_call = std::chrono::steady_clock::now();
@@ -1554,9 +1581,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ctx->info.ms_total = ctx->info.ms_main = ms;
         return st;
     }
-    // labels + bitmap + queues (+ next hops: pred[V]) must fit the LDS for the LDS-label kernels
-    const size_t lds = sssp_lds_bytes(P.V, 1024, false) + (ctx->nh_out ? (size_t)P.V * 4 + 8 : 0);
-    if (algo == SHD_ALGO_BLOCKED && P.narrow_arcs && lds <= ctx->max_lds && P.V <= kBlockedMaxV) {
+    if (blocked) {
         bool ovf = false;
         SHD_TRY(run_blocked(ctx, rb, re, d_lat, d_loss, &ovf));
         ctx->info.algo_used = SHD_ALGO_BLOCKED;
@@ -1564,7 +1589,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;
         ms = call_ms();
-        (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);
+        ms_main = main_ms(ctx);
         ctx->info.ms_total = ms;
         ctx->info.ms_main = ms_main;
         if (!ovf) {
@@ -1576,11 +1601,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         SHD_TRY(reset_flags(ctx));
         return run_wide(ctx, rb, re, d_lat, d_loss, err);
     }
-    if (P.narrow_arcs && lds <= ctx->max_lds && env_u32("SHD_SSSP_GLOBAL", 0) != 1) {
-        const bool dense = P.V <= kPruneMaxV && P.arcs * 8 >= (uint64_t)P.V * P.V;
-        const bool prune = (algo == SHD_ALGO_PRUNED ||
-                            ((algo == SHD_ALGO_AUTO || algo == SHD_ALGO_DELTA) && dense)) &&
-                           P.V <= kPruneMaxV;
+    if (lds_path) {
         ArcView A{ctx->g_off.as<uint32_t>(), ctx->g_off.as<uint32_t>() + 1, ctx->g_arc16.as<uint4>(),
                   P.arcs};
         if (prune) {
@@ -1606,7 +1627,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;
         ms = call_ms();
-        (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);
+        ms_main = main_ms(ctx);
         ctx->info.ms_total = ms;
         ctx->info.ms_main = ms_main;
         if (prune && P.pruned_arcs == 0) SHD_TRY(count_kept(ctx, A));  // once per prepared graph
@@ -1627,7 +1648,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;
         ms = call_ms();
-        (void)hipEventElapsedTime(&ms_main, ctx->ev[2], ctx->ev[3]);
+        ms_main = main_ms(ctx);
         ctx->info.ms_total = ms;
         ctx->info.ms_main = ms_main;
         if (!ovf) return check_unreach(ctx, err);
