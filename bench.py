@@ -229,6 +229,33 @@ def cpu_rows_baseline(el, rows, n_total, what):
                        f"extrapolated x{n_total / k:.0f} (faithful: heap Dijkstra + Vec::contains + HashMap)"), lat, loss
 
 
+def c2_engines(eng, el, reps=5):
+    """Every engine on the C2 graph (all rows, identical tables): what AUTO chose it against."""
+    import torch
+    from shadow_amd import _native as N
+    n = prepare(eng, el)
+    lat = torch.empty((n, n), dtype=torch.int64, device="cuda")
+    loss = torch.empty((n, n), dtype=torch.float32, device="cuda")
+    res, ref = {}, None
+    for name, algo in (("auto", N.ALGO_AUTO), ("sssp", N.ALGO_SSSP), ("pruned", N.ALGO_PRUNED),
+                       ("delta", N.ALGO_DELTA), ("blocked", N.ALGO_BLOCKED)):
+        tot, main = [], []
+        for _ in range(reps):
+            run_rows(eng, algo, 0, n, lat, loss)
+            i = eng.last_info()
+            tot.append(i["ms_total"])
+            main.append(i["ms_main"])
+        h = (int(lat.sum().item()), int(loss.view(torch.int32).to(torch.int64).sum().item()))
+        ref = ref or h
+        res[name] = dict(ms_total=float(np.median(tot)), ms_main=float(np.median(main)),
+                         algo_used=int(i["algo_used"]), arcs_kept=int(i["arcs_kept"]), identical_to_auto=h == ref)
+        if name == "blocked":
+            res[name]["ms_minplus"] = i["ms_minplus"]
+    del lat, loss
+    torch.cuda.empty_cache()
+    return res
+
+
 def c3_leg(eng, reps=2, cpu=True):
     """C3 (10k-node sparse, BA m=3): the three algorithms on the same rows, bit-identical."""
     import torch
@@ -674,6 +701,7 @@ def main():
         res["cpu_baseline"] = cb
     if world == 1 and not args.no_e2e:
         res["routing_e2e"] = routing_e2e(eng, r["el"])
+        res["c2_engines"] = c2_engines(eng, r["el"])
     if not args.no_relay:
         ks = args.relay_steps or max(3, args.steps // 2)
         inputs = relay_inputs()

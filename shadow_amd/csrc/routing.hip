@@ -109,9 +109,13 @@ __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* la
 #pragma unroll
             for (int i = 0; i < R; ++i)
                 if ((imp >> i) & 1u) {
-                    if (bkt) bkt[a[i].x] = bucket_of(key_lat(cand[i]), inv_delta);
+                    uint32_t key = key_lat(cand[i]);
+                    if (bkt) {
+                        key = bucket_of(key, inv_delta);
+                        bkt[a[i].x] = (uint8_t)key;
+                    }
                     atomicOr(&bits[a[i].x >> 5], 1u << (a[i].x & 31));
-                    mnext = min(mnext, key_lat(cand[i]));
+                    mnext = min(mnext, key);
                 }
         }
     }
@@ -164,7 +168,8 @@ __device__ __forceinline__ void relax_node_pad(uint32_t u, uint32_t gl, uint64_t
     }
 }
 
-constexpr uint32_t kQCap = 64;   // per-wave expansion queue (+32 overflow slots)
+constexpr uint32_t kQCap = 64;   // per-wave expansion queue: flushed at kQCap, one scan step adds <= 64
+constexpr uint32_t kQStride = kQCap + 64;
 constexpr uint32_t kFlatWords = 257;   // per-wave scratch of expand_flat: pre[65], beg, lat, q [64]
 constexpr int kFlatR = 8;              // arcs per lane per round of expand_flat
 
@@ -179,7 +184,7 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
                                             uint32_t* bits, const uint2* rng, const uint32_t* __restrict__ abeg,
                                             const uint32_t* __restrict__ aend, const uint4* __restrict__ arcs,
                                             uint32_t* fx, bool& ovf, bool& dirty, uint8_t* bkt, float inv_delta,
-                                            uint32_t scratch) {
+                                            uint32_t scratch, uint32_t& mnext) {
     uint32_t* pre = fx;          // [65]
     uint32_t* beg = fx + 65;     // [64]
     uint32_t* nl = fx + 129;     // [64] latency of the node's label
@@ -249,7 +254,11 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
                             atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[r].x]), (unsigned long long)cand[r]);
                         if (cand[r] < old) {
                             dirty = true;
-                            if (bkt) bkt[a[r].x] = bucket_of(key_lat(cand[r]), inv_delta);
+                            if (bkt) {
+                                const uint8_t bk = bucket_of(key_lat(cand[r]), inv_delta);
+                                bkt[a[r].x] = bk;
+                                mnext = min(mnext, (uint32_t)bk);
+                            }
                             atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
                         }
                     }
@@ -266,7 +275,10 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
                     dirty = true;
 #pragma unroll
                     for (int r = 0; r < kFlatR; ++r)
-                        if ((imp >> r) & 1u) atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
+                        if ((imp >> r) & 1u) {
+                            atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
+                            mnext = min(mnext, key_lat(cand[r]));
+                        }
                 }
             }
         }
@@ -275,7 +287,8 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
 }
 
 // One source row: init, sweeps until nothing improves, emit the used columns.
-template <int BLOCK, int G, int R, bool CACHE, bool GLAB, int PADR = 0>
+// FASTG (global labels): flat expansion + bucket bytes + one-barrier delta sweeps only (C4)
+template <int BLOCK, int G, int R, bool CACHE, bool GLAB, int PADR = 0, bool FASTG = false>
 __device__ __forceinline__ void sssp_row(
     uint64_t* lab, uint32_t* bits, uint32_t* ctl, uint32_t* wq, uint2* rng,
     const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
@@ -293,14 +306,14 @@ __device__ __forceinline__ void sssp_row(
     const uint32_t W = (V + 31) >> 5;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t grp = lane / G, gl = lane % G;
-    uint32_t* q = wq + wave * (kQCap + 32);
+    uint32_t* q = wq + wave * kQStride;
     const uint32_t src = used[row];
     // PADR kernels run only delta-stepping with one-barrier sweeps and no seed (launch_group)
-    const bool use_delta = PADR != 0 || delta != kLat32Inf;
+    const bool use_delta = PADR != 0 || FASTG || delta != kLat32Inf;
     const float inv_delta = use_delta ? 1.0f / (float)delta : 0.0f;
     // the ordering key of an active node: its bucket byte, or its label's latency
     auto act_key = [&](uint32_t v) -> uint32_t {
-        return bkt ? (uint32_t)bkt[v] : key_lat(ld_lab<GLAB>(&lab[v]));
+        return FASTG || bkt ? (uint32_t)bkt[v] : key_lat(ld_lab<GLAB>(&lab[v]));
     };
 
     // seed_lat (blocked path): labels start at (final latency, +inf loss) so only the loss
@@ -333,7 +346,7 @@ __device__ __forceinline__ void sssp_row(
     // slot k%3, all read it after the barrier, and sweep k resets slot (k+1)%3, whose last
     // readers passed the barrier of sweep k-1.  A floor taken from a node that the same sweep
     // then expands is only lower than needed: the next sweep selects less, never wrongly.
-    const bool fused = PADR != 0 || (!GLAB && use_delta && flat == nullptr);
+    const bool fused = PADR != 0 || FASTG || (use_delta && (!GLAB || bkt));
     if (tid == 0) {
         if (!GLAB) lab[src] = 0;  // PathProperties::default() = (0 ns, 0.0)
         bits[src >> 5] = 1u << (src & 31);
@@ -351,7 +364,7 @@ __device__ __forceinline__ void sssp_row(
             const uint32_t lo = sweeps == 0 ? 0u : ctl[1 + (slot + 2) % 3];
             if (lo == kLat32Inf) break;  // no active node anywhere
             if (tid == 0) ctl[1 + (slot + 1) % 3] = kLat32Inf;
-            thr = lo + delta < lo ? kLat32Inf - 1 : lo + delta;
+            thr = bkt ? lo : lo + delta < lo ? kLat32Inf - 1 : lo + delta;
         } else {
             if (tid == 0) {
                 ctl[0] = 0;
@@ -361,10 +374,9 @@ __device__ __forceinline__ void sssp_row(
         }
         if (use_delta && !fused) {
             uint32_t m = kLat32Inf;
-            for (uint32_t widx = wave; widx < W; widx += NW) {
+            for (uint32_t widx = lane * NW + wave; widx < W; widx += NW * 64) {   // lane per word
                 const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (word == 0) continue;
-                if (lane < 32 && ((word >> lane) & 1u)) m = min(m, act_key(widx * 32 + lane));
+                for (uint32_t mm = word; mm; mm &= mm - 1) m = min(m, act_key(widx * 32 + __builtin_ctz(mm)));
             }
             for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
             if (lane == 0 && m != kLat32Inf) atomicMin(&ctl[1], m);
@@ -375,59 +387,114 @@ __device__ __forceinline__ void sssp_row(
         }
         bool dirty = false;
         uint32_t qn = 0;  // wave-uniform queue length
-        for (uint32_t widx = wave;; widx += NW) {
-            const bool more = widx < W;
-            if (more) {
-                const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (word != 0) {  // wave-uniform
-                    bool sel = lane < 32 && ((word >> lane) & 1u);
-                    if (use_delta && sel) {
-                        const uint32_t key = act_key(widx * 32 + lane);
-                        sel = key <= thr;
-                        if (!sel) mnext = min(mnext, key);
-                    }
-                    const uint32_t mask = (uint32_t)__ballot(sel);
-                    if (mask) {
-                        // words are owned by one wave; other waves only set bits: clearing is exact
-                        if (lane == 0) atomicAnd(&bits[widx], ~mask);
-                        if (sel) q[qn + __popc(mask & ((1u << lane) - 1u))] = widx * 32 + lane;
-                        qn += __popc(mask);
-                    }
-                }
-            }
-            if (qn >= kQCap || (!more && qn > 0)) {   // flush: NG nodes per step, G lanes each
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                expanded += qn;
-                if constexpr (GLAB) {
-                    if (flat) {
-                        expand_flat<GLAB>(q, qn, lane, lab, bits, nullptr, abeg, aend, arcs, flat + wave * kFlatWords,
-                                          ovf, dirty, bkt, inv_delta, V + lane);
-                    } else {
-                        for (uint32_t t = 0; t < qn; t += NG) {
-                            const uint32_t qi = t + grp;
-                            if (qi < qn)
-                                relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
-                                                              ovf, dirty, bkt, inv_delta, mnext);
-                        }
-                    }
+        // expand the queued nodes: NG nodes per step, G lanes each (or edge-parallel, global labels)
+        auto flush = [&]() {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            expanded += qn;
+            if constexpr (GLAB) {
+                if (FASTG || flat) {
+                    expand_flat<GLAB>(q, qn, lane, lab, bits, nullptr, abeg, aend, arcs, flat + wave * kFlatWords,
+                                      ovf, dirty, bkt, inv_delta, V + lane, mnext);
                 } else {
                     for (uint32_t t = 0; t < qn; t += NG) {
                         const uint32_t qi = t + grp;
-                        if (qi >= qn) continue;
-                        if constexpr (PADR != 0)   // padded lists: a whole 64-slot list per group step
-                            relax_node_pad<G, PADR, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, lat_guard,
-                                                           ovf, dirty, mnext);
-                        else
+                        if (qi < qn)
                             relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
                                                           ovf, dirty, bkt, inv_delta, mnext);
                     }
                 }
-                qn = 0;
-                __builtin_amdgcn_wave_barrier();
+            } else {
+                for (uint32_t t = 0; t < qn; t += NG) {
+                    const uint32_t qi = t + grp;
+                    if (qi >= qn) continue;
+                    if constexpr (PADR != 0)   // padded lists: a whole 64-slot list per group step
+                        relax_node_pad<G, PADR, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, lat_guard,
+                                                       ovf, dirty, mnext);
+                    else
+                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
+                                                      ovf, dirty, bkt, inv_delta, mnext);
+                }
+            }
+            qn = 0;
+            __builtin_amdgcn_wave_barrier();
+        };
+        // scan form: padded-list kernels (dense graphs, V <= kPruneMaxV) only the small-bitmap
+        // one, global-label kernels (large V) only the lane-per-word one, so each kernel carries
+        // one loop (fewer registers)
+        constexpr int kScan = PADR != 0 ? 1 : GLAB ? 2 : 0;   // 1 small, 2 lane, 0 by W
+        if (kScan == 1 || (kScan == 0 && W <= NW * 16)) {
+            // small bitmap (C2: 32 words over 4 waves): a word per wave step, lane per bit
+            for (uint32_t widx = wave;; widx += NW) {
+                const bool more = widx < W;
+                if (more) {
+                    const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (word != 0) {  // wave-uniform
+                        bool sel = lane < 32 && ((word >> lane) & 1u);
+                        if (use_delta && sel) {
+                            const uint32_t key = act_key(widx * 32 + lane);
+                            sel = key <= thr;
+                            if (!sel) mnext = min(mnext, key);
+                        }
+                        const uint32_t mask = (uint32_t)__ballot(sel);
+                        if (mask) {
+                            // words are owned by one wave; other waves only set bits: clearing is exact
+                            if (lane == 0) atomicAnd(&bits[widx], ~mask);
+                            if (sel) q[qn + __popc(mask & ((1u << lane) - 1u))] = widx * 32 + lane;
+                            qn += __popc(mask);
+                        }
+                    }
+                }
+                if (qn >= kQCap || (!more && qn > 0)) flush();
+                if (!more) break;
+            }
+        }
+        if (kScan == 2 || (kScan == 0 && W > NW * 16)) {
+        // Lane per bitmap word: a wave reads 64 words at once, each lane picks its word's selected
+        // nodes (bits clear first; other waves only set bits in a word this lane owns, so the
+        // atomicAnd is exact), then the selected nodes enter the queue one per lane per step.  A
+        // sweep's frontier is sparse (C4: about one active node per word), so this reads the
+        // bitmap 64x faster than a word per wave step with half the lanes idle (C4 DELTA, 4096
+        // rows: 50.8 -> 38.7 ms).  Words are dealt round-robin (word k*NW + wave to lane k).
+        for (uint32_t k0 = 0;; k0 += 64) {
+            const bool more = k0 * NW + wave < W;   // wave-uniform: the wave has words in this batch
+            const uint32_t widx = (k0 + lane) * NW + wave;
+            uint32_t rem = 0;           // this lane's selected nodes not yet queued
+            if (more && widx < W) {
+                const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (word) {
+                    uint32_t selm = word;
+                    if (use_delta) {
+                        selm = 0;
+                        for (uint32_t mm = word; mm; mm &= mm - 1) {
+                            const uint32_t b = __builtin_ctz(mm);
+                            const uint32_t key = act_key(widx * 32 + b);
+                            if (key <= thr) selm |= 1u << b;
+                            else mnext = min(mnext, key);
+                        }
+                    }
+                    if (selm) atomicAnd(&bits[widx], ~selm);
+                    rem = selm;
+                }
+            }
+            for (;;) {
+                const uint64_t bal = __ballot(rem != 0);
+                if (more && bal == 0) break;   // this batch of words is queued
+                if (rem) {
+                    q[qn + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = widx * 32 + __builtin_ctz(rem);
+                    rem &= rem - 1;
+                }
+                qn += (uint32_t)__popcll(bal);
+                if (qn < kQCap && (more || qn == 0)) {
+                    if (more) continue;
+                    break;
+                }
+                flush();
+                if (!more && bal == 0) break;
             }
             if (!more) break;
+        }
         }
         ++sweeps;
         if (fused) {
@@ -533,10 +600,10 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V + 64);
     uint32_t* ctl = bits + W;            // [0] dirty  [1..3] min active latency
-    uint32_t* wq = ctl + 4;              // per-wave queue (kQCap + 32 node ids)
+    uint32_t* wq = ctl + 4;              // per-wave queue (kQStride node ids)
     // [V] arc range {beg, end}, 8-byte aligned after the queues
     const uint32_t rng_off =
-        (((uint32_t)((wq + NW * (kQCap + 32)) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
+        (((uint32_t)((wq + NW * kQStride) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
     uint2* rng = reinterpret_cast<uint2*>(smem + rng_off);
     sssp_row<BLOCK, G, R, CACHE, false, PADR>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
                                               row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
@@ -549,7 +616,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
 // nodes = 400 KB per source).  A persistent grid of slots: slot b owns the label array
 // glab[b*V, (b+1)*V) and walks rows row_begin + b, + gridDim.x, ...; the bitmap and the queues
 // stay in LDS (V/8 bytes).
-template <int BLOCK, int G, int R>
+template <int BLOCK, int G, int R, bool FASTG>
 __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
     const uint4* __restrict__ arcs, uint32_t V, const uint32_t* __restrict__ used,
@@ -564,12 +631,12 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
     uint32_t* ctl = bits + W;
     uint32_t* wq = ctl + 4;
-    uint32_t* flat = use_flat ? wq + (BLOCK / 64) * (kQCap + 32) : nullptr;
-    uint8_t* bkt = use_bkt ? reinterpret_cast<uint8_t*>(wq + (BLOCK / 64) * (kQCap + 32 + (use_flat ? kFlatWords : 0)))
+    uint32_t* flat = use_flat ? wq + (BLOCK / 64) * kQStride : nullptr;
+    uint8_t* bkt = use_bkt ? reinterpret_cast<uint8_t*>(wq + (BLOCK / 64) * (kQStride + (use_flat ? kFlatWords : 0)))
                            : nullptr;
     uint64_t* lab = glab + (size_t)blockIdx.x * V;
     for (uint32_t row = row_begin + blockIdx.x; row < row_end; row += gridDim.x) {
-        sssp_row<BLOCK, G, R, false, true>(lab, bits, ctl, wq, nullptr, abeg, aend, arcs, V, used,
+        sssp_row<BLOCK, G, R, false, true, 0, FASTG>(lab, bits, ctl, wq, nullptr, abeg, aend, arcs, V, used,
                                            n_used, row, (size_t)(row - row_begin) * n_used,
                                            diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
                                            delta, stats, nullptr, 0, bkt, flat, nh_out,
@@ -1328,7 +1395,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
 
 static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
     // labels + bitmap + control + per-wave queues (+ arc ranges, 8-byte aligned)
-    const size_t head = (size_t)(V + 64) * 8 + (size_t)((V + 31) / 32) * 4 + 16 + (block / 64) * (kQCap + 32) * 4;
+    const size_t head = (size_t)(V + 64) * 8 + (size_t)((V + 31) / 32) * 4 + 16 + (block / 64) * kQStride * 4;
     return cache ? ((head + 7) & ~(size_t)7) + (size_t)V * 8 : head;
 }
 
@@ -1405,8 +1472,11 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
     PreparedGraph& P = ctx->prep;
     constexpr int R = G >= 32 ? 2 : 4;
     // the events ride on the dispatch packet: the kernel's own duration, no marker gaps
+    // flat + bucket bytes + delta (C4's configuration): the kernel without the other paths
+    auto kern = use_bkt && use_flat && delta != kLat32Inf ? sssp_global_group<BLOCK, G, R, true>
+                                                          : sssp_global_group<BLOCK, G, R, false>;
     hipExtLaunchKernelGGL(
-        sssp_global_group<BLOCK, G, R>, dim3(grid), dim3(BLOCK), (uint32_t)lds, ctx->stream,
+        kern, dim3(grid), dim3(BLOCK), (uint32_t)lds, ctx->stream,
         ctx->time_now ? ctx->ev[2] : nullptr, ctx->time_now ? ctx->ev[3] : nullptr, 0u,
         A.beg, A.end, A.arcs, P.V, (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb, re,
         (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(), (const float*)ctx->g_diag_loss.as<float>(), d_lat, d_loss,
@@ -1425,7 +1495,7 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     // bitmap + control + per-wave queues (+ delta-stepping: one bucket byte per node, when it
     // fits beside the bitmap; else the sweeps read the active nodes' global labels)
     const uint32_t use_flat = env_u32("SHD_SSSP_FLAT", 1) != 0;   // edge-parallel expansion
-    size_t lds = (size_t)W * 4 + 16 + (BLOCK / 64) * (kQCap + 32 + (use_flat ? kFlatWords : 0)) * 4;
+    size_t lds = (size_t)W * 4 + 16 + (BLOCK / 64) * (kQStride + (use_flat ? kFlatWords : 0)) * 4;
     if (lds > ctx->max_lds) return SHD_ERR_INVALID;   // bitmap of > ~1.2M nodes
     const size_t lds_bkt = lds + ((size_t)P.V + 3) / 4 * 4;
     const uint32_t use_bkt = delta != kLat32Inf && lds_bkt <= ctx->max_lds && env_u32("SHD_SSSP_NO_BKT", 0) != 1;

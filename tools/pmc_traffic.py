@@ -31,10 +31,8 @@ ka = [k for k in pf if k.startswith("kA(")][0]
 n_pkt = 10_000_000
 read_factor = 24.0 * n_pkt / (sum(pf[ka]) / len(pf[ka]))
 write_factor = 21.0 * n_pkt / (sum(pw[ka]) / len(pw[ka]))
-bf, bw = load("bench", "FETCH_SIZE"), load("bench", "WRITE_SIZE")
-
-
-def per_launch(sel):
+def per_launch(run, sel):
+    bf, bw = load(run, "FETCH_SIZE"), load(run, "WRITE_SIZE")
     out = {}
     for k in bf:
         if sel(k):
@@ -42,18 +40,19 @@ def per_launch(sel):
     return out
 
 
-sssp = per_launch(lambda k: "sssp_lds_group" in k)
+sssp = per_launch("bench", lambda k: "sssp_lds_group" in k)
 r_read = sum(v[0] * v[2] for v in sssp.values()) / sum(v[2] for v in sssp.values())
 r_write = sum(v[1] * v[2] for v in sssp.values()) / sum(v[2] for v in sssp.values())
 relay_sel = ("relay_draws", "relay_stamp", "rocprim", "bucket_offsets", "segment_sort", "relay_bin_hist",
-             "bin_col_scan", "bin_base_scan", "bin_sort_v7")
-relay = per_launch(lambda k: any(s in k for s in relay_sel))
+             "bin_col_scan", "bin_base_scan", "bin_sort_v7", "red_init")
+relay = per_launch("relay", lambda k: any(s in k for s in relay_sel))
 rounds = sum(v[2] for k, v in relay.items() if "relay_stamp" in k)
 rel_read = sum(v[0] * v[2] for v in relay.values()) / rounds
 rel_write = sum(v[1] * v[2] for v in relay.values()) / rounds
 doc = {
-    "source": "tools/pmc_traffic.sh + tools/pmc_traffic.py (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE "
-              "in separate runs of bench.py --steps 3 --relay-steps 3 --no-c3 --no-c4)",
+    "source": "tools/pmc_traffic.sh + tools/pmc_traffic.py (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE in "
+              "separate runs: routing from bench.py --no-relay (C2 builds), relay from tools/relay_only.py 10 "
+              "(C5 rounds, pipeline 7, no counters))",
     "read_factor": read_factor, "write_factor_measured": write_factor,
     "routing": r_read + r_write,
     "routing_detail": {"kernel": "sssp_lds_group", "read_bytes": r_read, "write_bytes": r_write},
@@ -72,7 +71,7 @@ if len(sys.argv) > 3:
     with open(sys.argv[3], "w", newline="") as f:
         wr = csv.writer(f)
         wr.writerow(["run", "counter", "kernel", "launches", "mean_KB"])
-        for run in ("probe", "bench"):
+        for run in ("probe", "bench", "relay"):
             for c in ("FETCH_SIZE", "WRITE_SIZE"):
                 for k, v in sorted(load(run, c).items()):
                     wr.writerow([run, c, k.split("(")[0], len(v), round(sum(v) / len(v) / 1e3, 1)])
