@@ -244,6 +244,15 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
                 cand[r] = ok ? pack_key(cl, fold_q(qu[r], __uint_as_float(a[r].z))) : kKeyInf;
             }
             if constexpr (GLAB) {
+                // bucket-byte filter: bkt[v] >= the bucket of v's label (it is written only by a
+                // relaxation that just lowered the label, and the label only falls further), so
+                // a candidate in a higher bucket cannot improve it -- skip its global label read
+                // (most relaxations of a sparse graph fail; the byte is in LDS)
+                if (bkt) {
+#pragma unroll
+                    for (int r = 0; r < kFlatR; ++r)
+                        if (cand[r] != kKeyInf && bucket_of(key_lat(cand[r]), inv_delta) > bkt[a[r].x]) cand[r] = kKeyInf;
+                }
 #pragma unroll
                 for (int r = 0; r < kFlatR; ++r) cur[r] = cand[r] != kKeyInf ? ld_lab<true>(&lab[a[r].x]) : 0ull;
 #pragma unroll
@@ -334,6 +343,8 @@ __device__ __forceinline__ void sssp_row(
         if (CACHE) rng[v] = make_uint2(abeg[v], aend[v]);
     }
     for (uint32_t w = tid; w < W; w += BLOCK) bits[w] = 0;
+    if (bkt)   // unreached: the top bucket (the relax filter never skips against it)
+        for (uint32_t w = tid; w < (V + 3) / 4; w += BLOCK) reinterpret_cast<uint32_t*>(bkt)[w] = 0xFFFFFFFFu;
     if (!GLAB && tid < 64) lab[V + tid] = 0;   // scratch labels: no candidate improves them
     // global labels: every storing wave drains its stores before the barrier, so the L2 holds
     // them before any wave's atomics
@@ -557,7 +568,7 @@ __device__ __forceinline__ void sssp_row(
                 }
                 if (pw == src) nh = w;
             }
-            nh_out[orow + j] = nh;
+            __builtin_nontemporal_store(nh, &nh_out[orow + j]);
         }
     }
     for (uint32_t j = tid; j < n_used; j += BLOCK) {
@@ -577,8 +588,10 @@ __device__ __forceinline__ void sssp_row(
                 p = key_loss(k);
             }
         }
-        out_lat[orow + j] = l;
-        out_loss[orow + j] = p;
+        // the table is written once and never read here: non-temporal stores keep it from
+        // evicting the label rows (C4: 600 KB of table per source row) from L2 / Infinity Cache
+        __builtin_nontemporal_store(l, &out_lat[orow + j]);
+        __builtin_nontemporal_store(p, &out_loss[orow + j]);
     }
 }
 
@@ -1708,8 +1721,12 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
     if (P.narrow_arcs && (lds > ctx->max_lds || env_u32("SHD_SSSP_GLOBAL", 0) == 1)) {
         // labels exceed the LDS: global-label kernel (C4)
         bool ovf = false;
+        // bucket width: 0.4 x the mean arc latency, never below the smallest arc (C4, rows
+        // 0-4095 with the bucket-byte relax filter: 1 ms 30.7 ms, 2 ms 25.8, 3 ms 24.1, 5-6 ms
+        // 23.0, 8 ms 23.4, 12.5 ms (the mean) 38.6 before the filter)
         uint32_t delta = kLat32Inf;
-        if (algo == SHD_ALGO_DELTA) delta = env_u32("SHD_SSSP_DELTA", P.mean_arc_lat);
+        if (algo == SHD_ALGO_DELTA)
+            delta = env_u32("SHD_SSSP_DELTA", std::max(P.min_arc_lat, (uint32_t)(P.mean_arc_lat * 2ull / 5)));
         ArcView A{ctx->g_off.as<uint32_t>(), ctx->g_off.as<uint32_t>() + 1, ctx->g_arc16.as<uint4>(),
                   P.arcs};
         SHD_TRY(run_sssp_global(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
