@@ -46,6 +46,9 @@ __device__ __forceinline__ uint64_t ld_lab(const uint64_t* p) {
 
 // delta-stepping bucket of a latency for the global-label kernel's LDS bucket bytes: any
 // estimate works (it only orders the expansions), so a float multiply, saturating at 255
+// The byte holds the latency in steps of delta / kBktSub: the sweeps schedule by byte >>
+// kBktShift (delta-wide buckets) while the relax filter compares whole bytes, kBktSub times finer.
+constexpr uint32_t kBktShift = 0, kBktSub = 1u << kBktShift;   // shift 2 (4x finer filter) measured no faster on C4
 __device__ __forceinline__ uint8_t bucket_of(uint32_t lat, float inv_delta) {
     return (uint8_t)fminf(255.0f, (float)lat * inv_delta);
 }
@@ -111,8 +114,9 @@ __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* la
                 if ((imp >> i) & 1u) {
                     uint32_t key = key_lat(cand[i]);
                     if (bkt) {
-                        key = bucket_of(key, inv_delta);
-                        bkt[a[i].x] = (uint8_t)key;
+                        const uint8_t bk = bucket_of(key, inv_delta);
+                        bkt[a[i].x] = bk;
+                        key = bk >> kBktShift;
                     }
                     atomicOr(&bits[a[i].x >> 5], 1u << (a[i].x & 31));
                     mnext = min(mnext, key);
@@ -266,7 +270,7 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
                             if (bkt) {
                                 const uint8_t bk = bucket_of(key_lat(cand[r]), inv_delta);
                                 bkt[a[r].x] = bk;
-                                mnext = min(mnext, (uint32_t)bk);
+                                mnext = min(mnext, (uint32_t)(bk >> kBktShift));
                             }
                             atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
                         }
@@ -295,6 +299,102 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
     }
 }
 
+// expand_flat for the global-label kernel on compact arcs: {dst, lat} (8 B) per arc, q = 1f32 -
+// loss in a side array read only by the relaxations that survive the bucket-byte filter.  Most
+// relaxations of a sparse graph fail, so the arc stream a sweep reads halves and (C4: 400k arcs,
+// 3.2 MB) fits one XCD's L2.
+__device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uint32_t lane, uint64_t* lab,
+                                             uint32_t* bits, const uint32_t* __restrict__ abeg,
+                                             const uint32_t* __restrict__ aend, const uint2* __restrict__ arcs8,
+                                             const float* __restrict__ aq, uint32_t* fx, bool& ovf, bool& dirty,
+                                             uint8_t* bkt, float inv_delta, uint32_t& mnext) {
+    uint32_t* pre = fx;          // [65]
+    uint32_t* beg = fx + 65;     // [64]
+    uint32_t* nl = fx + 129;     // [64] latency of the node's label
+    uint32_t* nq = fx + 193;     // [64] q = 1f32 - loss of the node's label
+    for (uint32_t c0 = 0; c0 < qn; c0 += 64) {
+        const uint32_t cn = min(64u, qn - c0);
+        uint32_t deg = 0, b = 0;
+        uint64_t ku = kKeyInf;
+        if (lane < cn) {
+            const uint32_t u = q[c0 + lane];
+            b = abeg[u];
+            deg = aend[u] - b;
+            ku = ld_lab<true>(&lab[u]);
+        }
+        uint32_t incl = deg;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t T = __shfl(incl, 63);
+        pre[lane] = incl - deg;
+        beg[lane] = b;
+        nl[lane] = key_lat(ku);
+        nq[lane] = __float_as_uint(one_minus(key_loss(ku)));
+        if (lane == 0) pre[64] = T;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t t0 = 0; t0 < T; t0 += 64 * kFlatR) {
+            uint2 a[kFlatR];
+            uint32_t lu[kFlatR], k[kFlatR], cl[kFlatR];
+            float qu[kFlatR];
+            bool ok[kFlatR];
+#pragma unroll
+            for (int r = 0; r < kFlatR; ++r) {
+                const uint32_t t = t0 + r * 64 + lane;
+                ok[r] = t < T;
+                const uint32_t tc = min(t, T - 1);   // dead slots load the last arc (in bounds)
+                uint32_t lo = 0, hi = 64;   // last j with pre[j] <= tc (zero-degree nodes are skipped)
+#pragma unroll
+                for (int it = 0; it < 6; ++it) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pre[mid] <= tc) lo = mid; else hi = mid;
+                }
+                lu[r] = nl[lo];
+                qu[r] = __uint_as_float(nq[lo]);
+                k[r] = beg[lo] + (tc - pre[lo]);
+                a[r] = arcs8[k[r]];
+            }
+#pragma unroll
+            for (int r = 0; r < kFlatR; ++r) {
+                cl[r] = lu[r] + a[r].y;
+                const bool fit = cl[r] >= lu[r] && cl[r] != kLat32Inf;
+                if (ok[r] && !fit) ovf = true;   // leaves u32: wide rerun
+                // bucket-byte filter (see expand_flat): a higher bucket cannot improve the label
+                ok[r] = ok[r] && fit && bucket_of(cl[r], inv_delta) <= bkt[a[r].x];
+            }
+            uint64_t cur[kFlatR];
+            float qa[kFlatR];
+#pragma unroll
+            for (int r = 0; r < kFlatR; ++r) {
+                cur[r] = ok[r] ? ld_lab<true>(&lab[a[r].x]) : 0ull;
+                qa[r] = ok[r] ? aq[k[r]] : 0.0f;
+            }
+#pragma unroll
+            for (int r = 0; r < kFlatR; ++r) {
+                if (!ok[r]) continue;
+                const uint64_t cand = pack_key(cl[r], fold_q(qu[r], qa[r]));
+                // labels only decrease: a candidate not below the label read now cannot improve it
+                if (cand < cur[r]) {
+                    const uint64_t old =
+                        atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[r].x]), (unsigned long long)cand);
+                    if (cand < old) {
+                        dirty = true;
+                        const uint8_t bk = bucket_of(cl[r], inv_delta);
+                        bkt[a[r].x] = bk;
+                        mnext = min(mnext, (uint32_t)(bk >> kBktShift));
+                        atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // One source row: init, sweeps until nothing improves, emit the used columns.
 // FASTG (global labels): flat expansion + bucket bytes + one-barrier delta sweeps only (C4)
 template <int BLOCK, int G, int R, bool CACHE, bool GLAB, int PADR = 0, bool FASTG = false>
@@ -308,7 +408,7 @@ __device__ __forceinline__ void sssp_row(
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
     uint32_t seed_stride, uint8_t* bkt, uint32_t* flat, uint32_t* nh_out, uint32_t* pred,
-    uint32_t lat_guard) {
+    uint32_t lat_guard, const uint2* __restrict__ arcs8 = nullptr, const float* __restrict__ aq = nullptr) {
     // bkt (global labels + delta-stepping): per node, the bucket of the latency that last
     // activated it, in LDS, so choosing a sweep's nodes reads no global label
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
@@ -319,10 +419,11 @@ __device__ __forceinline__ void sssp_row(
     const uint32_t src = used[row];
     // PADR kernels run only delta-stepping with one-barrier sweeps and no seed (launch_group)
     const bool use_delta = PADR != 0 || FASTG || delta != kLat32Inf;
-    const float inv_delta = use_delta ? 1.0f / (float)delta : 0.0f;
+    // bucket bytes count steps of delta / kBktSub (global labels); the LDS kernels do not use them
+    const float inv_delta = use_delta ? (float)kBktSub / (float)delta : 0.0f;
     // the ordering key of an active node: its bucket byte, or its label's latency
     auto act_key = [&](uint32_t v) -> uint32_t {
-        return FASTG || bkt ? (uint32_t)bkt[v] : key_lat(ld_lab<GLAB>(&lab[v]));
+        return FASTG || bkt ? (uint32_t)(bkt[v] >> kBktShift) : key_lat(ld_lab<GLAB>(&lab[v]));
     };
 
     // seed_lat (blocked path): labels start at (final latency, +inf loss) so only the loss
@@ -405,7 +506,10 @@ __device__ __forceinline__ void sssp_row(
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             expanded += qn;
             if constexpr (GLAB) {
-                if (FASTG || flat) {
+                if constexpr (FASTG) {
+                    expand_flat8(q, qn, lane, lab, bits, abeg, aend, arcs8, aq, flat + wave * kFlatWords, ovf, dirty,
+                                 bkt, inv_delta, mnext);
+                } else if (flat) {
                     expand_flat<GLAB>(q, qn, lane, lab, bits, nullptr, abeg, aend, arcs, flat + wave * kFlatWords,
                                       ovf, dirty, bkt, inv_delta, V + lane, mnext);
                 } else {
@@ -638,7 +742,8 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, uint64_t* __restrict__ glab, uint32_t use_bkt, uint32_t use_flat,
-    uint32_t* __restrict__ nh_out, uint32_t* __restrict__ gpred) {
+    uint32_t* __restrict__ nh_out, uint32_t* __restrict__ gpred, const uint2* __restrict__ arcs8,
+    const float* __restrict__ aq) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
@@ -653,7 +758,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
                                            n_used, row, (size_t)(row - row_begin) * n_used,
                                            diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
                                            delta, stats, nullptr, 0, bkt, flat, nh_out,
-                                           gpred ? gpred + (size_t)blockIdx.x * V : nullptr, 0u);
+                                           gpred ? gpred + (size_t)blockIdx.x * V : nullptr, 0u, arcs8, aq);
         __syncthreads();   // the next row re-initialises labels and bitmap
     }
 }
@@ -661,9 +766,14 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
 __global__ __launch_bounds__(256) void arcs_pack(const uint32_t* __restrict__ dst,
                                                  const uint32_t* __restrict__ lat,
                                                  const float* __restrict__ loss,
-                                                 uint4* __restrict__ out, uint64_t n) {
+                                                 uint4* __restrict__ out, uint2* __restrict__ out8,
+                                                 float* __restrict__ outq, uint64_t n) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) out[i] = make_uint4(dst[i], lat[i], __float_as_uint(one_minus(loss[i])), 0u);
+    if (i >= n) return;
+    const float q = one_minus(loss[i]);
+    out[i] = make_uint4(dst[i], lat[i], __float_as_uint(q), 0u);
+    out8[i] = make_uint2(dst[i], lat[i]);   // compact arcs of the global-label kernel
+    outq[i] = q;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1304,10 +1414,12 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
             SHD_TRY(upload(ctx->g_lat, l32, s));
             SHD_TRY(upload(ctx->g_aux, H.loss, s));
             SHD_TRY(ctx->g_arc16.ensure(std::max<size_t>(H.loss.size(), 1) * 16));
+            SHD_TRY(ctx->g_arc8.ensure(std::max<size_t>(H.loss.size(), 1) * 8));
+            SHD_TRY(ctx->g_aq.ensure(std::max<size_t>(H.loss.size(), 1) * 4));
             if (!H.loss.empty())
                 arcs_pack<<<div_up(H.loss.size(), 256), 256, 0, s>>>(
                     ctx->g_dst.as<uint32_t>(), ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(),
-                    ctx->g_arc16.as<uint4>(), H.loss.size());
+                    ctx->g_arc16.as<uint4>(), ctx->g_arc8.as<uint2>(), ctx->g_aq.as<float>(), H.loss.size());
             P.pruned_arcs = 0;
             P.tight_arcs = 0;
         }
@@ -1496,7 +1608,8 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16), delta,
         ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
         ctx->g_glab.as<uint64_t>(), use_bkt, use_flat, ctx->nh_out,
-        ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr);
+        ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr, (const uint2*)ctx->g_arc8.as<uint2>(),
+        (const float*)ctx->g_aq.as<float>());
 }
 
 // Kernel 1b driver: labels in global memory (graphs whose labels exceed the LDS).
