@@ -538,8 +538,11 @@ __device__ __forceinline__ void sssp_row(
         // scan form: padded-list kernels (dense graphs, V <= kPruneMaxV) only the small-bitmap
         // one, global-label kernels (large V) only the lane-per-word one, so each kernel carries
         // one loop (fewer registers)
-        constexpr int kScan = PADR != 0 ? 1 : GLAB ? 2 : 0;   // 1 small, 2 lane, 0 by W
-        if (kScan == 1 || (kScan == 0 && W <= NW * 16)) {
+        // (plain chaotic sweeps, no delta, keep the word-per-step form: C3 SSSP 11.2 ms against
+        // 17.4 with lane-per-word, whose frontier there is dense)
+        constexpr int kScan = PADR != 0 ? 1 : GLAB ? 2 : 0;   // 1 small, 2 lane, 0 by W / delta
+        const bool lane_scan = kScan == 2 || (kScan == 0 && use_delta && W > NW * 16);
+        if (!lane_scan) {
             // small bitmap (C2: 32 words over 4 waves): a word per wave step, lane per bit
             for (uint32_t widx = wave;; widx += NW) {
                 const bool more = widx < W;
@@ -565,7 +568,7 @@ __device__ __forceinline__ void sssp_row(
                 if (!more) break;
             }
         }
-        if (kScan == 2 || (kScan == 0 && W > NW * 16)) {
+        if (lane_scan) {
         // Lane per bitmap word: a wave reads 64 words at once, each lane picks its word's selected
         // nodes (bits clear first; other waves only set bits in a word this lane owns, so the
         // atomicAnd is exact), then the selected nodes enter the queue one per lane per step.  A
@@ -1812,13 +1815,16 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         // sweep count explode -- a bucket no wider than every arc settles in one sweep, so each
         // node is expanded once (Dial order); the sweep jumps to the smallest active label, so
         // empty buckets cost nothing.  C2: 1 ms -> main kernel 172 -> 120 us, tables identical.
+        // AUTO on a sparse graph: buckets of the mean arc latency (C3: 9.9 ms against 11.6 for
+        // plain sweeps; 5 ms buckets 11.4, 2 ms 15.8)
         uint32_t delta = kLat32Inf;
-        if (algo == SHD_ALGO_DELTA) delta = env_u32("SHD_SSSP_DELTA", P.mean_arc_lat);
+        if (algo == SHD_ALGO_DELTA || (algo == SHD_ALGO_AUTO && !prune && env_u32("SHD_SSSP_NO_DELTA", 0) != 1))
+            delta = env_u32("SHD_SSSP_DELTA", P.mean_arc_lat);
         else if (algo == SHD_ALGO_AUTO && prune && env_u32("SHD_SSSP_NO_DELTA", 0) != 1)
             delta = env_u32("SHD_SSSP_DELTA", std::max(P.min_arc_lat, P.mean_arc_lat / 256));
         SHD_TRY(run_sssp(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
         ctx->info.algo_used = algo == SHD_ALGO_DELTA ? SHD_ALGO_DELTA
-                              : prune ? SHD_ALGO_PRUNED : SHD_ALGO_SSSP;
+                              : prune ? SHD_ALGO_PRUNED : delta != kLat32Inf ? SHD_ALGO_DELTA : SHD_ALGO_SSSP;
         SHD_TRY(read_flags(ctx));
         ovf = flag_ovf(ctx);
         float ms = 0, ms_main = 0;

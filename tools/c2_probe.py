@@ -13,7 +13,8 @@ from shadow_amd import synth  # noqa: E402
 from shadow_amd.routing import Engine  # noqa: E402
 
 eng = Engine(0)
-el = synth.complete_graph(1000, 1)
+GRAPH = os.environ.get("PROBE_GRAPH", "c2")   # c2: 1k complete graph; c3: 10k-node BA m=3
+el = synth.complete_graph(1000, 1) if GRAPH == "c2" else synth.barabasi_albert(10_000, 3, 2)
 n = prepare(eng, el)
 lat = torch.empty((n, n), dtype=torch.int64, device="cuda")
 loss = torch.empty((n, n), dtype=torch.float32, device="cuda")
@@ -24,7 +25,7 @@ for spec in sys.argv[1:]:           # "algo[:ENV=val,ENV=val]"
         k, v = kv.split("=")
         os.environ[k] = v
     ms = []
-    for rep in range(8):
+    for rep in range(8 if GRAPH == "c2" else 3):
         run_rows(eng, int(algo), 0, n, lat, loss)
         ms.append(eng.last_info()["ms_main"])
     h = (int(lat.sum().item()), int(loss.view(torch.int32).to(torch.int64).sum().item()))

@@ -1,20 +1,18 @@
-"""Summarise rocprofv3 --pmc CSVs: per kernel, mean of each counter over dispatches."""
+"""Reduce rocprofv3 --pmc passes to one CSV: mean counter value per dispatch of the kernels whose
+name contains a filter string.   python tools/pmc_summary.py <out.csv> <filter> <dir> [<dir> ...]"""
 import csv
-import glob
-import os
 import sys
 from collections import defaultdict
 
-root = sys.argv[1]
-flt = sys.argv[2] if len(sys.argv) > 2 else ""
-acc = defaultdict(lambda: defaultdict(list))
-for f in sorted(glob.glob(os.path.join(root, "p*", "run_counter_collection.csv"))):
-    for row in csv.DictReader(open(f)):
-        k = row["Kernel_Name"]
-        if flt and flt not in k:
-            continue
-        acc[k[:60]][row["Counter_Name"]].append(float(row["Counter_Value"]))
-for k, cs in acc.items():
-    print(k)
-    for c, v in sorted(cs.items()):
-        print(f"   {c:28s} {sum(v)/len(v):16.1f}  (n={len(v)})")
+out, filt, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
+acc = defaultdict(list)
+for d in dirs:
+    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+        if filt in r["Kernel_Name"]:
+            acc[(r["Kernel_Name"].split("(")[0], r["Counter_Name"])].append(float(r["Counter_Value"]))
+with open(out, "w", newline="") as f:
+    w = csv.writer(f)
+    w.writerow(["kernel", "counter", "dispatches", "mean_per_dispatch"])
+    for (k, c), v in sorted(acc.items()):
+        w.writerow([k, c, len(v), round(sum(v) / len(v), 1)])
+print(open(out).read())
