@@ -88,17 +88,35 @@ struct EqOut {
     uint64_t* tag;
 };
 
-// one wave per host: every event of its pending run and of its batch run goes to its merged
-// rank, in the popped output (rank < pop count) or the new pending run
+// One wave per host: every event of its pending run and of its batch run goes to its merged
+// rank, in the popped output (rank < pop count) or the new pending run.  The rank is a binary
+// search in the other run; both runs' deliver times are staged in LDS first (when they fit
+// kEqCapP / kEqCapB), so the searches step through LDS and touch global memory only on an equal
+// deliver time (the (src, seq) tie-break).  Every event is read and written once, coalesced.
+constexpr uint32_t kEqCapP = 640, kEqCapB = 192;   // 1024 + 256: 847 us at C5 (LDS-limited occupancy)
 __global__ __launch_bounds__(256) void eq_merge(uint32_t n_hosts, EqRuns P, EqRuns B, bool has_b,
                                                 uint64_t batch_no, const uint32_t* __restrict__ pop_off,
                                                 const uint32_t* __restrict__ keep_off, EqOut popped,
                                                 EqOut pending) {
-    const uint32_t h = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (h >= n_hosts) return;
+    __shared__ uint64_t s_p[4][kEqCapP];
+    __shared__ uint64_t s_b[4][kEqCapB];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t h = blockIdx.x * 4 + w;
+    if (h >= n_hosts) return;   // wave-uniform; the kernel has no workgroup barrier
     const uint32_t pb = P.off[h], pe = P.off[h + 1];
     const uint32_t bb = has_b ? B.off[h] : 0u, be = has_b ? B.off[h + 1] : 0u;
+    const uint32_t np = pe - pb, nb = be - bb;
     const uint32_t po = pop_off[h], npop = pop_off[h + 1] - po, ko = keep_off[h];
+    const bool stage = np <= kEqCapP && nb <= kEqCapB;
+    uint64_t* sp = s_p[w];
+    uint64_t* sb = s_b[w];
+    if (stage) {
+        for (uint32_t i = lane; i < np; i += 64) sp[i] = P.deliver[pb + i];
+        for (uint32_t j = lane; j < nb; j += 64) sb[j] = B.deliver[bb + j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     auto put = [&](uint32_t m, uint64_t t, uint32_t s, uint64_t q, uint64_t tg) {
         const EqOut& o = m < npop ? popped : pending;
         const uint32_t at = m < npop ? po + m : ko + (m - npop);
@@ -107,25 +125,42 @@ __global__ __launch_bounds__(256) void eq_merge(uint32_t n_hosts, EqRuns P, EqRu
         o.seq[at] = q;
         o.tag[at] = tg;
     };
-    for (uint32_t i = pb + lane; i < pe; i += 64) {   // pending events: rank among the batch's
-        const uint64_t t = P.deliver[i], q = P.seq[i];
-        const uint32_t s = P.src[i];
-        uint32_t a = bb, b = be;
+    for (uint32_t i = lane; i < np; i += 64) {   // pending events: rank among the batch's
+        const uint64_t t = stage ? sp[i] : P.deliver[pb + i], q = P.seq[pb + i];
+        const uint32_t s = P.src[pb + i];
+        const uint64_t tg = P.tag[pb + i];
+        uint32_t a = 0, b = nb;
         while (a < b) {
             const uint32_t m = (a + b) >> 1;
-            if (eq_less(B.deliver[m], B.src[m], B.seq[m], t, s, q)) a = m + 1; else b = m;
+            const uint64_t tm = stage ? sb[m] : B.deliver[bb + m];
+            const bool less = tm != t ? tm < t : eq_less(tm, B.src[bb + m], B.seq[bb + m], t, s, q);
+            if (less) a = m + 1; else b = m;
         }
-        put((i - pb) + (a - bb), t, s, q, P.tag[i]);
+        put(i + a, t, s, q, tg);
     }
-    for (uint32_t j = bb + lane; j < be; j += 64) {   // batch events: rank among the pending ones
-        const uint64_t t = B.deliver[j], q = B.seq[j];
-        const uint32_t s = B.src[j];
-        uint32_t a = pb, b = pe;
+    for (uint32_t j = lane; j < nb; j += 64) {   // batch events: rank among the pending ones
+        const uint64_t t = stage ? sb[j] : B.deliver[bb + j], q = B.seq[bb + j];
+        const uint32_t s = B.src[bb + j];
+        const uint64_t tg = (batch_no << 32) | B.pkt[bb + j];
+        uint32_t a = 0, b = np;
         while (a < b) {
             const uint32_t m = (a + b) >> 1;
-            if (eq_less(P.deliver[m], P.src[m], P.seq[m], t, s, q)) a = m + 1; else b = m;
+            const uint64_t tm = stage ? sp[m] : P.deliver[pb + m];
+            const bool less = tm != t ? tm < t : eq_less(tm, P.src[pb + m], P.seq[pb + m], t, s, q);
+            if (less) a = m + 1; else b = m;
         }
-        put((j - bb) + (a - pb), t, s, q, (batch_no << 32) | B.pkt[j]);
+        put(j + a, t, s, q, tg);
+    }
+}
+
+// the advance's totals (events popped, events kept, new head time) into one word triple, so the
+// host reads them with one copy
+__global__ void eq_totals(uint32_t n_hosts, const uint32_t* __restrict__ pop_off, const uint32_t* __restrict__ keep_off,
+                          const unsigned long long* __restrict__ next, uint64_t* __restrict__ out) {
+    if (threadIdx.x == 0) {
+        out[0] = pop_off[n_hosts];
+        out[1] = keep_off[n_hosts];
+        out[2] = *next;
     }
 }
 
@@ -138,7 +173,11 @@ static shd_status eq_scan(EqState& Q, const uint32_t* in, uint32_t* out, uint32_
 }
 
 static shd_status eq_alloc(EqState& Q, int k, uint64_t n) {
-    const size_t m = std::max<uint64_t>(n, 1);
+    // half again as much as asked when a buffer must grow: the pending set creeps up over the
+    // first rounds, and a reallocation (free + malloc) costs more than the merge
+    const size_t m = std::max<uint64_t>(n, 1) * 3 / 2 + 1;
+    if ((size_t)std::max<uint64_t>(n, 1) * 8 <= Q.deliver[k].bytes && (size_t)std::max<uint64_t>(n, 1) * 4 <= Q.src[k].bytes)
+        return SHD_OK;
     SHD_TRY(Q.deliver[k].ensure(m * 8));
     SHD_TRY(Q.src[k].ensure(m * 4));
     SHD_TRY(Q.seq[k].ensure(m * 8));
@@ -163,7 +202,7 @@ shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_hosts) {
     SHD_TRY(Q.pop_cnt.ensure((size_t)(n_hosts + 1) * 4));
     SHD_TRY(Q.keep_cnt.ensure((size_t)(n_hosts + 1) * 4));
     SHD_TRY(Q.pop_off.ensure((size_t)(n_hosts + 1) * 4));
-    SHD_TRY(Q.next.ensure(8));
+    SHD_TRY(Q.next.ensure(32));   // [0] head time accumulator, [1..3] totals
     SHD_HIP(hipMemsetAsync(Q.off[0].p, 0, (size_t)(n_hosts + 1) * 4, ctx->stream));
     SHD_HIP(hipStreamSynchronize(ctx->stream));
     Q.cur = 0;
@@ -192,10 +231,13 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     const uint64_t n_in = Q.n_pending + (has_b ? d_batch->n_sent : 0);
     if (n_in >= 0xFFFFFFFFull) return SHD_ERR_INVALID;   // 32-bit positions
     SHD_TRY(eq_alloc(Q, n, n_in));
-    SHD_TRY(Q.pd.ensure(std::max<uint64_t>(n_in, 1) * 8));
-    SHD_TRY(Q.ps.ensure(std::max<uint64_t>(n_in, 1) * 4));
-    SHD_TRY(Q.pq.ensure(std::max<uint64_t>(n_in, 1) * 8));
-    SHD_TRY(Q.pt.ensure(std::max<uint64_t>(n_in, 1) * 8));
+    const uint64_t n_cap = std::max<uint64_t>(n_in, 1) * 3 / 2 + 1;   // growth headroom, as eq_alloc
+    if (Q.ps.bytes < std::max<uint64_t>(n_in, 1) * 4) {
+        SHD_TRY(Q.pd.ensure(n_cap * 8));
+        SHD_TRY(Q.ps.ensure(n_cap * 4));
+        SHD_TRY(Q.pq.ensure(n_cap * 8));
+        SHD_TRY(Q.pt.ensure(n_cap * 8));
+    }
     EqRuns P{Q.off[c].as<uint32_t>(), Q.deliver[c].as<uint64_t>(), Q.src[c].as<uint32_t>(),
              Q.seq[c].as<uint64_t>(), Q.tag[c].as<uint64_t>(), nullptr};
     EqRuns B{};
@@ -217,9 +259,9 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
                                               Q.off[n].as<uint32_t>(), popped, pending);
     SHD_HIP(hipGetLastError());
     // totals and the new head time: one pinned read-back
-    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 32, Q.pop_off.as<uint32_t>() + H, 4, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 33, Q.off[n].as<uint32_t>() + H, 4, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 34, Q.next.p, 8, hipMemcpyDeviceToHost, s));
+    eq_totals<<<1, 64, 0, s>>>(H, Q.pop_off.as<uint32_t>(), Q.off[n].as<uint32_t>(),
+                               Q.next.as<unsigned long long>(), Q.next.as<uint64_t>() + 1);
+    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 32, Q.next.as<uint64_t>() + 1, 24, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     const uint32_t n_pop = (uint32_t)ctx->h_pin[32], n_keep = (uint32_t)ctx->h_pin[33];
     if ((uint64_t)n_pop + n_keep != n_in) return SHD_ERR_INVALID;   // batch ev_off / n_sent disagree
