@@ -55,14 +55,15 @@ __device__ __forceinline__ uint8_t bucket_of(uint32_t lat, float inv_delta) {
 
 template <int G, int R, bool CACHE, bool GLAB>
 __device__ __forceinline__ void relax_node(uint32_t u, uint32_t gl, uint64_t* lab, uint32_t* bits,
-                                           uint32_t scratch, const uint2* rng, const uint32_t* __restrict__ abeg,
+                                           uint32_t scratch, const uint2* rng, const uint32_t* offl,
+                                           const uint32_t* __restrict__ abeg,
                                            const uint32_t* __restrict__ aend,
                                            const uint4* __restrict__ arcs, bool& ovf, bool& dirty,
                                            uint8_t* bkt, float inv_delta, uint32_t& mnext) {
     const uint64_t ku = ld_lab<GLAB>(&lab[u]);
     const uint32_t lu = key_lat(ku);
     const float qu = one_minus(key_loss(ku));
-    const uint2 r = CACHE ? rng[u] : make_uint2(abeg[u], aend[u]);
+    const uint2 r = CACHE ? rng[u] : offl ? make_uint2(offl[u], offl[u + 1]) : make_uint2(abeg[u], aend[u]);
     for (uint32_t k0 = r.x + gl; k0 < r.y; k0 += G * R) {
         // R arc loads, then R label atomics, all issued back to back: the loads are clamped into
         // the node's range and the atomics are unconditional (a dead slot carries the +inf key,
@@ -408,7 +409,8 @@ __device__ __forceinline__ void sssp_row(
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
     uint32_t seed_stride, uint8_t* bkt, uint32_t* flat, uint32_t* nh_out, uint32_t* pred,
-    uint32_t lat_guard, const uint2* __restrict__ arcs8 = nullptr, const float* __restrict__ aq = nullptr) {
+    uint32_t lat_guard, const uint2* __restrict__ arcs8 = nullptr, const float* __restrict__ aq = nullptr,
+    uint32_t* offl = nullptr) {
     // bkt (global labels + delta-stepping): per node, the bucket of the latency that last
     // activated it, in LDS, so choosing a sweep's nodes reads no global label
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
@@ -442,10 +444,12 @@ __device__ __forceinline__ void sssp_row(
             lab[v] = l0;
         }
         if (CACHE) rng[v] = make_uint2(abeg[v], aend[v]);
+        else if (offl) offl[v] = abeg[v];
     }
     for (uint32_t w = tid; w < W; w += BLOCK) bits[w] = 0;
     if (bkt)   // unreached: the top bucket (the relax filter never skips against it)
         for (uint32_t w = tid; w < (V + 3) / 4; w += BLOCK) reinterpret_cast<uint32_t*>(bkt)[w] = 0xFFFFFFFFu;
+    if (offl && tid == 0) offl[V] = aend[V - 1];   // CSR: aend == abeg + 1
     if (!GLAB && tid < 64) lab[V + tid] = 0;   // scratch labels: no candidate improves them
     // global labels: every storing wave drains its stores before the barrier, so the L2 holds
     // them before any wave's atomics
@@ -516,7 +520,7 @@ __device__ __forceinline__ void sssp_row(
                     for (uint32_t t = 0; t < qn; t += NG) {
                         const uint32_t qi = t + grp;
                         if (qi < qn)
-                            relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
+                            relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, offl, abeg, aend, arcs,
                                                           ovf, dirty, bkt, inv_delta, mnext);
                     }
                 }
@@ -528,7 +532,7 @@ __device__ __forceinline__ void sssp_row(
                         relax_node_pad<G, PADR, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, lat_guard,
                                                        ovf, dirty, mnext);
                     else
-                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, abeg, aend, arcs,
+                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, offl, abeg, aend, arcs,
                                                       ovf, dirty, bkt, inv_delta, mnext);
                 }
             }
@@ -713,7 +717,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
-    uint32_t seed_stride, uint32_t* __restrict__ nh_out, uint32_t lat_guard) {
+    uint32_t seed_stride, uint32_t* __restrict__ nh_out, uint32_t lat_guard, uint32_t use_offl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr uint32_t NW = BLOCK / 64;
     uint64_t* lab = reinterpret_cast<uint64_t*>(smem);   // V labels + 64 per-lane scratch labels
@@ -725,11 +729,15 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     const uint32_t rng_off =
         (((uint32_t)((wq + NW * kQStride) - reinterpret_cast<uint32_t*>(smem)) * 4u) + 7u) & ~7u;
     uint2* rng = reinterpret_cast<uint2*>(smem + rng_off);
+    // !CACHE on a plain CSR (aend == abeg + 1): the offsets alone, 4 B/node, in LDS (use_offl);
+    // next hops' pred[V] then follows them
+    uint32_t* offl = !CACHE && use_offl ? reinterpret_cast<uint32_t*>(smem + rng_off) : nullptr;
+    uint32_t* pred = offl ? offl + V + 1 : reinterpret_cast<uint32_t*>(smem + rng_off);
     sssp_row<BLOCK, G, R, CACHE, false, PADR>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
                                               row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
                                               diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
                                               delta, stats, seed_lat, seed_stride, nullptr, nullptr, nh_out,
-                                              reinterpret_cast<uint32_t*>(smem + rng_off), lat_guard);
+                                              pred, lat_guard, nullptr, nullptr, offl);
 }
 
 // Kernel 1b: labels in global memory, for graphs whose labels do not fit the LDS (C4: 50k
@@ -1489,7 +1497,7 @@ struct ArcView {
 template <int BLOCK, int G, bool CACHE>
 static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, size_t lds,
                          uint64_t* d_lat, float* d_loss, uint32_t delta, const uint32_t* seed,
-                         uint32_t seed_stride) {
+                         uint32_t seed_stride, uint32_t use_offl) {
     PreparedGraph& P = ctx->prep;
     constexpr int R = G >= 32 ? 2 : G == 4 ? 2 : 4;   // arcs in flight per lane (R = 6, 8 at G = 8 measured slower on C2)
     // padded lists: labels stay below 2^32 - 1 while lu <= guard (0 = unpadded path)
@@ -1510,7 +1518,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
                                   (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
                                   (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(),
                                   (const float*)ctx->g_diag_loss.as<float>(), d_lat, d_loss, flags, unreach, delta,
-                                  stats, seed, seed_stride, ctx->nh_out, lat_guard);
+                                  stats, seed, seed_stride, ctx->nh_out, lat_guard, use_offl);
             return;
         }
     }
@@ -1518,7 +1526,8 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
                           ctx->stream, e0, e1, 0u, A.beg, A.end, A.arcs, P.V,
                           (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
                           (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(), (const float*)ctx->g_diag_loss.as<float>(),
-                          d_lat, d_loss, flags, unreach, delta, stats, seed, seed_stride, ctx->nh_out, 0u);
+                          d_lat, d_loss, flags, unreach, delta, stats, seed, seed_stride, ctx->nh_out, 0u,
+                          use_offl);
 }
 
 static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
@@ -1531,14 +1540,23 @@ template <int BLOCK, bool CACHE>
 static void launch_by_degree(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint64_t* d_lat,
                              float* d_loss, uint32_t delta, uint32_t G, const uint32_t* seed,
                              uint32_t ss) {
-    size_t lds = sssp_lds_bytes(ctx->prep.V, BLOCK, CACHE);
-    if (ctx->nh_out && !CACHE) lds = ((lds + 7) & ~(size_t)7) + (size_t)ctx->prep.V * 4;   // pred[V]
+    const uint32_t V = ctx->prep.V;
+    size_t lds = sssp_lds_bytes(V, BLOCK, CACHE);
+    if (ctx->nh_out && !CACHE) lds = ((lds + 7) & ~(size_t)7) + (size_t)V * 4;   // pred[V]
+    // no room for the {beg, end} cache: a plain CSR's offsets alone (4 B/node) when they fit
+    // (C3, 10k nodes: every relaxation's arc range from LDS instead of two dependent loads)
+    uint32_t use_offl = 0;
+    if (!CACHE && A.end == A.beg + 1 && lds + (size_t)(V + 1) * 4 + 8 <= ctx->max_lds &&
+        env_u32("SHD_SSSP_NO_OFFL", 0) != 1) {
+        lds = ((lds + 7) & ~(size_t)7) + (size_t)(V + 1) * 4;
+        use_offl = 1;
+    }
     switch (G) {
-        case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
-        case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
-        case 16: launch_group<BLOCK, 16, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
-        case 8: launch_group<BLOCK, 8, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
-        default: launch_group<BLOCK, 4, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss); break;
+        case 64: launch_group<BLOCK, 64, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, use_offl); break;
+        case 32: launch_group<BLOCK, 32, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, use_offl); break;
+        case 16: launch_group<BLOCK, 16, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, use_offl); break;
+        case 8: launch_group<BLOCK, 8, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, use_offl); break;
+        default: launch_group<BLOCK, 4, CACHE>(ctx, A, rb, re, lds, d_lat, d_loss, delta, seed, ss, use_offl); break;
     }
 }
 
