@@ -103,6 +103,7 @@ struct PreparedGraph {
     bool directed = false, narrow_arcs = false;
     uint64_t arcs = 0, max_arc_lat = 0, pruned_arcs = 0, tight_arcs = 0;
     uint32_t mean_arc_lat = 1, min_arc_lat = 1;
+    bool reordered = false;   // g_offr / g_usedr / g_arc8r / g_aqr hold the locality order
     std::vector<uint32_t> used, node_ids, es, ed;
     std::vector<uint64_t> el;
     std::vector<float> ep;
@@ -146,7 +147,8 @@ struct shd_ctx {
     shd::DevBuf d_es, d_ed, d_el, d_ep, d_col;   // direct mode edge arrays
     // routing scratch
     shd::DevBuf g_off, g_dst, g_lat, g_q, g_lat64, g_used, g_diag_lat, g_diag_loss, g_flags,
-        g_dense, g_prune_dst, g_prune_cnt, g_labels, g_aux, g_arc16, g_arc8, g_aq, g_fw, g_glab, g_pred;
+        g_dense, g_prune_dst, g_prune_cnt, g_labels, g_aux, g_arc16, g_arc8, g_aq, g_fw, g_glab, g_pred,
+        g_offr, g_usedr, g_arc8r, g_aqr;   // locality-ordered copies (global-label kernel)
     uint32_t* nh_out = nullptr;   // next-hop rows of the running build (shd_routing_run_next_hops)
 
     std::unique_ptr<shd::Comm> comm;   // multi-GPU communicator (shd_comm_init*), or none

@@ -787,6 +787,16 @@ __global__ __launch_bounds__(256) void arcs_pack(const uint32_t* __restrict__ ds
     outq[i] = q;
 }
 
+// compact arcs only (the locality-ordered copy of the global-label kernel)
+__global__ __launch_bounds__(256) void arcs_pack8(const uint32_t* __restrict__ dst, const uint32_t* __restrict__ lat,
+                                                  const float* __restrict__ loss, uint2* __restrict__ out8,
+                                                  float* __restrict__ outq, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    out8[i] = make_uint2(dst[i], lat[i]);
+    outq[i] = one_minus(loss[i]);
+}
+
 // ------------------------------------------------------------------------------------------
 // Dense-graph arc pruning (SHD_ALGO_PRUNED).  An arc (u,v) lies on no shortest-latency path if
 // some 2-hop detour u->x->v is STRICTLY shorter; such arcs cannot change any lexicographic
@@ -1187,6 +1197,14 @@ struct HostGraph {
     double sum_arc_lat = 0;
 };
 
+// Locality order for the global-label kernel (graphs whose labels leave the LDS, C4): nodes
+// renumbered in breadth-first order from the highest-degree nodes, so a node's neighbours get
+// nearby numbers -- the label reads and memory-side label atomics of one wave's relaxations then
+// share cache lines instead of hitting one line each.  Only that kernel's copies are renumbered
+// (offsets, compact arcs, the used list); results are indexed by used position, so the table is
+// unchanged.  Next hops (lowest-index tie-break in GML order) run on the original numbering.
+static shd_status prepare_reordered(shd_ctx* ctx, const HostGraph& H, const uint32_t* used, uint32_t n_used);
+
 static uint32_t gml_id(const shd_graph* g, uint32_t idx) {
     return g->node_ids ? g->node_ids[idx] : idx;
 }
@@ -1387,6 +1405,7 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
     if (mode != SHD_ROUTE_SHORTEST && mode != SHD_ROUTE_DIRECT) return SHD_ERR_INVALID;
     hipStream_t s = ctx->stream;
     P.mode = mode;
+    P.reordered = false;
     P.V = g->n_nodes;
     P.n_used = n_used;
     P.directed = g->directed != 0;
@@ -1433,6 +1452,7 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
                     ctx->g_arc16.as<uint4>(), ctx->g_arc8.as<uint2>(), ctx->g_aq.as<float>(), H.loss.size());
             P.pruned_arcs = 0;
             P.tight_arcs = 0;
+            SHD_TRY(prepare_reordered(ctx, H, used, n_used));
         }
     }
     SHD_HIP(hipStreamSynchronize(s));
@@ -1619,18 +1639,24 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
     constexpr int R = G >= 32 ? 2 : 4;
     // the events ride on the dispatch packet: the kernel's own duration, no marker gaps
     // flat + bucket bytes + delta (C4's configuration): the kernel without the other paths
-    auto kern = use_bkt && use_flat && delta != kLat32Inf ? sssp_global_group<BLOCK, G, R, true>
-                                                          : sssp_global_group<BLOCK, G, R, false>;
+    const bool fast = use_bkt && use_flat && delta != kLat32Inf;
+    auto kern = fast ? sssp_global_group<BLOCK, G, R, true> : sssp_global_group<BLOCK, G, R, false>;
+    // the locality-ordered copy (prepare_reordered) when it exists and no next hops are asked for
+    const bool ro = fast && P.reordered && !ctx->nh_out && env_u32("SHD_SSSP_NO_REORDER", 0) != 1;
+    const uint32_t* beg = ro ? ctx->g_offr.as<uint32_t>() : A.beg;
+    const uint32_t* end = ro ? ctx->g_offr.as<uint32_t>() + 1 : A.end;
+    const uint32_t* usedp = ro ? ctx->g_usedr.as<uint32_t>() : ctx->g_used.as<uint32_t>();
+    const uint2* a8 = ro ? ctx->g_arc8r.as<uint2>() : ctx->g_arc8.as<uint2>();
+    const float* aqp = ro ? ctx->g_aqr.as<float>() : ctx->g_aq.as<float>();
     hipExtLaunchKernelGGL(
         kern, dim3(grid), dim3(BLOCK), (uint32_t)lds, ctx->stream,
         ctx->time_now ? ctx->ev[2] : nullptr, ctx->time_now ? ctx->ev[3] : nullptr, 0u,
-        A.beg, A.end, A.arcs, P.V, (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb, re,
+        beg, end, A.arcs, P.V, usedp, P.n_used, rb, re,
         (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(), (const float*)ctx->g_diag_loss.as<float>(), d_lat, d_loss,
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16), delta,
         ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
         ctx->g_glab.as<uint64_t>(), use_bkt, use_flat, ctx->nh_out,
-        ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr, (const uint2*)ctx->g_arc8.as<uint2>(),
-        (const float*)ctx->g_aq.as<float>());
+        ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr, a8, aqp);
 }
 
 // Kernel 1b driver: labels in global memory (graphs whose labels exceed the LDS).
@@ -1662,7 +1688,8 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     (void)ovf;   // the caller reads the overflow flag with read_flags()
     if (ctx->stats_on) {
         unsigned long long st[2];
-        SHD_HIP(hipMemcpy(st, ctx->g_flags.as<char>() + 32, 16, hipMemcpyDeviceToHost));
+        SHD_HIP(hipMemcpyAsync(st, ctx->g_flags.as<char>() + 32, 16, hipMemcpyDeviceToHost, ctx->stream));
+        SHD_HIP(hipStreamSynchronize(ctx->stream));
         std::fprintf(stderr, "shd_sssp_global: rows=%u G=%u slots=%u delta=%u expanded=%llu (%.2f per node) "
                      "sweeps=%llu (%.1f per row)\n", re - rb, G, grid, delta, st[0],
                      (double)st[0] / ((double)(re - rb) * P.V), st[1], (double)st[1] / (re - rb));
@@ -1754,6 +1781,76 @@ static shd_status count_kept(shd_ctx* ctx, const ArcView& A) {
     for (size_t i = 0; i < b.size(); i++) k += e[i] - b[i];
     ctx->info.arcs_kept = k;
     ctx->prep.pruned_arcs = k;
+    return SHD_OK;
+}
+
+static uint32_t env_u32(const char* name, uint32_t dflt);
+static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache);
+
+static shd_status prepare_reordered(shd_ctx* ctx, const HostGraph& H, const uint32_t* used, uint32_t n_used) {
+    PreparedGraph& P = ctx->prep;
+    P.reordered = false;
+    const uint32_t V = P.V;
+    if (V == 0 || sssp_lds_bytes(V, 1024, false) <= ctx->max_lds || env_u32("SHD_SSSP_NO_REORDER", 0) == 1)
+        return SHD_OK;   // the LDS kernels take this graph
+    hipStream_t s = ctx->stream;
+    std::vector<uint32_t> deg(V), roots(V), ord, pi(V, 0xFFFFFFFFu);
+    for (uint32_t v = 0; v < V; ++v) {
+        deg[v] = H.off[v + 1] - H.off[v];
+        roots[v] = v;
+    }
+    std::stable_sort(roots.begin(), roots.end(), [&](uint32_t a, uint32_t b) { return deg[a] > deg[b]; });
+    ord.reserve(V);
+    const uint32_t mode = env_u32("SHD_REORDER_MODE", 0);   // tuning: 1 = degree order only
+    if (mode == 1)
+        for (uint32_t r : roots) {
+            pi[r] = (uint32_t)ord.size();
+            ord.push_back(r);
+        }
+    for (uint32_t r : roots) {   // breadth-first from each not yet numbered node, hubs first
+        if (pi[r] != 0xFFFFFFFFu) continue;
+        size_t head = ord.size();
+        pi[r] = (uint32_t)ord.size();
+        ord.push_back(r);
+        while (head < ord.size()) {
+            const uint32_t u = ord[head++];
+            for (uint32_t k = H.off[u]; k < H.off[u + 1]; ++k) {
+                const uint32_t w = H.dst[k];
+                if (pi[w] == 0xFFFFFFFFu) {
+                    pi[w] = (uint32_t)ord.size();
+                    ord.push_back(w);
+                }
+            }
+        }
+    }
+    const size_t A = H.dst.size();
+    std::vector<uint32_t> offr(V + 1, 0), dstr(A), latr(A), usedr(n_used);
+    std::vector<float> lossr(A);
+    for (uint32_t i = 0; i < V; ++i) {
+        const uint32_t u = ord[i];
+        uint32_t at = offr[i];
+        for (uint32_t k = H.off[u]; k < H.off[u + 1]; ++k, ++at) {
+            dstr[at] = pi[H.dst[k]];
+            latr[at] = (uint32_t)H.lat[k];
+            lossr[at] = H.loss[k];
+        }
+        offr[i + 1] = at;
+    }
+    for (uint32_t j = 0; j < n_used; ++j) usedr[j] = pi[used[j]];
+    SHD_TRY(upload(ctx->g_offr, offr, s));
+    SHD_TRY(upload(ctx->g_usedr, usedr, s));
+    DevBuf d_dst, d_lat, d_loss;
+    SHD_TRY(upload(d_dst, dstr, s));
+    SHD_TRY(upload(d_lat, latr, s));
+    SHD_TRY(upload(d_loss, lossr, s));
+    SHD_TRY(ctx->g_arc8r.ensure(std::max<size_t>(A, 1) * 8));
+    SHD_TRY(ctx->g_aqr.ensure(std::max<size_t>(A, 1) * 4));
+    if (A)
+        arcs_pack8<<<div_up(A, 256), 256, 0, s>>>(d_dst.as<uint32_t>(), d_lat.as<uint32_t>(), d_loss.as<float>(),
+                                                   ctx->g_arc8r.as<uint2>(), ctx->g_aqr.as<float>(), A);
+    SHD_HIP(hipGetLastError());
+    SHD_HIP(hipStreamSynchronize(s));   // the temporaries are freed on return
+    P.reordered = true;
     return SHD_OK;
 }
 
