@@ -222,6 +222,18 @@ shd_status shd_routing_build(shd_ctx* ctx, const shd_graph* g, const uint32_t* u
 // the source rows are independent, so the only collective is the final gather.
 // Every rank learns every rank's outcome first, so all of them return the same error (the
 // lowest rank's: its rows come first, as the reference's first failing pair would).
+// Rows per exchange chunk of shd_routing_run_sharded: about 256 MB of table per rank and chunk
+// (C4 at 8 ranks: 3.75 GB per rank in ~15 chunks), at least 4 chunks once a rank's share passes
+// 256 MB; SHD_SHARD_CHUNK_ROWS overrides (tests use it to exercise the chunked path on small
+// graphs).
+static uint64_t env_chunk_rows(uint64_t per, uint64_t row_bytes, int ranks) {
+    const char* v = std::getenv("SHD_SHARD_CHUNK_ROWS");
+    if (v && *v) return std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
+    if (ranks <= 1 || per * row_bytes <= (256ull << 20)) return per;
+    const uint64_t by_size = std::max<uint64_t>(1, (256ull << 20) / std::max<uint64_t>(row_bytes, 1));
+    return std::min<uint64_t>(by_size, (per + 3) / 4);
+}
+
 shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_full,
                                    float* d_loss_full, shd_error* err) {
     if (!ctx || !d_lat_full || !d_loss_full) return SHD_ERR_INVALID;
@@ -232,12 +244,49 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
     const uint64_t per = ((uint64_t)n + C.size - 1) / C.size;
     uint32_t rb = 0, re = 0;
     shard_range(n, C.size, C.rank, &rb, &re);
+    hipStream_t s = ctx->stream;
+    // Large tables (C4: 3.75 GB per rank) move in row chunks: chunk k goes to every peer on the
+    // side stream (grouped point-to-point) while chunk k+1 is built, so the exchange hides
+    // under the build instead of following it.  Every rank runs every chunk's exchange, also
+    // after a failure (its peers wait for it); the lowest failing rank's error is agreed at the
+    // end.  Small tables keep one all-gather.
+    const uint64_t row_bytes = (uint64_t)n * 12;
+    const uint64_t want = env_chunk_rows(per, row_bytes, C.size);
+    const uint32_t cs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(per, want));
+    const uint32_t n_chunks = C.size > 1 && cs < per ? (uint32_t)((per + cs - 1) / cs) : 1u;
     shd_error e{SHD_OK, 0, 0};
     shd_status st = SHD_OK;
-    if (re > rb)
-        st = routing_run_impl(ctx, algo, rb, re, d_lat_full + (size_t)C.rank * per * n,
-                              d_loss_full + (size_t)C.rank * per * n, &e);
-    hipStream_t s = ctx->stream;
+    auto rows_of = [&](int q, uint32_t k) -> uint32_t {   // rank q's rows in chunk k
+        uint32_t a = 0, z = 0;
+        shard_range(n, C.size, q, &a, &z);
+        const uint64_t lo = (uint64_t)k * cs, cnt = z - a;
+        return lo >= cnt ? 0u : (uint32_t)std::min<uint64_t>(cs, cnt - lo);
+    };
+    for (uint32_t k = 0; k < n_chunks; ++k) {
+        const uint32_t mine = n_chunks == 1 ? re - rb : rows_of(C.rank, k);
+        const uint32_t a = rb + (n_chunks == 1 ? 0u : k * cs);
+        const size_t at = ((size_t)C.rank * per + (size_t)(a - rb)) * n;
+        if (mine && st == SHD_OK) st = routing_run_impl(ctx, algo, a, a + mine, d_lat_full + at, d_loss_full + at, &e);
+        if (n_chunks == 1) break;
+        // the build of this chunk has completed (routing_run_impl ends with a stream sync)
+        std::vector<const void*> sp(4 * (size_t)C.size);
+        std::vector<void*> rp(4 * (size_t)C.size);
+        std::vector<size_t> sb(4 * (size_t)C.size), rbytes(4 * (size_t)C.size);
+        for (int q = 0; q < C.size; ++q) {
+            const size_t qat = ((size_t)q * per + (size_t)k * cs) * n;
+            const uint32_t theirs = rows_of(q, k);
+            sp[2 * q] = d_lat_full + at;
+            sp[2 * q + 1] = d_loss_full + at;
+            sb[2 * q] = q == C.rank ? 0 : (size_t)mine * n * 8;
+            sb[2 * q + 1] = q == C.rank ? 0 : (size_t)mine * n * 4;
+            rp[2 * q] = d_lat_full + qat;
+            rp[2 * q + 1] = d_loss_full + qat;
+            rbytes[2 * q] = q == C.rank ? 0 : (size_t)theirs * n * 8;
+            rbytes[2 * q + 1] = q == C.rank ? 0 : (size_t)theirs * n * 4;
+        }
+        SHD_TRY(C.exchange(2, sp.data(), sb.data(), rp.data(), rbytes.data(), ctx->side));
+    }
+    if (n_chunks > 1) SHD_HIP(hipStreamSynchronize(ctx->side));
     SHD_TRY(ctx->comm_scratch.ensure((size_t)(C.size + 1) * 16));
     uint64_t* w = ctx->comm_scratch.as<uint64_t>();
     ctx->h_pin[40] = ((uint64_t)(uint32_t)st << 32) | (uint32_t)e.code;
@@ -254,9 +303,11 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
                                   (uint32_t)all[2 * r + 1]};
         return sr;
     }
-    SHD_TRY(C.all_gather(d_lat_full + (size_t)C.rank * per * n, d_lat_full, per * n * 8, s));
-    SHD_TRY(C.all_gather(d_loss_full + (size_t)C.rank * per * n, d_loss_full, per * n * 4, s));
-    SHD_HIP(hipStreamSynchronize(s));
+    if (n_chunks == 1) {
+        SHD_TRY(C.all_gather(d_lat_full + (size_t)C.rank * per * n, d_lat_full, per * n * 8, s));
+        SHD_TRY(C.all_gather(d_loss_full + (size_t)C.rank * per * n, d_loss_full, per * n * 4, s));
+        SHD_HIP(hipStreamSynchronize(s));
+    }
     return SHD_OK;
 }
 
