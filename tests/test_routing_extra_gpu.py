@@ -136,3 +136,27 @@ def test_resident_table_lookups(engine):
     assert engine.smallest_latency_ns() == int(lat.min())
     st = engine.lib.shd_routing_lookup(engine.ctx, 700, 0, C.byref(C.c_uint64()), C.byref(C.c_float()))
     assert st == 5   # out of range: SHD_ERR_INVALID
+
+
+def test_kernel_timing_sampling(engine):
+    """shd_routing_set_timing: the dominant kernel is timed on every `every`-th build only
+    (ms_main = -1 on the others, 0 = never); the tables are the same either way."""
+    from shadow_amd import synth
+    el = synth.complete_graph(200, 5)
+    g = engine_graph_from_edges(el)
+    used = np.arange(200, dtype=np.uint32)
+    ref = g.compute_shortest_paths(used, engine)
+    try:
+        engine.lib.shd_routing_set_timing(engine.ctx, 3)
+        seen = []
+        for _ in range(6):
+            t = g.compute_shortest_paths(used, engine)
+            seen.append(engine.last_info()["ms_main"])
+            assert np.array_equal(t.lat, ref.lat) and np.array_equal(t.loss.view(np.uint32), ref.loss.view(np.uint32))
+        assert [m >= 0 for m in seen] == [True, False, False, True, False, False]
+        assert all(m > 0 for m in seen[::3])
+        engine.lib.shd_routing_set_timing(engine.ctx, 0)
+        g.compute_shortest_paths(used, engine)
+        assert engine.last_info()["ms_main"] == -1
+    finally:
+        engine.lib.shd_routing_set_timing(engine.ctx, 1)
