@@ -308,7 +308,8 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
                                              uint32_t* bits, const uint32_t* __restrict__ abeg,
                                              const uint32_t* __restrict__ aend, const uint2* __restrict__ arcs8,
                                              const float* __restrict__ aq, uint32_t* fx, bool& ovf, bool& dirty,
-                                             uint8_t* bkt, float inv_delta, uint32_t& mnext) {
+                                             uint8_t* bkt, float inv_delta, uint32_t& mnext, uint64_t* llab,
+                                             uint32_t kl) {
     uint32_t* pre = fx;          // [65]
     uint32_t* beg = fx + 65;     // [64]
     uint32_t* nl = fx + 129;     // [64] latency of the node's label
@@ -321,7 +322,7 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
             const uint32_t u = q[c0 + lane];
             b = abeg[u];
             deg = aend[u] - b;
-            ku = ld_lab<true>(&lab[u]);
+            ku = u < kl ? llab[u] : ld_lab<true>(&lab[u]);
         }
         uint32_t incl = deg;
 #pragma unroll
@@ -371,7 +372,7 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
             float qa[kFlatR];
 #pragma unroll
             for (int r = 0; r < kFlatR; ++r) {
-                cur[r] = ok[r] ? ld_lab<true>(&lab[a[r].x]) : 0ull;
+                cur[r] = !ok[r] ? 0ull : a[r].x < kl ? llab[a[r].x] : ld_lab<true>(&lab[a[r].x]);
                 qa[r] = ok[r] ? aq[k[r]] : 0.0f;
             }
 #pragma unroll
@@ -380,8 +381,11 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
                 const uint64_t cand = pack_key(cl[r], fold_q(qu[r], qa[r]));
                 // labels only decrease: a candidate not below the label read now cannot improve it
                 if (cand < cur[r]) {
+                    // the hottest nodes' labels live in LDS (kl, locality order: highest degree
+                        // first), the rest in the slot's global row
                     const uint64_t old =
-                        atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[r].x]), (unsigned long long)cand);
+                        a[r].x < kl ? atomicMin(reinterpret_cast<unsigned long long*>(&llab[a[r].x]), (unsigned long long)cand)
+                                    : atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[r].x]), (unsigned long long)cand);
                     if (cand < old) {
                         dirty = true;
                         const uint8_t bk = bucket_of(cl[r], inv_delta);
@@ -410,7 +414,7 @@ __device__ __forceinline__ void sssp_row(
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
     uint32_t seed_stride, uint8_t* bkt, uint32_t* flat, uint32_t* nh_out, uint32_t* pred,
     uint32_t lat_guard, const uint2* __restrict__ arcs8 = nullptr, const float* __restrict__ aq = nullptr,
-    uint32_t* offl = nullptr) {
+    uint32_t* offl = nullptr, uint64_t* llab = nullptr, uint32_t kl = 0) {
     // bkt (global labels + delta-stepping): per node, the bucket of the latency that last
     // activated it, in LDS, so choosing a sweep's nodes reads no global label
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
@@ -439,7 +443,8 @@ __device__ __forceinline__ void sssp_row(
         }
         if (GLAB) {
             if (v == src) l0 = 0;   // PathProperties::default() = (0 ns, 0.0)
-            __hip_atomic_store(&lab[v], l0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v < kl) llab[v] = l0;
+            else __hip_atomic_store(&lab[v], l0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             lab[v] = l0;
         }
@@ -512,7 +517,7 @@ __device__ __forceinline__ void sssp_row(
             if constexpr (GLAB) {
                 if constexpr (FASTG) {
                     expand_flat8(q, qn, lane, lab, bits, abeg, aend, arcs8, aq, flat + wave * kFlatWords, ovf, dirty,
-                                 bkt, inv_delta, mnext);
+                                 bkt, inv_delta, mnext, llab, kl);
                 } else if (flat) {
                     expand_flat<GLAB>(q, qn, lane, lab, bits, nullptr, abeg, aend, arcs, flat + wave * kFlatWords,
                                       ovf, dirty, bkt, inv_delta, V + lane, mnext);
@@ -689,7 +694,8 @@ __device__ __forceinline__ void sssp_row(
             l = diag_lat[j];
             p = diag_loss[j];
         } else {
-            const uint64_t k = ld_lab<GLAB>(&lab[used[j]]);
+            const uint32_t uj = used[j];
+            const uint64_t k = uj < kl ? llab[uj] : ld_lab<GLAB>(&lab[uj]);
             if (k == kKeyInf) {
                 atomicMin(unreach, (unsigned long long)((uint64_t)row * n_used + j));
                 l = ~0ull;
@@ -754,7 +760,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, uint64_t* __restrict__ glab, uint32_t use_bkt, uint32_t use_flat,
     uint32_t* __restrict__ nh_out, uint32_t* __restrict__ gpred, const uint2* __restrict__ arcs8,
-    const float* __restrict__ aq) {
+    const float* __restrict__ aq, uint32_t kl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
@@ -764,12 +770,19 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     uint8_t* bkt = use_bkt ? reinterpret_cast<uint8_t*>(wq + (BLOCK / 64) * (kQStride + (use_flat ? kFlatWords : 0)))
                            : nullptr;
     uint64_t* lab = glab + (size_t)blockIdx.x * V;
+    // kl > 0 (FASTG, no next hops): the labels of nodes [0, kl) in LDS after the bucket bytes
+    uint64_t* llab = nullptr;
+    if (FASTG && kl) {
+        const size_t at = ((size_t)((bkt + ((V + 3) / 4) * 4) - smem) + 7) & ~(size_t)7;
+        llab = reinterpret_cast<uint64_t*>(smem + at);
+    }
     for (uint32_t row = row_begin + blockIdx.x; row < row_end; row += gridDim.x) {
         sssp_row<BLOCK, G, R, false, true, 0, FASTG>(lab, bits, ctl, wq, nullptr, abeg, aend, arcs, V, used,
                                            n_used, row, (size_t)(row - row_begin) * n_used,
                                            diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
                                            delta, stats, nullptr, 0, bkt, flat, nh_out,
-                                           gpred ? gpred + (size_t)blockIdx.x * V : nullptr, 0u, arcs8, aq);
+                                           gpred ? gpred + (size_t)blockIdx.x * V : nullptr, 0u, arcs8, aq, nullptr,
+                                           llab, FASTG ? kl : 0u);
         __syncthreads();   // the next row re-initialises labels and bitmap
     }
 }
@@ -1634,7 +1647,7 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
 template <int BLOCK, int G>
 static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re, uint32_t grid,
                           size_t lds, uint64_t* d_lat, float* d_loss, uint32_t delta, uint32_t use_bkt,
-                          uint32_t use_flat) {
+                          uint32_t use_flat, uint32_t kl) {
     PreparedGraph& P = ctx->prep;
     constexpr int R = G >= 32 ? 2 : 4;
     // the events ride on the dispatch packet: the kernel's own duration, no marker gaps
@@ -1656,7 +1669,7 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16), delta,
         ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
         ctx->g_glab.as<uint64_t>(), use_bkt, use_flat, ctx->nh_out,
-        ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr, a8, aqp);
+        ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr, a8, aqp, ro ? kl : 0u);
 }
 
 // Kernel 1b driver: labels in global memory (graphs whose labels exceed the LDS).
@@ -1674,15 +1687,24 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     const uint32_t use_bkt = delta != kLat32Inf && lds_bkt <= ctx->max_lds && env_u32("SHD_SSSP_NO_BKT", 0) != 1;
     if (use_bkt) lds = lds_bkt;
     const uint32_t per_cu = std::max<uint32_t>(1, env_u32("SHD_SSSP_SLOTS", 2));
+    // labels of the first kl nodes (locality order: highest degree first) in the LDS left over by
+    // per_cu slots per CU: their relaxations take LDS atomics instead of memory-side ones
+    uint32_t kl = 0;
+    if (use_bkt && use_flat && delta != kLat32Inf && P.reordered && !ctx->nh_out &&
+        env_u32("SHD_SSSP_NO_LDS_LABELS", 0) != 1) {
+        const size_t room = ctx->max_lds / per_cu;
+        if (room > lds + 64) kl = std::min<uint32_t>(std::min<uint32_t>(P.V, P.lds_labels), (uint32_t)((room - lds - 16) / 8)) & ~63u;
+        if (kl) lds = ((lds + 7) & ~(size_t)7) + (size_t)kl * 8;
+    }
     const uint32_t grid = std::min<uint32_t>(re - rb, (uint32_t)ctx->n_cu * per_cu);
     SHD_TRY(ctx->g_glab.ensure((size_t)grid * P.V * 8));
     if (ctx->nh_out) SHD_TRY(ctx->g_pred.ensure((size_t)grid * P.V * 4));
     const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
     const uint32_t G = env_u32("SHD_SSSP_G", deg >= 64 ? 16 : deg >= 24 ? 8 : 4);
     switch (G) {
-        case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat); break;
-        case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat); break;
-        default: launch_global<BLOCK, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat); break;
+        case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
+        case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
+        default: launch_global<BLOCK, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
     }
     SHD_HIP(hipGetLastError());
     (void)ovf;   // the caller reads the overflow flag with read_flags()
@@ -1802,11 +1824,32 @@ static shd_status prepare_reordered(shd_ctx* ctx, const HostGraph& H, const uint
     std::stable_sort(roots.begin(), roots.end(), [&](uint32_t a, uint32_t b) { return deg[a] > deg[b]; });
     ord.reserve(V);
     const uint32_t mode = env_u32("SHD_REORDER_MODE", 0);   // tuning: 1 = degree order only
-    if (mode == 1)
-        for (uint32_t r : roots) {
-            pi[r] = (uint32_t)ord.size();
-            ord.push_back(r);
+    // the K highest-degree nodes first: the global kernel keeps their labels in LDS (the LDS a
+    // slot has left at 2 slots per CU, as run_sssp_global sizes it)
+    {
+        const size_t W = (V + 31) / 32;
+        const size_t lds = W * 4 + 16 + 8 * (kQStride + kFlatWords) * 4 + ((size_t)V + 3) / 4 * 4;
+        const size_t room = ctx->max_lds / 2;
+        P.lds_labels = room > lds + 64 ? (uint32_t)std::min<size_t>(V, (room - lds - 16) / 8) & ~63u : 0u;
+    }
+    const uint32_t K = mode == 1 ? V : P.lds_labels;
+    for (uint32_t i = 0; i < K && i < V; ++i) {
+        pi[roots[i]] = (uint32_t)ord.size();
+        ord.push_back(roots[i]);
+    }
+    {   // breadth-first from the hubs placed so far: their neighbours come next, together
+        size_t head = 0;
+        while (head < ord.size()) {
+            const uint32_t u = ord[head++];
+            for (uint32_t k = H.off[u]; k < H.off[u + 1]; ++k) {
+                const uint32_t w = H.dst[k];
+                if (pi[w] == 0xFFFFFFFFu) {
+                    pi[w] = (uint32_t)ord.size();
+                    ord.push_back(w);
+                }
+            }
         }
+    }
     for (uint32_t r : roots) {   // breadth-first from each not yet numbered node, hubs first
         if (pi[r] != 0xFFFFFFFFu) continue;
         size_t head = ord.size();
