@@ -1887,20 +1887,24 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     SHD_TRY(R.bin_cnt.ensure((size_t)G * (kHistSplit + 1) * n_bins * 4));
     SHD_TRY(R.bin_base.ensure((size_t)(2 * n_bins + 1) * 4));
     SHD_TRY(R.bin_lb.ensure((size_t)(n_bins + 1) * 8));
-    red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.bin_base.as<uint32_t>());
     RelayArgs3 a = relay_args3(ctx, b, rd, o);
     uint32_t* tot = R.bin_base.as<uint32_t>() + n_bins + 1;
     a.bin_base = R.bin_base.as<uint32_t>();
     a.n_bins = n_bins;
     uint32_t* seg = R.bin_cnt.as<uint32_t>() + (size_t)G * kHistSplit * n_bins;
     a.seg_pre = seg;
+    // the histogram goes first: a round starts on an idle GPU, and the host calls that set up
+    // the side stream (~20 us of them) then run while it does; the reductions' reset only has
+    // to precede the scans.  The fork event is recorded first (the side stream must follow the
+    // caller's work on the stream, e.g. the kernels that wrote the batch), the wait after.
+    if (!b->chance) SHD_HIP(hipEventRecord(ctx->sev[0], s));
+    relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
+    red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.bin_base.as<uint32_t>());
     if (!b->chance) {   // K0: the per-host generator streams, on the side stream next to the bins
-        SHD_HIP(hipEventRecord(ctx->sev[0], s));
         SHD_HIP(hipStreamWaitEvent(ctx->side, ctx->sev[0], 0));
         relay_draws<<<div_up(R.n_src, 64), 64, 0, ctx->side>>>(a, R.draws.as<uint64_t>());
         SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));
     }
-    relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
     bin_col_scan<<<div_up(n_bins, 64), 1024, 0, s>>>(G, n_bins, R.bin_cnt.as<uint32_t>(), seg, tot, a.red);
     bin_base_scan<<<1, 1024, 0, s>>>(n_bins, tot, R.bin_base.as<uint32_t>(), R.bin_lb.as<unsigned long long>(), a.red);
     if (!b->chance) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
