@@ -23,12 +23,14 @@ def _check(p, oq, H, window_end):
     assert p.next_time == (min(heads) if heads else 2**64 - 1)
 
 
-@pytest.mark.parametrize("chance_mode", [False, True])
-def test_queues_across_rounds_vs_oracle(engine, chance_mode):
+@pytest.mark.parametrize("chance_mode,H,P", [(False, 3000, 120_000), (True, 3000, 120_000), (False, 40, 40_000)])
+def test_queues_across_rounds_vs_oracle(engine, chance_mode, H, P):
+    """H=40: ~1000 events per host and round, past the merge's LDS stage (640 pending / 192
+    batch events per host), so the global-search path of eq_merge is the one checked."""
     from shadow_amd import synth
     from shadow_amd.equeue import EventQueues
     from shadow_amd.relay import Relay
-    H, NN, P = 3000, 60, 120_000
+    NN = 60
     el = synth.complete_graph(NN, 31)
     used = np.arange(NN, dtype=np.uint32)
     code, lat, loss, _ = corc.routing(NN, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
