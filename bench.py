@@ -149,7 +149,8 @@ def sharded_build(eng, world, rank, n, algo, steps, warmup, keep=False, gather=T
     barrier_sync(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
     eng.lib.shd_routing_set_timing(eng.ctx, 1)
-    out = dict(dt=dt, ms_per_step=dt / steps * 1e3, rows=re - rb, rb=rb, infos=infos,
+    built = n if (world > 1 and gather and D.routing_replicates(n, world)) else re - rb
+    out = dict(dt=dt, ms_per_step=dt / steps * 1e3, rows=built, rb=rb, infos=infos,
                kernel_ms=float(np.mean([i["ms_main"] for i in infos if i["ms_main"] >= 0] or [0.0])))
     if keep:
         k = n if (world == 1 or gather) else 0
@@ -686,8 +687,10 @@ def main():
                                "graph + self-loops, 1000 used nodes",
                    "nodes": r["n"], "arcs": int(r["arcs"]), "arcs_after_prune": int(r["arcs_kept"]),
                    "algo": int(r["algo"]),
-                   "parallelism": (f"source-row shards x{world} + engine RCCL all-gather (shd_routing_run_sharded)"
-                                   if world > 1 else "1 GPU")},
+                   "parallelism": ("1 GPU" if world == 1 else
+                                   f"whole table on each of {world} ranks (12 MB: replicated, no exchange; "
+                                   "shd_routing_run_sharded)" if r["rows"] == r["n"] else
+                                   f"source-row shards x{world} + engine RCCL all-gather (shd_routing_run_sharded)")},
         "roofline": {"bound": "valu", "achieved": r["achieved"], "peak": VALU_PEAK_TOPS,
                      "unit": "Tops/s", "frac": r["achieved"] / VALU_PEAK_TOPS,
                      "traffic": load_pmc("routing"),

@@ -287,7 +287,9 @@ shd_status shd_shard_range(uint32_t total, int32_t n_ranks, int32_t rank, uint32
 /*
  * Routing build over the communicator (after shd_routing_prepare of the same graph on every
  * rank): each rank builds its source rows into its slice of the full table, then one
- * all-gather leaves the whole table on every rank.  d_lat_full / d_loss_full are device buffers
+ * all-gather leaves the whole table on every rank (tables of at most SHD_SHARD_REPLICATE_MB MiB,
+ * default 64, are instead built whole on every rank: no exchange; shares above 256 MB per rank
+ * are exchanged in row chunks overlapping the build).  d_lat_full / d_loss_full are device buffers
  * of n_ranks * ceil(n_used / n_ranks) rows of n_used (rows >= n_used are padding).  Every rank
  * returns the same status: the lowest failing rank's error.  Replaces the rayon fan-out of
  * compute_shortest_paths (graph/mod.rs:192-210) across GPUs.

@@ -251,9 +251,17 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
     // after a failure (its peers wait for it); the lowest failing rank's error is agreed at the
     // end.  Small tables keep one all-gather.
     const uint64_t row_bytes = (uint64_t)n * 12;
+    // A small table (C2: 12 MB, built in ~0.13 ms) is built whole on every rank: the exchange
+    // (~10 MB over xGMI plus the all-gather's latency) costs more than the rows it would save.
+    // Every rank prepared the same graph and gets the same table; the status agreement below
+    // still runs, so a failure on one rank (allocation) fails every rank.
+    const char* rv = std::getenv("SHD_SHARD_REPLICATE_MB");
+    const uint64_t rep_bytes = (rv && *rv ? std::strtoull(rv, nullptr, 10) : 64ull) << 20;
+    const bool replicate = C.size > 1 && (uint64_t)n * row_bytes <= rep_bytes;
+    if (replicate) { rb = 0; re = n; }
     const uint64_t want = env_chunk_rows(per, row_bytes, C.size);
     const uint32_t cs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(per, want));
-    const uint32_t n_chunks = C.size > 1 && cs < per ? (uint32_t)((per + cs - 1) / cs) : 1u;
+    const uint32_t n_chunks = !replicate && C.size > 1 && cs < per ? (uint32_t)((per + cs - 1) / cs) : 1u;
     shd_error e{SHD_OK, 0, 0};
     shd_status st = SHD_OK;
     auto rows_of = [&](int q, uint32_t k) -> uint32_t {   // rank q's rows in chunk k
@@ -265,7 +273,7 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
     for (uint32_t k = 0; k < n_chunks; ++k) {
         const uint32_t mine = n_chunks == 1 ? re - rb : rows_of(C.rank, k);
         const uint32_t a = rb + (n_chunks == 1 ? 0u : k * cs);
-        const size_t at = ((size_t)C.rank * per + (size_t)(a - rb)) * n;
+        const size_t at = replicate ? 0 : ((size_t)C.rank * per + (size_t)(a - rb)) * n;
         if (mine && st == SHD_OK) st = routing_run_impl(ctx, algo, a, a + mine, d_lat_full + at, d_loss_full + at, &e);
         if (n_chunks == 1) break;
         // the build of this chunk has completed (routing_run_impl ends with a stream sync)
@@ -303,7 +311,7 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
                                   (uint32_t)all[2 * r + 1]};
         return sr;
     }
-    if (n_chunks == 1) {
+    if (n_chunks == 1 && !replicate) {
         SHD_TRY(C.all_gather(d_lat_full + (size_t)C.rank * per * n, d_lat_full, per * n * 8, s));
         SHD_TRY(C.all_gather(d_loss_full + (size_t)C.rank * per * n, d_loss_full, per * n * 4, s));
         SHD_HIP(hipStreamSynchronize(s));

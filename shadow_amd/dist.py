@@ -19,6 +19,7 @@ exchange and merge logic with gloo at world size 2.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 import torch
@@ -240,6 +241,13 @@ def shard_range(total: int, world: int, rank: int):
     lo, hi = C.c_uint32(0), C.c_uint32(0)
     N.check(lib.shd_shard_range(total, world, rank, C.byref(lo), C.byref(hi)), "shd_shard_range")
     return lo.value, hi.value
+
+
+def routing_replicates(n: int, world: int) -> bool:
+    """True when shd_routing_run_sharded builds the whole n x n table on every rank instead of
+    exchanging row shards (api.cpp: tables up to SHD_SHARD_REPLICATE_MB, default 64 MiB)."""
+    mb = os.environ.get("SHD_SHARD_REPLICATE_MB", "")
+    return world > 1 and n * n * 12 <= (int(mb) if mb else 64) << 20
 
 
 def routing_run_sharded(engine, algo, lat_full, loss_full):

@@ -134,12 +134,16 @@ def test_local_two_ranks_failure_is_global(engine):
             e.close()
 
 
-@pytest.mark.parametrize("chunk_rows", [None, 7, 64])
+@pytest.mark.parametrize("chunk_rows", [None, 7, 64, "replicate"])
 def test_local_two_ranks_routing_sharded(engine, monkeypatch, chunk_rows):
     """Row shards + the table exchange: one all-gather, or row chunks exchanged while the next
     chunk is built (SHD_SHARD_CHUNK_ROWS forces the chunked path on a small graph; 7 leaves a
-    short last chunk, 64 a rank whose last chunk is shorter than its peer's)."""
-    if chunk_rows:
+    short last chunk, 64 a rank whose last chunk is shorter than its peer's); "replicate" is the
+    small-table default, every rank building the whole table (SHD_SHARD_REPLICATE_MB=0 turns it
+    off for the exchange cases)."""
+    if chunk_rows != "replicate":
+        monkeypatch.setenv("SHD_SHARD_REPLICATE_MB", "0")
+    if chunk_rows not in (None, "replicate"):
         monkeypatch.setenv("SHD_SHARD_CHUNK_ROWS", str(chunk_rows))
     import torch
     from shadow_amd import dist as D
