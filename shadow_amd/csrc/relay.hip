@@ -322,6 +322,7 @@ struct RelayArgs3 {
     const uint32_t* bin_base;
     const uint32_t* seg_pre;
     uint32_t n_bins;
+    uint32_t gs;         // hosts per group of relay_stamp_v6 / relay_bin_hist (<= kS5Hosts)
 };
 
 constexpr uint32_t kDrawSlice = 16;   // draws per host per LDS transpose (16: 43 us vs 47 at 8 on C5)
@@ -578,7 +579,10 @@ __global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint64
 // dominant cost -- becomes an LDS read.  One persistent 1024-thread workgroup per CU loads the
 // packed map once and walks the host groups (kS5Hosts hosts each, in source-node order).
 constexpr uint32_t kS6Threads = 1024;
-constexpr uint32_t kS6Per = 4;
+#ifndef SHD_S6PER
+#define SHD_S6PER 4   // sends per thread and chunk (5 and 6 spill registers: slower)
+#endif
+constexpr uint32_t kS6Per = SHD_S6PER;
 constexpr uint32_t kS6Cap = kS6Threads * kS6Per;
 constexpr uint32_t kS6FixedLds = kS5RowLds * 8 + (kS6Cap + 2) * 2 + kS6Cap + 4096;   // rows + scan + owners + small
 
@@ -632,7 +636,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     for (uint32_t i = tid; i < n_words; i += kS6Threads) s_tbl[i] = packed[i];
     if (BIN)
         for (uint32_t i = tid; i < (a.n_bins + 3) / 4; i += kS6Threads) s_cur[i] = 0;
-    const uint32_t n_groups = (a.n_src + kS5Hosts - 1) / kS5Hosts;
+    const uint32_t n_groups = (a.n_src + a.gs - 1) / a.gs;
     uint64_t min_d = ~0ull, min_l = ~0ull, ns_total = 0;
     bool wide = false, disorder = false;
     // wave 0 keeps the next group's host descriptors in registers: order[] is fetched when a
@@ -640,16 +644,16 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     // path rows are staged, so neither latency sits on the critical path of the next group
     uint32_t p_h = 0, p_b = 0, p_len = 0, p_nd = 0, p_base = 0;
     auto fetch_hosts = [&](uint32_t g) {
-        const uint32_t hh0 = g * kS5Hosts;
-        if (g < n_groups && tid < min(kS5Hosts, a.n_src - hh0)) {
+        const uint32_t hh0 = g * a.gs;
+        if (g < n_groups && tid < min(a.gs, a.n_src - hh0)) {
             p_b = a.src_off[p_h - a.src_lo];
             p_len = a.src_off[p_h - a.src_lo + 1] - p_b;
             p_nd = a.host_node[p_h];
             p_base = a.abs_seq ? (uint32_t)a.next_id[p_h] : 0u;
         }
     };
-    if (tid < 64 && blockIdx.x < n_groups && tid < min(kS5Hosts, a.n_src - blockIdx.x * kS5Hosts)) {
-        p_h = a.order[blockIdx.x * kS5Hosts + tid];
+    if (tid < 64 && blockIdx.x < n_groups && tid < min(a.gs, a.n_src - blockIdx.x * a.gs)) {
+        p_h = a.order[blockIdx.x * a.gs + tid];
     }
     if (tid < 64) fetch_hosts(blockIdx.x);
     // 16 threads per host slot fill the owner map of the chunk starting at position cb
@@ -663,8 +667,8 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     };
     const uint64_t* __restrict__ rsrc = a.chance ? reinterpret_cast<const uint64_t*>(a.chance) : draw;
     for (uint32_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
-        const uint32_t h0 = grp * kS5Hosts;
-        const uint32_t nh = min(kS5Hosts, a.n_src - h0);
+        const uint32_t h0 = grp * a.gs;
+        const uint32_t nh = min(a.gs, a.n_src - h0);
         const uint32_t nxt = grp + gridDim.x;
         __syncthreads();   // the previous group's host arrays / rows are no longer read
         SP_MARK(0);
@@ -679,8 +683,8 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 s_run[tid] = 0;
                 s_base[tid] = p_base;
             }
-            if (nxt < n_groups && tid < min(kS5Hosts, a.n_src - nxt * kS5Hosts))
-                p_h = a.order[nxt * kS5Hosts + tid];
+            if (nxt < n_groups && tid < min(a.gs, a.n_src - nxt * a.gs))
+                p_h = a.order[nxt * a.gs + tid];
             uint32_t incl = len;
             for (uint32_t o = 1; o < 64; o <<= 1) {
                 const uint32_t y = __shfl_up(incl, o);
@@ -723,7 +727,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
         for (uint32_t c0 = 0; c0 < T; c0 += kS6Cap) {
             const uint32_t cn = min(kS6Cap, T - c0);
             if (c0 == 0 && tid < 64) {   // the next group's distinct source nodes, as at its start
-                const uint32_t nh2 = nxt < n_groups ? min(kS5Hosts, a.n_src - nxt * kS5Hosts) : 0u;
+                const uint32_t nh2 = nxt < n_groups ? min(a.gs, a.n_src - nxt * a.gs) : 0u;
                 const uint32_t nd = p_nd, prev = __shfl_up(nd, 1);
                 const bool first = tid < nh2 && (tid == 0 || nd != prev);
                 const uint64_t fm = __ballot(first);
@@ -945,6 +949,8 @@ __device__ __forceinline__ bool rec_less(const uint4& a, const uint4& b) {
 
 constexpr uint32_t kWaveSeg = 256;
 
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, uint32_t j, uint32_t lane);
+
 // Bitonic sort of 64 * NPL keys held NPL per lane (element e = lane + 64 c), ascending.
 template <int NPL>
 __device__ __forceinline__ void wave_bitonic(uint64_t (&k)[NPL], uint32_t lane) {
@@ -960,7 +966,7 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&k)[NPL], uint32_t lane) 
                         const uint32_t e = lane + 64u * c;
                         const bool asc = (e & kk) == 0;
                         const uint64_t x = k[c], y = k[c | cj];
-                        const bool sw = asc ? (y < x) : (x < y);
+                        const bool sw = (y < x) == asc;   // equal keys: the swap is a no-op
                         k[c] = sw ? y : x;
                         k[c | cj] = sw ? x : y;
                     }
@@ -969,11 +975,13 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&k)[NPL], uint32_t lane) 
 #pragma unroll
                 for (int c = 0; c < NPL; ++c) {
                     const uint32_t e = lane + 64u * c;
-                    const uint64_t o = __shfl_xor(k[c], (int)j);
+                    const uint32_t olo = xor_lane((uint32_t)k[c], j, lane);
+                    const uint32_t ohi = xor_lane((uint32_t)(k[c] >> 32), j, lane);
+                    const uint64_t o = ((uint64_t)ohi << 32) | olo;
                     const bool lower = (lane & j) == 0;
                     const bool asc = (e & kk) == 0;
                     const bool take_min = lower == asc;
-                    k[c] = take_min ? (o < k[c] ? o : k[c]) : (o > k[c] ? o : k[c]);
+                    k[c] = (o < k[c]) == take_min ? o : k[c];
                 }
             }
         }
@@ -1420,9 +1428,9 @@ __global__ __launch_bounds__(256) void relay_bin_hist(RelayArgs3 a, uint32_t G, 
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t g = blockIdx.x / kHistSplit, k = blockIdx.x % kHistSplit;
     for (uint32_t i = tid; i < a.n_bins; i += 256) s_cnt[i] = 0;
-    const uint32_t n_groups = (a.n_src + kS5Hosts - 1) / kS5Hosts;
+    const uint32_t n_groups = (a.n_src + a.gs - 1) / a.gs;
     for (uint32_t grp = g + k * G; grp < n_groups; grp += kHistSplit * G) {
-        const uint32_t h0 = grp * kS5Hosts, nh = min(kS5Hosts, a.n_src - h0);
+        const uint32_t h0 = grp * a.gs, nh = min(a.gs, a.n_src - h0);
         __syncthreads();
         if (tid < 64) {
             uint32_t len = 0;
@@ -1555,7 +1563,7 @@ __device__ __forceinline__ void wave_bitonic64(uint64_t (&k)[NPL], uint32_t lane
                     if ((c & cj) == 0) {
                         const bool asc = ((lane + 64u * c) & kk) == 0;
                         const uint64_t x = k[c], y = k[c | cj];
-                        const bool sw = asc ? (y < x) : (x < y);
+                        const bool sw = (y < x) == asc;   // unique keys
                         k[c] = sw ? y : x;
                         k[c | cj] = sw ? x : y;
                     }
@@ -1566,8 +1574,10 @@ __device__ __forceinline__ void wave_bitonic64(uint64_t (&k)[NPL], uint32_t lane
                     const uint32_t lo = xor_lane((uint32_t)k[c], j, lane);
                     const uint32_t hi = xor_lane((uint32_t)(k[c] >> 32), j, lane);
                     const uint64_t o = ((uint64_t)hi << 32) | lo;
+                    // keys are unique: take the partner's key iff it is smaller where this lane
+                    // keeps the minimum (one 64-bit compare, one select)
                     const bool take_min = ((lane & j) == 0) == (((lane + 64u * c) & kk) == 0);
-                    k[c] = take_min ? (o < k[c] ? o : k[c]) : (o > k[c] ? o : k[c]);
+                    k[c] = (o < k[c]) == take_min ? o : k[c];
                 }
             }
         }
@@ -1773,6 +1783,7 @@ static RelayArgs3 relay_args3(shd_ctx* ctx, const shd_batch* b, const shd_round*
     const uint64_t n = b->n_packets;
     const uint32_t H = R.n_hosts;
     RelayArgs3 a{};
+    a.gs = kS5Hosts;
     a.n_hosts = H;
     a.n_nodes = R.n_nodes;
     a.src_lo = R.src_lo;
@@ -1873,6 +1884,20 @@ static bool relay_v7_ok(shd_ctx* ctx, uint64_t n) {
     return stat_lds + (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4 <= 160 * 1024;
 }
 
+// Hosts per stamp group: about S sends per group (SHD_RELAY_GROUP_SENDS, 0 = fixed kS5Hosts),
+// so a group is one full chunk of the stamp, and a group count that is a multiple of the stamp's
+// G workgroups, so no pass of the persistent grid runs with most workgroups idle.
+static uint32_t v7_group_size(uint32_t n_src, uint32_t G, uint64_t n) {
+    const char* v = std::getenv("SHD_RELAY_GROUP_SENDS");
+    // default: one chunk's worth (C5: 40 hosts, ~4000 sends; stamp 310 -> 283 us; 36 hosts: 290)
+    const uint64_t S = v && *v ? std::strtoull(v, nullptr, 10) : (uint64_t)kS6Cap;
+    if (!S || !n || !n_src || !G) return kS5Hosts;
+    const double per_host = (double)n / n_src;
+    const uint32_t want = (uint32_t)std::min<double>(kS5Hosts, std::max<double>(8.0, (double)S / per_host));
+    const uint64_t m = div_up((uint64_t)n_src, (uint64_t)G * want);
+    return (uint32_t)std::min<uint64_t>(kS5Hosts, std::max<uint64_t>(1, div_up((uint64_t)n_src, (uint64_t)G * m)));
+}
+
 static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
                                   shd_relay_out* o) {
     RelayState& R = ctx->relay;
@@ -1888,6 +1913,7 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     SHD_TRY(R.bin_base.ensure((size_t)(2 * n_bins + 1) * 4));
     SHD_TRY(R.bin_lb.ensure((size_t)(n_bins + 1) * 8));
     RelayArgs3 a = relay_args3(ctx, b, rd, o);
+    a.gs = v7_group_size(R.n_src, G, n);
     uint32_t* tot = R.bin_base.as<uint32_t>() + n_bins + 1;
     a.bin_base = R.bin_base.as<uint32_t>();
     a.n_bins = n_bins;
