@@ -48,11 +48,21 @@ struct CodelState {   // CoDel router queues (codel.hip)
     bool ready = false;
 };
 
-struct EqState {   // destination event queues (equeue.hip): pending runs, double-buffered
-    DevBuf off[2], deliver[2], src[2], seq[2], tag[2];
-    DevBuf pd, ps, pq, pt;                       // the last call's popped events
-    DevBuf pop_cnt, keep_cnt, pop_off, next, scan_tmp;
-    int cur = 0;
+constexpr int kEqMaxRuns = 8;   // stored runs of the event queues before they are compacted
+
+struct EqRunBuf {   // one stored run of the event queues: a CSR of per-host sorted events
+    DevBuf off, deliver, src, seq, tag;
+    uint64_t n = 0, left = 0;   // events stored / not yet popped
+    bool live = false;
+};
+
+struct EqState {   // destination event queues (equeue.hip): a list of sorted runs (one per batch)
+    EqRunBuf run[kEqMaxRuns + 1];   // slots; one more than kEqMaxRuns for the compaction target
+    DevBuf curs[2];                 // [kEqMaxRuns + 1][n_hosts] u32 cursors (first unpopped), double-buffered
+    DevBuf bcut;                    // [n_hosts] the batch's first kept event per host
+    DevBuf pd, ps, pq, pt;          // the last call's popped events
+    DevBuf pop_cnt, keep_cnt, pop_off, next, left, scan_tmp;
+    int ccur = 0;
     uint32_t n_hosts = 0;
     uint64_t n_pending = 0, n_popped = 0, batches = 0;
     bool ready = false;

@@ -8,13 +8,18 @@
 // remains waits for a later round (a latency longer than one window keeps an event pending for
 // several rounds).  next_event_time() is the head's time (event_queue.rs:43-45).
 //
-// Here the packet events of all destinations of this GPU stay on the device as one CSR of
-// per-host runs sorted by (deliver, src, seq).  One call (shd_equeue_advance) merges a round's
-// batch (the relay output: per destination already in that order) into the pending runs and
-// splits the merged runs at window_end: the prefix is handed back for Host::execute, the suffix
-// stays pending.  Keys are unique ((src, seq) never repeats: event ids are per-host monotone),
-// so every event's merged rank is its index in its own run plus the number of smaller events in
-// the other run -- a binary search, no atomics, deterministic.
+// Here the pending packet events of all destinations of this GPU are a short list of RUNS, one
+// per batch (the relay output of a round: per destination already in that order), each a CSR
+// of per-host sorted events with a per-host cursor (its first unpopped event).  An advance
+// (shd_equeue_advance) never rewrites the pending events: per host it finds every run's prefix
+// below window_end (a binary search from the cursor), merges those prefixes and the batch's into
+// the popped output -- an event's rank is its index in its own run plus the number of smaller
+// events in each other run, binary searches over the deliver times staged in LDS, no atomics,
+// deterministic (keys are unique: (src, seq) never repeats) -- moves the cursors, and stores the
+// batch's remainder as a new run.  A run whose events are all popped is dropped; when
+// kEqMaxRuns runs are alive, they are first compacted into one (the same merge, every event).
+// Traffic per advance ~ the batch (read + its remainder written) + the popped events (read +
+// written), instead of every pending event read and written each round.
 #include <algorithm>
 #include <cstring>
 
@@ -24,13 +29,24 @@
 
 namespace shd {
 
-struct EqRuns {   // a CSR of per-host runs
-    const uint32_t* off;
+constexpr uint32_t kEqSrcMax = kEqMaxRuns + 1;   // the stored runs + the incoming batch
+
+struct EqSrc {   // one source of an advance: a stored run (from its cursor) or the batch
+    const uint32_t* off;       // [n_hosts + 1]
+    const uint32_t* lo;        // stored run: per-host cursor; batch: nullptr (= off)
+    uint32_t* cut;             // per host: first event not popped (eqr_count writes, eqr_merge reads)
     const uint64_t* deliver;
     const uint32_t* src;
     const uint64_t* seq;
-    const uint64_t* tag;   // pending runs: the packet tag; batch runs: nullptr (tag from pkt)
-    const uint32_t* pkt;   // batch runs only
+    const uint64_t* tag;       // stored run
+    const uint32_t* pkt;       // batch: tag = batch << 32 | pkt
+    uint64_t batch;
+};
+
+struct EqSrcs {
+    EqSrc s[kEqSrcMax];
+    uint32_t n;
+    int32_t b;   // index of the batch source, -1 without one
 };
 
 __device__ __forceinline__ bool eq_less(uint64_t ta, uint32_t sa, uint64_t qa, uint64_t tb, uint32_t sb,
@@ -48,37 +64,65 @@ __device__ __forceinline__ uint32_t lower_bound_time(const uint64_t* t, uint32_t
     return b;
 }
 
-// per host: events of the merged run that are popped (deliver < window_end) and kept; the
-// time of the first kept event (the queue head after the pop) into next[0] by atomic min
-__global__ __launch_bounds__(256) void eq_count(uint32_t n_hosts, EqRuns P, EqRuns B, bool has_b,
-                                                uint64_t window_end, uint32_t* __restrict__ pop,
-                                                uint32_t* __restrict__ keep,
-                                                unsigned long long* __restrict__ next) {
-    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
-    uint64_t head = ~0ull;
-    if (h < n_hosts) {
-        const uint32_t pb = P.off[h], pe = P.off[h + 1];
-        const uint32_t lp = lower_bound_time(P.deliver, pb, pe, window_end);
-        uint32_t np = lp - pb, nk = pe - lp;
-        if (lp < pe) head = P.deliver[lp];
-        if (has_b) {
-            const uint32_t bb = B.off[h], be = B.off[h + 1];
-            const uint32_t lb = lower_bound_time(B.deliver, bb, be, window_end);
-            np += lb - bb;
-            nk += be - lb;
-            if (lb < be) head = B.deliver[lb] < head ? B.deliver[lb] : head;
+// Q.next layout (one read-back per call): [0] unused, [1] popped, [2] kept batch events, [3] head
+// time, [4 + k] events of source k left after the pop; then eqr_count's per-block partials
+constexpr uint32_t kEqWords = 4 + kEqSrcMax;
+
+// per host and source: the cut (first event at or past window_end); popped count per host, the
+// batch's kept count per host, events left per source and the earliest kept deliver time.
+// kEqLanes lanes per host, lane k on source k: the sources' binary searches run side by side.
+constexpr uint32_t kEqLanes = 16;
+static_assert(kEqSrcMax <= kEqLanes, "a lane per source");
+
+constexpr uint32_t kEqCountBlocks = 1024;   // eqr_count's grid: per-block partials, no hot atomics
+constexpr uint32_t kEqPart = 1 + kEqSrcMax;  // partial words per block: head time, left per source
+
+__global__ __launch_bounds__(256) void eqr_count(uint32_t n_hosts, EqSrcs S, uint64_t window_end,
+                                                 uint32_t* __restrict__ pop, uint32_t* __restrict__ keep,
+                                                 unsigned long long* __restrict__ part) {
+    __shared__ unsigned long long s_w[4][kEqPart];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t total = ((uint64_t)n_hosts + 1) * kEqLanes;
+    uint64_t head = ~0ull, rem_acc = 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t - threadIdx.x < total;
+         t += (uint64_t)gridDim.x * 256) {   // wave-uniform trip count (total is a multiple of 16)
+        const uint32_t h = (uint32_t)(t / kEqLanes), k = (uint32_t)(t % kEqLanes);
+        uint32_t np = 0;
+        uint64_t rem = 0;
+        if (h < n_hosts && k < S.n) {
+            const EqSrc& q = S.s[k];
+            const uint32_t lo = q.lo ? q.lo[h] : q.off[h], hi = q.off[h + 1];
+            const uint32_t m = lower_bound_time(q.deliver, lo, hi, window_end);
+            q.cut[h] = m;
+            np = m - lo;
+            rem = hi - m;
+            if (m < hi) head = q.deliver[m] < head ? q.deliver[m] : head;
+            if ((int32_t)k == S.b) keep[h] = (uint32_t)rem;
         }
-        pop[h] = np;
-        keep[h] = nk;
-    } else if (h == n_hosts) {
-        pop[h] = 0;
-        keep[h] = 0;
+        for (uint32_t o = kEqLanes / 2; o > 0; o >>= 1) np += __shfl_xor(np, o);
+        if (h < n_hosts && k == 0) pop[h] = np;
+        if (h == n_hosts && k == 0) {
+            pop[n_hosts] = 0;
+            keep[n_hosts] = 0;
+        }
+        rem_acc += rem;   // lane k mod kEqLanes keeps source k's sum
     }
+    for (uint32_t o = kEqLanes; o < 64; o <<= 1) rem_acc += __shfl_xor(rem_acc, o);
     for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t w = __shfl_xor(head, o);
-        head = w < head ? w : head;
+        const uint64_t x = __shfl_xor(head, o);
+        head = x < head ? x : head;
     }
-    if ((threadIdx.x & 63) == 0 && head != ~0ull) atomicMin(next, (unsigned long long)head);
+    if (lane < kEqSrcMax) s_w[w][1 + lane] = rem_acc;
+    if (lane == 0) s_w[w][0] = head;
+    __syncthreads();
+    if (threadIdx.x < kEqPart) {
+        unsigned long long v = s_w[0][threadIdx.x];
+        for (int ww = 1; ww < 4; ++ww) {
+            const unsigned long long x = s_w[ww][threadIdx.x];
+            v = threadIdx.x == 0 ? (x < v ? x : v) : v + x;
+        }
+        part[(size_t)blockIdx.x * kEqPart + threadIdx.x] = v;
+    }
 }
 
 struct EqOut {
@@ -88,79 +132,165 @@ struct EqOut {
     uint64_t* tag;
 };
 
-// One wave per host: every event of its pending run and of its batch run goes to its merged
-// rank, in the popped output (rank < pop count) or the new pending run.  The rank is a binary
-// search in the other run; both runs' deliver times are staged in LDS first (when they fit
-// kEqCapP / kEqCapB), so the searches step through LDS and touch global memory only on an equal
-// deliver time (the (src, seq) tie-break).  Every event is read and written once, coalesced.
-constexpr uint32_t kEqCapP = 640, kEqCapB = 192;   // 1024 + 256: 847 us at C5 (LDS-limited occupancy)
-__global__ __launch_bounds__(256) void eq_merge(uint32_t n_hosts, EqRuns P, EqRuns B, bool has_b,
-                                                uint64_t batch_no, const uint32_t* __restrict__ pop_off,
-                                                const uint32_t* __restrict__ keep_off, EqOut popped,
-                                                EqOut pending) {
-    __shared__ uint64_t s_p[4][kEqCapP];
-    __shared__ uint64_t s_b[4][kEqCapB];
+// One wave per host: every source's popped prefix [lo, cut) goes to its merged rank in the
+// popped output: its index in its own prefix + the number of smaller events in each other
+// prefix.  When the host's popped events fit kEqStage, the prefixes are staged in LDS (whole
+// events, source after source, coalesced loads), every lane then takes one staged event and
+// binary-searches the other prefixes in LDS; larger hosts search global memory source by
+// source.  Then the batch's remainder [cut, end) is copied to the new run (nrun), whose cursor
+// starts at its offset.
+constexpr uint32_t kEqStage = 256;
+
+__global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, const uint32_t* __restrict__ pop_off,
+                                                 EqOut popped, EqOut nrun, const uint32_t* __restrict__ nrun_off,
+                                                 uint32_t* __restrict__ nrun_cur) {
+    __shared__ uint64_t s_t[4][kEqStage], s_q[4][kEqStage], s_g[4][kEqStage];
+    __shared__ uint32_t s_s[4][kEqStage];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t h = blockIdx.x * 4 + w;
     if (h >= n_hosts) return;   // wave-uniform; the kernel has no workgroup barrier
-    const uint32_t pb = P.off[h], pe = P.off[h + 1];
-    const uint32_t bb = has_b ? B.off[h] : 0u, be = has_b ? B.off[h + 1] : 0u;
-    const uint32_t np = pe - pb, nb = be - bb;
-    const uint32_t po = pop_off[h], npop = pop_off[h + 1] - po, ko = keep_off[h];
-    const bool stage = np <= kEqCapP && nb <= kEqCapB;
-    uint64_t* sp = s_p[w];
-    uint64_t* sb = s_b[w];
-    if (stage) {
-        for (uint32_t i = lane; i < np; i += 64) sp[i] = P.deliver[pb + i];
-        for (uint32_t j = lane; j < nb; j += 64) sb[j] = B.deliver[bb + j];
+    // lane k < S.n holds source k's popped range and its place in the LDS stage
+    uint32_t my_lo = 0, my_m = 0;
+    for (uint32_t k = 0; k < S.n; ++k) {
+        const EqSrc& q = S.s[k];
+        const uint32_t lo = q.lo ? q.lo[h] : q.off[h], m = q.cut[h];
+        if (lane == k) {
+            my_lo = lo;
+            my_m = m;
+        }
+    }
+    const uint32_t cnt = my_m - my_lo;
+    uint32_t incl = cnt;
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const uint32_t my_sb = incl - cnt, npop = __shfl(incl, 63);
+    // every source's range as wave-uniform values (read while all lanes are active: a lane read
+    // from inside the divergent loops below would see inactive lanes as 0)
+    uint32_t u_lo[kEqSrcMax], u_c[kEqSrcMax], u_sb[kEqSrcMax];
+#pragma unroll
+    for (uint32_t k = 0; k < kEqSrcMax; ++k) {
+        u_lo[k] = __builtin_amdgcn_readlane(my_lo, k);
+        u_c[k] = __builtin_amdgcn_readlane(cnt, k);
+        u_sb[k] = __builtin_amdgcn_readlane(my_sb, k);
+    }
+    const uint32_t po = pop_off[h];
+    if (npop <= kEqStage) {
+        uint64_t* st = s_t[w];
+        uint64_t* sq = s_q[w];
+        uint64_t* sg = s_g[w];
+        uint32_t* ss = s_s[w];
+        for (uint32_t k = 0; k < S.n; ++k) {
+            const EqSrc& q = S.s[k];
+            const uint32_t lo = u_lo[k], c = u_c[k], sb = u_sb[k];
+            for (uint32_t i = lane; i < c; i += 64) {
+                st[sb + i] = q.deliver[lo + i];
+                sq[sb + i] = q.seq[lo + i];
+                ss[sb + i] = q.src[lo + i];
+                sg[sb + i] = q.tag ? q.tag[lo + i] : ((q.batch << 32) | q.pkt[lo + i]);
+            }
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    auto put = [&](uint32_t m, uint64_t t, uint32_t s, uint64_t q, uint64_t tg) {
-        const EqOut& o = m < npop ? popped : pending;
-        const uint32_t at = m < npop ? po + m : ko + (m - npop);
-        o.deliver[at] = t;
-        o.src[at] = s;
-        o.seq[at] = q;
-        o.tag[at] = tg;
-    };
-    for (uint32_t i = lane; i < np; i += 64) {   // pending events: rank among the batch's
-        const uint64_t t = stage ? sp[i] : P.deliver[pb + i], q = P.seq[pb + i];
-        const uint32_t s = P.src[pb + i];
-        const uint64_t tg = P.tag[pb + i];
-        uint32_t a = 0, b = nb;
-        while (a < b) {
-            const uint32_t m = (a + b) >> 1;
-            const uint64_t tm = stage ? sb[m] : B.deliver[bb + m];
-            const bool less = tm != t ? tm < t : eq_less(tm, B.src[bb + m], B.seq[bb + m], t, s, q);
-            if (less) a = m + 1; else b = m;
+        for (uint32_t i0 = lane; i0 < npop; i0 += 64) {
+            uint32_t k = 0;   // staged event i0 belongs to source k: u_sb[k] <= i0 < u_sb[k + 1]
+            for (uint32_t j = 1; j < S.n; ++j) k = u_sb[j] <= i0 ? j : k;
+            const uint64_t t = st[i0], qq = sq[i0];
+            const uint32_t sv = ss[i0];
+            uint32_t rank = i0 - u_sb[k];
+            for (uint32_t k2 = 0; k2 < S.n; ++k2) {
+                if (k2 == k) continue;
+                const uint32_t sb2 = u_sb[k2];
+                uint32_t a = 0, b = u_c[k2];
+                while (a < b) {
+                    const uint32_t m = (a + b) >> 1, x = sb2 + m;
+                    const uint64_t tm = st[x];
+                    const bool less = tm != t ? tm < t : eq_less(tm, ss[x], sq[x], t, sv, qq);
+                    if (less) a = m + 1; else b = m;
+                }
+                rank += a;
+            }
+            popped.deliver[po + rank] = t;
+            popped.src[po + rank] = sv;
+            popped.seq[po + rank] = qq;
+            popped.tag[po + rank] = sg[i0];
         }
-        put(i + a, t, s, q, tg);
-    }
-    for (uint32_t j = lane; j < nb; j += 64) {   // batch events: rank among the pending ones
-        const uint64_t t = stage ? sb[j] : B.deliver[bb + j], q = B.seq[bb + j];
-        const uint32_t s = B.src[bb + j];
-        const uint64_t tg = (batch_no << 32) | B.pkt[bb + j];
-        uint32_t a = 0, b = np;
-        while (a < b) {
-            const uint32_t m = (a + b) >> 1;
-            const uint64_t tm = stage ? sp[m] : P.deliver[pb + m];
-            const bool less = tm != t ? tm < t : eq_less(tm, P.src[pb + m], P.seq[pb + m], t, s, q);
-            if (less) a = m + 1; else b = m;
+    } else {
+        for (uint32_t k = 0; k < S.n; ++k) {
+            const EqSrc& q = S.s[k];
+            const uint32_t lo = u_lo[k], c = u_c[k];
+            for (uint32_t i = lane; i < c; i += 64) {
+                const uint64_t t = q.deliver[lo + i], qq = q.seq[lo + i];
+                const uint32_t sv = q.src[lo + i];
+                const uint64_t tg = q.tag ? q.tag[lo + i] : ((q.batch << 32) | q.pkt[lo + i]);
+                uint32_t rank = i;
+                for (uint32_t k2 = 0; k2 < S.n; ++k2) {
+                    if (k2 == k) continue;
+                    const EqSrc& r = S.s[k2];
+                    const uint32_t lo2 = u_lo[k2];
+                    uint32_t a = 0, b = u_c[k2];
+                    while (a < b) {
+                        const uint32_t m = (a + b) >> 1;
+                        const uint64_t tm = r.deliver[lo2 + m];
+                        const bool less = tm != t ? tm < t : eq_less(tm, r.src[lo2 + m], r.seq[lo2 + m], t, sv, qq);
+                        if (less) a = m + 1; else b = m;
+                    }
+                    rank += a;
+                }
+                popped.deliver[po + rank] = t;
+                popped.src[po + rank] = sv;
+                popped.seq[po + rank] = qq;
+                popped.tag[po + rank] = tg;
+            }
         }
-        put(j + a, t, s, q, tg);
+    }
+    if (S.b >= 0) {   // the batch's remainder becomes the new run
+        const EqSrc& q = S.s[S.b];
+        const uint32_t m = q.cut[h], e = q.off[h + 1], no = nrun_off[h];
+        for (uint32_t j = m + lane; j < e; j += 64) {
+            const uint32_t at = no + (j - m);
+            nrun.deliver[at] = q.deliver[j];
+            nrun.src[at] = q.src[j];
+            nrun.seq[at] = q.seq[j];
+            nrun.tag[at] = (q.batch << 32) | q.pkt[j];
+        }
+        if (lane == 0) nrun_cur[h] = no;
     }
 }
 
-// the advance's totals (events popped, events kept, new head time) into one word triple, so the
-// host reads them with one copy
-__global__ void eq_totals(uint32_t n_hosts, const uint32_t* __restrict__ pop_off, const uint32_t* __restrict__ keep_off,
-                          const unsigned long long* __restrict__ next, uint64_t* __restrict__ out) {
+// the call's totals (popped, kept batch events, head time, left per source) from eqr_count's
+// per-block partials, into one word array the host reads with one copy
+__global__ __launch_bounds__(256) void eq_totals(uint32_t n_hosts, uint32_t n_part, const uint32_t* __restrict__ pop_off,
+                                                 const uint32_t* __restrict__ keep_off,
+                                                 const unsigned long long* __restrict__ part,
+                                                 unsigned long long* __restrict__ words) {
+    __shared__ unsigned long long s_v[4][kEqPart];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (uint32_t j = 0; j < kEqPart; ++j) {
+        unsigned long long v = j == 0 ? ~0ull : 0ull;
+        for (uint32_t b = threadIdx.x; b < n_part; b += 256) {
+            const unsigned long long x = part[(size_t)b * kEqPart + j];
+            v = j == 0 ? (x < v ? x : v) : v + x;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long x = __shfl_xor(v, o);
+            v = j == 0 ? (x < v ? x : v) : v + x;
+        }
+        if (lane == 0) s_v[w][j] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < kEqPart) {
+        const uint32_t j = threadIdx.x;
+        unsigned long long v = s_v[0][j];
+        for (int ww = 1; ww < 4; ++ww) v = j == 0 ? (s_v[ww][j] < v ? s_v[ww][j] : v) : v + s_v[ww][j];
+        if (j == 0) words[3] = v;
+        else words[3 + j] = v;   // words[4 + k] = left of source k
+    }
     if (threadIdx.x == 0) {
-        out[0] = pop_off[n_hosts];
-        out[1] = keep_off[n_hosts];
-        out[2] = *next;
+        words[1] = pop_off[n_hosts];
+        words[2] = keep_off ? keep_off[n_hosts] : 0u;
     }
 }
 
@@ -172,16 +302,92 @@ static shd_status eq_scan(EqState& Q, const uint32_t* in, uint32_t* out, uint32_
     return SHD_OK;
 }
 
-static shd_status eq_alloc(EqState& Q, int k, uint64_t n) {
-    // half again as much as asked when a buffer must grow: the pending set creeps up over the
-    // first rounds, and a reallocation (free + malloc) costs more than the merge
-    const size_t m = std::max<uint64_t>(n, 1) * 3 / 2 + 1;
-    if ((size_t)std::max<uint64_t>(n, 1) * 8 <= Q.deliver[k].bytes && (size_t)std::max<uint64_t>(n, 1) * 4 <= Q.src[k].bytes)
-        return SHD_OK;
-    SHD_TRY(Q.deliver[k].ensure(m * 8));
-    SHD_TRY(Q.src[k].ensure(m * 4));
-    SHD_TRY(Q.seq[k].ensure(m * 8));
-    SHD_TRY(Q.tag[k].ensure(m * 8));
+// a stored run's event arrays for n events (the ensure keeps growth headroom: slots are reused
+// round after round)
+static shd_status eq_run_alloc(EqRunBuf& r, uint32_t n_hosts, uint64_t n) {
+    const size_t m = std::max<uint64_t>(n, 1);
+    SHD_TRY(r.off.ensure((size_t)(n_hosts + 1) * 4));
+    SHD_TRY(r.deliver.ensure(m * 8));
+    SHD_TRY(r.src.ensure(m * 4));
+    SHD_TRY(r.seq.ensure(m * 8));
+    SHD_TRY(r.tag.ensure(m * 8));
+    return SHD_OK;
+}
+
+static EqOut eq_run_out(EqRunBuf& r) {
+    return EqOut{r.deliver.as<uint64_t>(), r.src.as<uint32_t>(), r.seq.as<uint64_t>(), r.tag.as<uint64_t>()};
+}
+
+constexpr int kEqPinWord = 48;   // ctx->h_pin words [48, 48 + kEqWords)
+
+// One pass: per-host cuts at window_end, scans, the merge of every source's popped prefix into
+// `out` at offsets out_off, and (nrun) the batch's remainder into a new run whose cursor goes to
+// nrun_cur.  Returns with the counts in ctx->h_pin + kEqPinWord.
+static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, uint32_t* out_off, EqOut out,
+                          EqRunBuf* nrun, uint32_t* nrun_cur, uint64_t n_in) {
+    EqState& Q = ctx->eq;
+    hipStream_t s = ctx->stream;
+    const uint32_t H = Q.n_hosts;
+    unsigned long long* words = Q.next.as<unsigned long long>();
+    unsigned long long* part = words + kEqWords;
+    const uint32_t nb = std::min<uint32_t>(kEqCountBlocks, div_up(((uint64_t)H + 1) * kEqLanes, 256));
+    eqr_count<<<nb, 256, 0, s>>>(H, S, window_end, Q.pop_cnt.as<uint32_t>(), Q.keep_cnt.as<uint32_t>(), part);
+    SHD_HIP(hipGetLastError());
+    SHD_TRY(eq_scan(Q, Q.pop_cnt.as<uint32_t>(), out_off, H + 1, s));
+    if (nrun) SHD_TRY(eq_scan(Q, Q.keep_cnt.as<uint32_t>(), nrun->off.as<uint32_t>(), H + 1, s));
+    const EqOut nr = nrun ? eq_run_out(*nrun) : EqOut{};
+    if (n_in)
+        eqr_merge<<<div_up(H, 4), 256, 0, s>>>(H, S, out_off, out, nr, nrun ? nrun->off.as<uint32_t>() : nullptr,
+                                               nrun_cur);
+    SHD_HIP(hipGetLastError());
+    eq_totals<<<1, 256, 0, s>>>(H, nb, out_off, nrun ? nrun->off.as<uint32_t>() : nullptr, part, words);
+    SHD_HIP(hipMemcpyAsync(ctx->h_pin + kEqPinWord, words, kEqWords * 8, hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    return SHD_OK;
+}
+
+static uint32_t* eq_cursor(EqState& Q, int buf, int slot) {
+    return Q.curs[buf].as<uint32_t>() + (size_t)slot * Q.n_hosts;
+}
+
+// the live runs as sources, from their cursors; cuts into the other cursor buffer
+static EqSrcs eq_sources(EqState& Q, int* slots) {
+    EqSrcs S{};
+    S.b = -1;
+    for (int r = 0; r <= kEqMaxRuns; ++r) {
+        EqRunBuf& R = Q.run[r];
+        if (!R.live) continue;
+        slots[S.n] = r;
+        S.s[S.n++] = EqSrc{R.off.as<uint32_t>(), eq_cursor(Q, Q.ccur, r), eq_cursor(Q, 1 - Q.ccur, r),
+                           R.deliver.as<uint64_t>(), R.src.as<uint32_t>(), R.seq.as<uint64_t>(),
+                           R.tag.as<uint64_t>(), nullptr, 0};
+    }
+    return S;
+}
+
+static int eq_free_slot(const EqState& Q) {
+    for (int r = 0; r <= kEqMaxRuns; ++r)
+        if (!Q.run[r].live) return r;
+    return -1;
+}
+
+// every pending event into one fresh run (cursor at its start); the old runs are dropped
+static shd_status eq_compact(shd_ctx* ctx) {
+    EqState& Q = ctx->eq;
+    int slots[kEqSrcMax];
+    EqSrcs S = eq_sources(Q, slots);
+    if (S.n == 0) return SHD_OK;
+    const int t = eq_free_slot(Q);
+    EqRunBuf& T = Q.run[t];
+    SHD_TRY(eq_run_alloc(T, Q.n_hosts, Q.n_pending));
+    SHD_TRY(eq_pass(ctx, S, ~0ull, T.off.as<uint32_t>(), eq_run_out(T), nullptr, nullptr, Q.n_pending));
+    if (ctx->h_pin[kEqPinWord + 1] != Q.n_pending) return SHD_ERR_INVALID;
+    SHD_HIP(hipMemcpyAsync(eq_cursor(Q, 1 - Q.ccur, t), T.off.p, (size_t)Q.n_hosts * 4, hipMemcpyDeviceToDevice,
+                           ctx->stream));
+    for (uint32_t k = 0; k < S.n; ++k) Q.run[slots[k]].live = false;
+    Q.ccur = 1 - Q.ccur;
+    T.live = Q.n_pending > 0;
+    T.n = T.left = Q.n_pending;
     return SHD_OK;
 }
 
@@ -195,17 +401,19 @@ shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_hosts) {
     if (!ctx || n_hosts == 0) return SHD_ERR_INVALID;
     SHD_HIP(hipSetDevice(ctx->device));
     EqState& Q = ctx->eq;
-    for (int k = 0; k < 2; ++k) {
-        SHD_TRY(Q.off[k].ensure((size_t)(n_hosts + 1) * 4));
-        SHD_TRY(eq_alloc(Q, k, 1));
+    for (int r = 0; r <= kEqMaxRuns; ++r) {
+        Q.run[r].live = false;
+        Q.run[r].n = Q.run[r].left = 0;
     }
+    for (int k = 0; k < 2; ++k) SHD_TRY(Q.curs[k].ensure((size_t)(kEqMaxRuns + 1) * n_hosts * 4));
+    SHD_TRY(Q.bcut.ensure((size_t)n_hosts * 4));
     SHD_TRY(Q.pop_cnt.ensure((size_t)(n_hosts + 1) * 4));
     SHD_TRY(Q.keep_cnt.ensure((size_t)(n_hosts + 1) * 4));
     SHD_TRY(Q.pop_off.ensure((size_t)(n_hosts + 1) * 4));
-    SHD_TRY(Q.next.ensure(32));   // [0] head time accumulator, [1..3] totals
-    SHD_HIP(hipMemsetAsync(Q.off[0].p, 0, (size_t)(n_hosts + 1) * 4, ctx->stream));
+    SHD_TRY(Q.next.ensure((kEqWords + (size_t)kEqCountBlocks * kEqPart) * 8));
+    SHD_HIP(hipMemsetAsync(Q.pop_off.p, 0, (size_t)(n_hosts + 1) * 4, ctx->stream));
     SHD_HIP(hipStreamSynchronize(ctx->stream));
-    Q.cur = 0;
+    Q.ccur = 0;
     Q.n_hosts = n_hosts;
     Q.n_pending = 0;
     Q.n_popped = 0;
@@ -225,58 +433,65 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
         return SHD_ERR_INVALID;
     if (has_b && Q.batches >= 0xFFFFFFFFull) return SHD_ERR_INVALID;   // tag bits exhausted
     SHD_HIP(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
     const uint32_t H = Q.n_hosts;
-    const int c = Q.cur, n = 1 - c;
-    const uint64_t n_in = Q.n_pending + (has_b ? d_batch->n_sent : 0);
+    const uint64_t n_b = has_b ? d_batch->n_sent : 0;
+    const uint64_t n_in = Q.n_pending + n_b;
     if (n_in >= 0xFFFFFFFFull) return SHD_ERR_INVALID;   // 32-bit positions
-    SHD_TRY(eq_alloc(Q, n, n_in));
-    const uint64_t n_cap = std::max<uint64_t>(n_in, 1) * 3 / 2 + 1;   // growth headroom, as eq_alloc
+    int live = 0;
+    for (int r = 0; r <= kEqMaxRuns; ++r) live += Q.run[r].live ? 1 : 0;
+    if (has_b && n_b && live >= kEqMaxRuns) SHD_TRY(eq_compact(ctx));   // room for the batch's run
+    // the popped events: at most everything (headroom: the pending set creeps up at first)
     if (Q.ps.bytes < std::max<uint64_t>(n_in, 1) * 4) {
-        SHD_TRY(Q.pd.ensure(n_cap * 8));
-        SHD_TRY(Q.ps.ensure(n_cap * 4));
-        SHD_TRY(Q.pq.ensure(n_cap * 8));
-        SHD_TRY(Q.pt.ensure(n_cap * 8));
+        const uint64_t cap = std::max<uint64_t>(n_in, 1) * 3 / 2 + 1;
+        SHD_TRY(Q.pd.ensure(cap * 8));
+        SHD_TRY(Q.ps.ensure(cap * 4));
+        SHD_TRY(Q.pq.ensure(cap * 8));
+        SHD_TRY(Q.pt.ensure(cap * 8));
     }
-    EqRuns P{Q.off[c].as<uint32_t>(), Q.deliver[c].as<uint64_t>(), Q.src[c].as<uint32_t>(),
-             Q.seq[c].as<uint64_t>(), Q.tag[c].as<uint64_t>(), nullptr};
-    EqRuns B{};
-    if (has_b)
-        B = EqRuns{d_batch->ev_off, d_batch->ev_deliver, d_batch->ev_src, d_batch->ev_seq, nullptr,
-                   d_batch->ev_pkt};
-    SHD_HIP(hipMemsetAsync(Q.next.p, 0xFF, 8, s));
-    eq_count<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(H, P, B, has_b, window_end, Q.pop_cnt.as<uint32_t>(),
-                                                          Q.keep_cnt.as<uint32_t>(),
-                                                          Q.next.as<unsigned long long>());
-    SHD_HIP(hipGetLastError());
-    SHD_TRY(eq_scan(Q, Q.pop_cnt.as<uint32_t>(), Q.pop_off.as<uint32_t>(), H + 1, s));
-    SHD_TRY(eq_scan(Q, Q.keep_cnt.as<uint32_t>(), Q.off[n].as<uint32_t>(), H + 1, s));
-    EqOut popped{Q.pd.as<uint64_t>(), Q.ps.as<uint32_t>(), Q.pq.as<uint64_t>(), Q.pt.as<uint64_t>()};
-    EqOut pending{Q.deliver[n].as<uint64_t>(), Q.src[n].as<uint32_t>(), Q.seq[n].as<uint64_t>(),
-                  Q.tag[n].as<uint64_t>()};
-    if (n_in)
-        eq_merge<<<div_up(H, 4), 256, 0, s>>>(H, P, B, has_b, Q.batches, Q.pop_off.as<uint32_t>(),
-                                              Q.off[n].as<uint32_t>(), popped, pending);
-    SHD_HIP(hipGetLastError());
-    // totals and the new head time: one pinned read-back
-    eq_totals<<<1, 64, 0, s>>>(H, Q.pop_off.as<uint32_t>(), Q.off[n].as<uint32_t>(),
-                               Q.next.as<unsigned long long>(), Q.next.as<uint64_t>() + 1);
-    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 32, Q.next.as<uint64_t>() + 1, 24, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    const uint32_t n_pop = (uint32_t)ctx->h_pin[32], n_keep = (uint32_t)ctx->h_pin[33];
-    if ((uint64_t)n_pop + n_keep != n_in) return SHD_ERR_INVALID;   // batch ev_off / n_sent disagree
-    Q.cur = n;
-    Q.n_pending = n_keep;
+    int slots[kEqSrcMax];
+    EqSrcs S = eq_sources(Q, slots);
+    const uint32_t n_runs = S.n;
+    EqRunBuf* nrun = nullptr;
+    int t = -1;
+    if (has_b) {
+        S.b = (int32_t)S.n;
+        S.s[S.n++] = EqSrc{d_batch->ev_off, nullptr, Q.bcut.as<uint32_t>(), d_batch->ev_deliver, d_batch->ev_src,
+                           d_batch->ev_seq, nullptr, d_batch->ev_pkt, Q.batches};
+        t = eq_free_slot(Q);
+        nrun = &Q.run[t];
+        SHD_TRY(eq_run_alloc(*nrun, H, n_b));
+    }
+    const EqOut popped{Q.pd.as<uint64_t>(), Q.ps.as<uint32_t>(), Q.pq.as<uint64_t>(), Q.pt.as<uint64_t>()};
+    SHD_TRY(eq_pass(ctx, S, window_end, Q.pop_off.as<uint32_t>(), popped, nrun,
+                    has_b ? eq_cursor(Q, 1 - Q.ccur, t) : nullptr, n_in));
+    const unsigned long long* wd = ctx->h_pin + kEqPinWord;
+    const uint64_t n_pop = wd[1], n_keep = wd[2];
+    uint64_t left = 0;
+    for (uint32_t k = 0; k < S.n; ++k) left += wd[4 + k];
+    if (n_pop + left != n_in || (has_b && wd[4 + S.b] != n_keep))
+        return SHD_ERR_INVALID;   // batch ev_off / n_sent disagree
+    // commit: cursors moved to the cut buffer; drained runs dropped; the batch's remainder is a run
+    for (uint32_t k = 0; k < n_runs; ++k) {
+        EqRunBuf& R = Q.run[slots[k]];
+        R.left = wd[4 + k];
+        R.live = R.left > 0;
+    }
+    if (has_b) {
+        nrun->n = nrun->left = n_keep;
+        nrun->live = n_keep > 0;
+        ++Q.batches;
+    }
+    Q.ccur = 1 - Q.ccur;
+    Q.n_pending = left;
     Q.n_popped = n_pop;
-    if (has_b) ++Q.batches;
     out->off = Q.pop_off.as<uint32_t>();
     out->deliver = Q.pd.as<uint64_t>();
     out->src = Q.ps.as<uint32_t>();
     out->seq = Q.pq.as<uint64_t>();
     out->tag = Q.pt.as<uint64_t>();
     out->n_popped = n_pop;
-    out->n_pending = n_keep;
-    out->next_time = ctx->h_pin[34];
+    out->n_pending = left;
+    out->next_time = wd[3];
     return SHD_OK;
 }
 
@@ -299,6 +514,8 @@ shd_status shd_equeue_copy_popped(shd_ctx* ctx, uint32_t* off, uint64_t* deliver
     return SHD_OK;
 }
 
+// The pending queues as one CSR: the runs are compacted into one first (the queues' content and
+// every later result are unchanged by a compaction).
 shd_status shd_equeue_pending(shd_ctx* ctx, uint32_t* off, uint64_t* deliver, uint32_t* src,
                               uint64_t* seq, uint64_t* tag, uint64_t* n_pending) {
     if (!ctx) return SHD_ERR_INVALID;
@@ -306,15 +523,23 @@ shd_status shd_equeue_pending(shd_ctx* ctx, uint32_t* off, uint64_t* deliver, ui
     if (!Q.ready) return SHD_ERR_STATE;
     SHD_HIP(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
-    const int c = Q.cur;
     const uint64_t n = Q.n_pending;
     if (n_pending) *n_pending = n;
-    if (off) SHD_HIP(hipMemcpyAsync(off, Q.off[c].p, (size_t)(Q.n_hosts + 1) * 4, hipMemcpyDeviceToHost, s));
-    if (n) {
-        if (deliver) SHD_HIP(hipMemcpyAsync(deliver, Q.deliver[c].p, n * 8, hipMemcpyDeviceToHost, s));
-        if (src) SHD_HIP(hipMemcpyAsync(src, Q.src[c].p, n * 4, hipMemcpyDeviceToHost, s));
-        if (seq) SHD_HIP(hipMemcpyAsync(seq, Q.seq[c].p, n * 8, hipMemcpyDeviceToHost, s));
-        if (tag) SHD_HIP(hipMemcpyAsync(tag, Q.tag[c].p, n * 8, hipMemcpyDeviceToHost, s));
+    if (!off && !(n && (deliver || src || seq || tag))) return SHD_OK;
+    SHD_TRY(eq_compact(ctx));
+    int live = -1;
+    for (int r = 0; r <= kEqMaxRuns; ++r)
+        if (Q.run[r].live) live = r;
+    if (off) {
+        if (live >= 0) SHD_HIP(hipMemcpyAsync(off, Q.run[live].off.p, (size_t)(Q.n_hosts + 1) * 4, hipMemcpyDeviceToHost, s));
+        else std::memset(off, 0, (size_t)(Q.n_hosts + 1) * 4);
+    }
+    if (n && live >= 0) {
+        const EqRunBuf& R = Q.run[live];
+        if (deliver) SHD_HIP(hipMemcpyAsync(deliver, R.deliver.p, n * 8, hipMemcpyDeviceToHost, s));
+        if (src) SHD_HIP(hipMemcpyAsync(src, R.src.p, n * 4, hipMemcpyDeviceToHost, s));
+        if (seq) SHD_HIP(hipMemcpyAsync(seq, R.seq.p, n * 8, hipMemcpyDeviceToHost, s));
+        if (tag) SHD_HIP(hipMemcpyAsync(tag, R.tag.p, n * 8, hipMemcpyDeviceToHost, s));
     }
     SHD_HIP(hipStreamSynchronize(s));
     return SHD_OK;
