@@ -84,3 +84,43 @@ def test_empty_queues_and_empty_batch(engine):
     assert p.events_for(1) == [(20, 1, 6, (2 << 32) | 5), (20, 1, 7, 1 << 32), (20, 4, 2, (1 << 32) | 1),
                                (25, 0, 1, (2 << 32) | 6), (30, 0, 9, (1 << 32) | 2)]
     assert p.n_pending == 1 and p.next_time == 40
+
+
+def test_run_compaction_and_pending_vs_oracle(engine):
+    """5 ms windows against 1-300 ms path latencies: no stored run drains for many rounds, so the
+    8-run limit compacts the runs (from round 9 on), and pending() -- a compaction itself --
+    returns every host's queue in EventQueue order, as the oracle's heaps hold it."""
+    from shadow_amd import synth
+    from shadow_amd.equeue import EventQueues
+    from shadow_amd.relay import Relay
+    H, P, NN = 500, 20_000, 60
+    el = synth.complete_graph(NN, 31)
+    used = np.arange(NN, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(NN, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    host_node = synth.c5_host_nodes(H, NN)
+    rng0 = synth.host_rng_states(H, 1)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    q = EventQueues(engine, H)
+    oq = OracleQueues(H)
+    orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+    start, win = 10**9, 5 * 10**6
+    for rnd in range(12):
+        b = synth.packet_batch(H, P, start, start + win, seed=90 + rnd)
+        r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, start + win, start + 10**12, 0)
+        o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, orng, onid,
+                             start + win, start + 10**12, 0)
+        ev = o["events"]
+        for d in range(H):
+            for k in range(int(ev["off"][d]), int(ev["off"][d + 1])):
+                oq.push(d, ev["deliver"][k], ev["src"][k], ev["seq"][k], (rnd << 32) | int(ev["pkt"][k]))
+        p = q.advance(r.ev_off, r.ev_deliver, r.ev_src, r.ev_seq, r.ev_pkt, window_end=start + 2 * win)
+        _check(p, oq, H, start + 2 * win)
+        if rnd in (3, 10):
+            off, d, s, sq, t = q.pending()
+            for h in range(H):
+                a, e = int(off[h]), int(off[h + 1])
+                got = list(zip(d[a:e].tolist(), s[a:e].tolist(), sq[a:e].tolist(), t[a:e].tolist()))
+                assert got == sorted(oq.q[h]), h
+        start += win
+    assert p.n_pending > 0
