@@ -609,7 +609,7 @@ __device__ unsigned long long g_stamp_prof[12];
 // status and the destination's low bits so bin_sort_v7 can filter and split them.
 constexpr uint32_t kBinShift = 5;
 constexpr uint32_t kBinDst = 1u << kBinShift;
-constexpr uint32_t kHistSplit = 8;   // histogram rows per stamp workgroup (relay_bin_hist)
+constexpr uint32_t kHistSplit = 2;   // histogram rows per stamp workgroup (relay_bin_hist)
 
 template <bool BIN>
 __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const uint64_t* __restrict__ draw,
@@ -1473,6 +1473,47 @@ __global__ __launch_bounds__(256) void relay_bin_hist(RelayArgs3 a, uint32_t G, 
     for (uint32_t i = tid; i < a.n_bins; i += 256) cnt[(size_t)blockIdx.x * a.n_bins + i] = s_cnt[i];
 }
 
+// relay_bin_hist, vector form (the batch's dst_host 16-byte aligned): the same rows, but four
+// threads per host of a group walk the host's own range in aligned 16-byte chunks (chunk c =
+// destinations [4c, 4c + 4), entries outside the host's range skipped), so no position needs a
+// search for its owner and each load brings four destinations.  Chunks reaching past the batch
+// end are read element by element.
+constexpr uint32_t kHist4Threads = 1024;   // four groups at a time: 4 threads x 64 host slots each
+
+__global__ __launch_bounds__(kHist4Threads) void relay_bin_hist4(RelayArgs3 a, uint32_t G, uint32_t n_pkt,
+                                                                 uint32_t* __restrict__ cnt) {
+    extern __shared__ uint32_t s_cnt[];
+    const uint32_t tid = threadIdx.x, hs = (tid >> 2) & 63, qq = tid & 3;
+    const uint32_t g = blockIdx.x / kHistSplit, k = blockIdx.x % kHistSplit;
+    for (uint32_t i = tid; i < a.n_bins; i += kHist4Threads) s_cnt[i] = 0;
+    __syncthreads();
+    const uint32_t n_groups = (a.n_src + a.gs - 1) / a.gs;
+    const uint32_t full = n_pkt & ~3u;   // chunks below this lie inside the batch
+    for (uint32_t grp = g + (k + (tid >> 8) * kHistSplit) * G; grp < n_groups; grp += 4 * kHistSplit * G) {
+        const uint32_t h0 = grp * a.gs, nh = min(a.gs, a.n_src - h0);
+        if (hs >= nh) continue;
+        const uint32_t h = a.order[h0 + hs];
+        const uint32_t b = a.src_off[h - a.src_lo], e = a.src_off[h - a.src_lo + 1];
+        for (uint32_t c = (b >> 2) + qq; 4 * c < e; c += 4) {
+            uint32_t d[4];
+            if (4 * c + 4 <= full) {
+                const uint4 v = reinterpret_cast<const uint4*>(a.dst_host)[c];
+                d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) d[u] = 4 * c + u < n_pkt ? a.dst_host[4 * c + u] : ~0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t i = 4 * c + u;
+                if (i >= b && i < e && d[u] < a.n_hosts) atomicAdd(&s_cnt[d[u] >> kBinShift], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < a.n_bins; i += kHist4Threads) cnt[(size_t)blockIdx.x * a.n_bins + i] = s_cnt[i];
+}
+
 // seg[g][b] = number of bin-b slots of stamp workgroups before g (the sum of kHistSplit
 // histogram rows per workgroup, exclusive prefix over g); tot[b] = all of bin b.  Lane = bin,
 // wave = a slice of workgroups; every row load of a slice is independent.  A workgroup count
@@ -1489,14 +1530,19 @@ __global__ __launch_bounds__(1024) void bin_col_scan(uint32_t G, uint32_t n_bins
     uint32_t c[kPer];
     uint32_t sum = 0;
     bool over = false;
+    // every row load unconditional (indices clamped, values masked) so all of them are in flight
+    // together instead of one guarded load at a time
+    const uint32_t bc = min(b, n_bins - 1);
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) {
-        const uint32_t g = g0 + i;
+        const uint32_t g = min(g0 + i, G - 1);
         c[i] = 0;
-        if (g < g1 && b < n_bins) {
 #pragma unroll
-            for (uint32_t k = 0; k < kHistSplit; ++k) c[i] += cnt[((size_t)g * kHistSplit + k) * n_bins + b];
-        }
+        for (uint32_t k = 0; k < kHistSplit; ++k) c[i] += cnt[((size_t)g * kHistSplit + k) * n_bins + bc];
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; ++i) {
+        if (!(g0 + i < g1 && b < n_bins)) c[i] = 0;
         over |= c[i] > 0xFFu;
         sum += c[i];
     }
@@ -1924,7 +1970,12 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     // to precede the scans.  The fork event is recorded first (the side stream must follow the
     // caller's work on the stream, e.g. the kernels that wrote the batch), the wait after.
     if (!b->chance) SHD_HIP(hipEventRecord(ctx->sev[0], s));
-    relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
+    const char* hv = std::getenv("SHD_HIST_SCALAR");   // tuning A/B: the flattened-position form
+    if (((uintptr_t)b->dst_host & 15) == 0 && n < (1ull << 31) && !(hv && *hv == '1'))
+        relay_bin_hist4<<<G * kHistSplit, kHist4Threads, (size_t)n_bins * 4, s>>>(a, G, (uint32_t)n,
+                                                                             R.bin_cnt.as<uint32_t>());
+    else
+        relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
     red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.bin_base.as<uint32_t>());
     if (!b->chance) {   // K0: the per-host generator streams, on the side stream next to the bins
         SHD_HIP(hipStreamWaitEvent(ctx->side, ctx->sev[0], 0));
