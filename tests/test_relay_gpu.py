@@ -314,3 +314,45 @@ def test_bin_pipeline_slot_counter_overflow_falls_back(engine):
         assert np.array_equal(getattr(r, "ev_" + k), o["events"][k]), k
     st, nid = rl.host_state()
     assert np.array_equal(st, orng) and np.array_equal(nid, onid)
+
+
+def test_device_batch_unaligned_inputs(engine):
+    """shd_relay_round_device with the batch arrays one element past a 16-byte boundary: the
+    histogram's vector form needs 16-byte aligned destinations, so its flattened-position form
+    runs; statuses and events bit-exact against the C oracle, on pipeline 7."""
+    import ctypes as C
+
+    import torch
+
+    from shadow_amd import _native as N
+    from shadow_amd.relay import Relay
+    H, NN = 3000, 40
+    lat, loss, host_node, rng0, b = _c5_like(H, NN, 200_000, 29)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    keep = []
+
+    def dev(a, np_dt, t_dt, pad=1):   # the array `pad` elements into a fresh device buffer
+        buf = torch.zeros(len(a) + pad, dtype=t_dt, device="cuda")
+        buf[pad:] = torch.from_numpy(np.ascontiguousarray(a, np_dt).view(t_dt == torch.int64 and np.int64 or np.int32)).cuda()
+        keep.append(buf)
+        return buf.data_ptr() + pad * buf.element_size()
+
+    n = b.n
+    batch = N.Batch(n, dev(b.src_off, np.uint32, torch.int32, 0), dev(b.send_time, np.uint64, torch.int64),
+                    dev(b.dst_host, np.uint32, torch.int32), dev(b.payload, np.uint32, torch.int32), None)
+    outs = [torch.empty(n, dtype=torch.uint8, device="cuda"), torch.empty(H + 1, dtype=torch.int32, device="cuda"),
+            torch.empty(n, dtype=torch.int64, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"),
+            torch.empty(n, dtype=torch.int64, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda")]
+    out = N.RelayOut(*(t.data_ptr() for t in outs), 0, 0, 0)
+    rd = N.Round(10**9 + 10**6, 10**12, 0)
+    N.check(engine.lib.shd_relay_round_device(engine.ctx, C.byref(batch), C.byref(rd), C.byref(out)), "round")
+    assert rl.last_pipeline() == 7
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(),
+                         np.zeros(H, np.uint64), 10**9 + 10**6, 10**12, 0)
+    ns = out.n_sent
+    assert ns == o["n_sent"]
+    assert np.array_equal(outs[0].cpu().numpy(), o["status"])
+    assert np.array_equal(outs[1].cpu().numpy().view(np.uint32), o["events"]["off"])
+    for t, k, dt in ((outs[2], "deliver", np.uint64), (outs[3], "src", np.uint32), (outs[4], "seq", np.uint64),
+                     (outs[5], "pkt", np.uint32)):
+        assert np.array_equal(t[:ns].cpu().numpy().view(dt), o["events"][k]), k
