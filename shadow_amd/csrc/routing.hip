@@ -1676,8 +1676,7 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
 static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t re,
                                   uint64_t* d_lat, float* d_loss, uint32_t delta, bool* ovf) {
     PreparedGraph& P = ctx->prep;
-    // 512 threads per slot (tuning: SHD_SSSP_BLOCK=1024 with the lane-group width 4)
-    const uint32_t BLOCK = env_u32("SHD_SSSP_BLOCK", 512) == 1024 ? 1024 : 512;
+    constexpr uint32_t BLOCK = 512;   // a 1024-thread single slot per CU: rows 0-4095 23.5 vs 19.1 ms
     const uint32_t W = (P.V + 31) / 32;
     // bitmap + control + per-wave queues (+ delta-stepping: one bucket byte per node, when it
     // fits beside the bitmap; else the sweeps read the active nodes' global labels)
@@ -1702,14 +1701,10 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     if (ctx->nh_out) SHD_TRY(ctx->g_pred.ensure((size_t)grid * P.V * 4));
     const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
     const uint32_t G = env_u32("SHD_SSSP_G", deg >= 64 ? 16 : deg >= 24 ? 8 : 4);
-    if (BLOCK == 1024) {
-        launch_global<1024, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl);
-    } else {
-        switch (G) {
-            case 16: launch_global<512, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
-            case 8: launch_global<512, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
-            default: launch_global<512, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
-        }
+    switch (G) {
+        case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
+        case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
+        default: launch_global<BLOCK, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
     }
     SHD_HIP(hipGetLastError());
     (void)ovf;   // the caller reads the overflow flag with read_flags()
