@@ -1813,7 +1813,8 @@ static shd_status prepare_reordered(shd_ctx* ctx, const HostGraph& H, const uint
     PreparedGraph& P = ctx->prep;
     P.reordered = false;
     const uint32_t V = P.V;
-    if (V == 0 || sssp_lds_bytes(V, 1024, false) <= ctx->max_lds || env_u32("SHD_SSSP_NO_REORDER", 0) == 1)
+    if (V == 0 || (sssp_lds_bytes(V, 1024, false) <= ctx->max_lds && env_u32("SHD_SSSP_REORDER", 0) != 1) ||
+        env_u32("SHD_SSSP_NO_REORDER", 0) == 1)
         return SHD_OK;   // the LDS kernels take this graph
     hipStream_t s = ctx->stream;
     std::vector<uint32_t> deg(V), roots(V), ord, pi(V, 0xFFFFFFFFu);
