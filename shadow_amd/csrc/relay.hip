@@ -53,6 +53,25 @@ struct Xoshiro {
     }
 };
 
+// chance >= reliability (worker.rs:365-370) from the draw's top 32 bits h = draw >> 32, which is
+// all K0 keeps (4 bytes per draw instead of 8).  chance = (draw >> 11) * 2^-53 exactly, so the
+// test is draw >> 11 >= T = ceil(reliability * 2^53) (exact: a power-of-two scale).  With
+// th = T >> 21 it is h >= th when T is a multiple of 2^21.  That always holds for a table loss
+// in [0, 1]: reliability = 1f32 - loss is >= 2^-9 (then reliability * 2^53 = m * 2^(e + 30),
+// e >= -9, a multiple of 2^21) or is 1 - loss for loss in [0.5, 1], a multiple of 2^-24 (T a
+// multiple of 2^29).  For any other value h > th decides unless h == th, where the low bits
+// would: `tie` is set and the round is redone on the 64-bit pipeline (its own exact draws).
+// reliability <= 0 always drops, NaN never (as the f64 comparison).
+__device__ __forceinline__ bool draw_drops(uint32_t h, double reliability, bool& tie) {
+    if (!(reliability > 0.0)) return reliability <= 0.0;
+    if (reliability >= 1.0) return false;   // chance < 1
+    const uint64_t T = (uint64_t)ceil(reliability * 9007199254740992.0);
+    const uint64_t th = T >> 21;
+    const bool low = (T & 0x1FFFFFull) != 0;
+    if (low && (uint64_t)h == th) tie = true;
+    return (uint64_t)h >= th + (low ? 1u : 0u);
+}
+
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     for (int o = 32; o > 0; o >>= 1) {
         const uint64_t w = __shfl_xor(v, o);
@@ -333,7 +352,7 @@ constexpr uint32_t kDrawSlice = 16;   // draws per host per LDS transpose (16: 4
 // draws iff now < sim_end (worker.rs:334-341); send times are non-decreasing within a host (a
 // host's sends happen in simulated-time order; the stamp checks it), so the drawing sends are a
 // prefix of the host's range, found from its last send (binary search when it is skipped).
-__global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint64_t* __restrict__ draw) {
+__global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint32_t* __restrict__ draw) {
     __shared__ uint64_t s[kDrawSlice][65];
     __shared__ uint32_t s_beg[64], s_nd[64];
     const uint32_t lane = threadIdx.x, hl = blockIdx.x * 64 + lane, h = a.src_lo + hl;
@@ -370,7 +389,7 @@ __global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint64_t* __rest
 #pragma unroll
         for (uint32_t g = 0; g < 64 * kDrawSlice / 64; ++g) {
             const uint32_t hl = g * (64 / kDrawSlice) + lane / kDrawSlice, k = lane % kDrawSlice;
-            if (j0 + k < s_nd[hl]) draw[s_beg[hl] + j0 + k] = s[k][hl];
+            if (j0 + k < s_nd[hl]) draw[s_beg[hl] + j0 + k] = (uint32_t)(s[k][hl] >> 32);   // see draw_drops
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -403,7 +422,7 @@ constexpr uint32_t kS5Per = 4;                  // sends per thread per chunk
 constexpr uint32_t kS5Cap = 256 * kS5Per;
 constexpr uint32_t kS5RowLds = 2048;            // staged path-table entries (16 KB)
 
-__global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint64_t* __restrict__ draw) {
+__global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint32_t* __restrict__ draw) {
     __shared__ uint2 s_rows[kS5RowLds];
     __shared__ uint16_t s_scan[kS5Cap + 1];
     __shared__ uint32_t s_host[kS5Hosts], s_beg[kS5Hosts], s_pre[kS5Hosts + 1], s_node[kS5Hosts];
@@ -486,9 +505,10 @@ __global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint64
                     const uint2 pp = staged ? s_rows[s_rowof[lo] * a.n_nodes + dn[i]]
                                             : path_global(a.path, (size_t)s_node[lo] * a.n_nodes + dn[i]);
                     const double reliability = (double)one_minus(__uint_as_float(pp.y));
-                    const double ch = a.chance ? a.chance[idx[i]]
-                                               : (double)(draw[idx[i]] >> 11) * (1.0 / 9007199254740992.0);
-                    if (!(now < a.bootstrap_end) && ch >= reliability && pay > 0) {
+                    bool tie = false;
+                    const bool ge = a.chance ? a.chance[idx[i]] >= reliability : draw_drops(draw[idx[i]], reliability, tie);
+                    wide |= tie;   // a draw whose low bits would decide: redo the round on pipeline 1
+                    if (!(now < a.bootstrap_end) && ge && pay > 0) {
                         st[i] = kStDropped;
                     } else {
                         uint64_t tt = now + pp.x;
@@ -612,7 +632,7 @@ constexpr uint32_t kBinDst = 1u << kBinShift;
 constexpr uint32_t kHistSplit = 2;   // histogram rows per stamp workgroup (relay_bin_hist)
 
 template <bool BIN>
-__global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const uint64_t* __restrict__ draw,
+__global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const uint32_t* __restrict__ draw,
                                                              const uint32_t* __restrict__ packed,
                                                              uint32_t n_words, uint32_t bits) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tbl[];   // packed host -> node
@@ -665,7 +685,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
             for (uint32_t p = pb + sub; p < pe; p += 16) s_own[p - cb] = (uint8_t)hh;
         }
     };
-    const uint64_t* __restrict__ rsrc = a.chance ? reinterpret_cast<const uint64_t*>(a.chance) : draw;
+    const uint64_t* __restrict__ chance64 = reinterpret_cast<const uint64_t*>(a.chance);
     for (uint32_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
         const uint32_t h0 = grp * a.gs;
         const uint32_t nh = min(a.gs, a.n_src - h0);
@@ -759,7 +779,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 prv[i] = a.send_time[idx[i] - (kk[i] > 0 ? 1u : 0u)];
                 dst[i] = a.dst_host[idx[i]];
                 pay[i] = a.payload[idx[i]];
-                rv[i] = rsrc[idx[i]];
+                rv[i] = a.chance ? chance64[idx[i]] : (uint64_t)draw[idx[i]];
             }
             SP_MARK(9);
             // (c) decisions
@@ -780,9 +800,11 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                         const uint2 pp = staged ? s_rows[s_rowof[hl[i]] * a.n_nodes + dn[i]]
                                                 : path_global(a.path, (size_t)s_node[hl[i]] * a.n_nodes + dn[i]);
                         const double reliability = (double)one_minus(__uint_as_float(pp.y));
-                        const double ch = a.chance ? __longlong_as_double((long long)rv[i])
-                                                   : (double)(rv[i] >> 11) * (1.0 / 9007199254740992.0);
-                        if (!(now[i] < a.bootstrap_end) && ch >= reliability && pay[i] > 0) {
+                        bool tie = false;
+                        const bool ge = a.chance ? __longlong_as_double((long long)rv[i]) >= reliability
+                                                 : draw_drops((uint32_t)rv[i], reliability, tie);
+                        wide |= tie;   // a draw whose low bits would decide: redo the round on pipeline 1
+                        if (!(now[i] < a.bootstrap_end) && ge && pay[i] > 0) {
                             st[i] = kStDropped;
                         } else {
                             uint64_t tt = now[i] + pp.x;
@@ -1426,6 +1448,7 @@ __global__ __launch_bounds__(256) void relay_bin_hist(RelayArgs3 a, uint32_t G, 
     extern __shared__ uint32_t s_cnt[];
     __shared__ uint32_t s_beg[kS5Hosts], s_pre[kS5Hosts + 1];
     const uint32_t tid = threadIdx.x, lane = tid & 63;
+    if (blockIdx.x == 0 && tid < 8) a.red[tid] = (tid <= 1 || tid == 3) ? ~0ull : 0ull;   // as red_init
     const uint32_t g = blockIdx.x / kHistSplit, k = blockIdx.x % kHistSplit;
     for (uint32_t i = tid; i < a.n_bins; i += 256) s_cnt[i] = 0;
     const uint32_t n_groups = (a.n_src + a.gs - 1) / a.gs;
@@ -1485,6 +1508,7 @@ __global__ __launch_bounds__(kHist4Threads) void relay_bin_hist4(RelayArgs3 a, u
     extern __shared__ uint32_t s_cnt[];
     const uint32_t tid = threadIdx.x, hs = (tid >> 2) & 63, qq = tid & 3;
     const uint32_t g = blockIdx.x / kHistSplit, k = blockIdx.x % kHistSplit;
+    if (blockIdx.x == 0 && tid < 8) a.red[tid] = (tid <= 1 || tid == 3) ? ~0ull : 0ull;   // as red_init
     for (uint32_t i = tid; i < a.n_bins; i += kHist4Threads) s_cnt[i] = 0;
     __syncthreads();
     const uint32_t n_groups = (a.n_src + a.gs - 1) / a.gs;
@@ -1871,20 +1895,20 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     SHD_TRY(R.ev_val.ensure(nn * 4));    // keys
     SHD_TRY(R.ev_key.ensure(nn * 4));    // keys (second buffer)
     SHD_TRY(R.ev_val2.ensure((size_t)(H + 2) * 4));
-    SHD_TRY(R.draws.ensure(nn * 8));
+    SHD_TRY(R.draws.ensure(nn * 4));
     red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.ev_val2.as<uint32_t>());
     RelayArgs3 a = relay_args3(ctx, b, rd, o);
     const uint64_t* seq_base = a.abs_seq ? nullptr : R.next_id.as<uint64_t>();
     if (!b->chance && R.n_src)   // K0: the per-host generator streams
-        relay_draws<<<div_up(R.n_src, 64), 64, 0, s>>>(a, R.draws.as<uint64_t>());
+        relay_draws<<<div_up(R.n_src, 64), 64, 0, s>>>(a, R.draws.as<uint32_t>());
     if (R.n_src == 0) {
     } else if (R.hn_bits) {   // host -> node map fits the LDS: persistent stamp, no node gathers
         const uint32_t groups = div_up(R.n_src, kS5Hosts);
         relay_stamp_v6<false><<<std::min<uint32_t>(groups, (uint32_t)ctx->n_cu), kS6Threads,
-                         (size_t)R.hn_words * 4, s>>>(a, R.draws.as<uint64_t>(),
+                         (size_t)R.hn_words * 4, s>>>(a, R.draws.as<uint32_t>(),
                                                       R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     } else {
-        relay_stamp_v5<<<div_up(R.n_src, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint64_t>());
+        relay_stamp_v5<<<div_up(R.n_src, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint32_t>());
     }
     SHD_HIP(hipGetLastError());
     // stable LSD radix sort of the records by destination (keys <= H)
@@ -1954,7 +1978,7 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     const uint32_t n_bins = div_up(H, kBinDst);
     const uint32_t G = std::min<uint32_t>(div_up(R.n_src, kS5Hosts), (uint32_t)ctx->n_cu);
     SHD_TRY(R.rec.ensure(nn * 16));
-    SHD_TRY(R.draws.ensure(nn * 8));
+    SHD_TRY(R.draws.ensure(nn * 4));
     SHD_TRY(R.bin_cnt.ensure((size_t)G * (kHistSplit + 1) * n_bins * 4));
     SHD_TRY(R.bin_base.ensure((size_t)(2 * n_bins + 1) * 4));
     SHD_TRY(R.bin_lb.ensure((size_t)(n_bins + 1) * 8));
@@ -1965,28 +1989,29 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.n_bins = n_bins;
     uint32_t* seg = R.bin_cnt.as<uint32_t>() + (size_t)G * kHistSplit * n_bins;
     a.seg_pre = seg;
-    // the histogram goes first: a round starts on an idle GPU, and the host calls that set up
-    // the side stream (~20 us of them) then run while it does; the reductions' reset only has
-    // to precede the scans.  The fork event is recorded first (the side stream must follow the
-    // caller's work on the stream, e.g. the kernels that wrote the batch), the wait after.
-    if (!b->chance) SHD_HIP(hipEventRecord(ctx->sev[0], s));
+    // K0 goes first: with the draws kept as 4 bytes and the histogram at 30 us, K0 plus the
+    // stream join (~12 us from its end to the stamp's start) was the longer of the two chains, so
+    // its fork is issued before anything else.  The fork event follows the caller's work on the
+    // stream (e.g. the kernels that wrote the batch).
+    if (!b->chance) {   // K0: the per-host generator streams, on the side stream next to the bins
+        SHD_HIP(hipEventRecord(ctx->sev[0], s));
+        SHD_HIP(hipStreamWaitEvent(ctx->side, ctx->sev[0], 0));
+        relay_draws<<<div_up(R.n_src, 64), 64, 0, ctx->side>>>(a, R.draws.as<uint32_t>());
+    }
+    // the histogram's first block also resets the round's reductions (red_init's job: one
+    // launch less; only the scans and the stamp read them, all after the histogram)
     const char* hv = std::getenv("SHD_HIST_SCALAR");   // tuning A/B: the flattened-position form
     if (((uintptr_t)b->dst_host & 15) == 0 && n < (1ull << 31) && !(hv && *hv == '1'))
         relay_bin_hist4<<<G * kHistSplit, kHist4Threads, (size_t)n_bins * 4, s>>>(a, G, (uint32_t)n,
                                                                              R.bin_cnt.as<uint32_t>());
     else
         relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
-    red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.bin_base.as<uint32_t>());
-    if (!b->chance) {   // K0: the per-host generator streams, on the side stream next to the bins
-        SHD_HIP(hipStreamWaitEvent(ctx->side, ctx->sev[0], 0));
-        relay_draws<<<div_up(R.n_src, 64), 64, 0, ctx->side>>>(a, R.draws.as<uint64_t>());
-        SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));
-    }
+    if (!b->chance) SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));   // after the histogram's launch
     bin_col_scan<<<div_up(n_bins, 64), 1024, 0, s>>>(G, n_bins, R.bin_cnt.as<uint32_t>(), seg, tot, a.red);
     bin_base_scan<<<1, 1024, 0, s>>>(n_bins, tot, R.bin_base.as<uint32_t>(), R.bin_lb.as<unsigned long long>(), a.red);
     if (!b->chance) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
     relay_stamp_v6<true><<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4, s>>>(
-        a, R.draws.as<uint64_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
+        a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     V7Out vo{o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt,
              a.abs_seq ? nullptr : R.next_id.as<uint64_t>(), rd->round_end};
     const char* stop = std::getenv("SHD_B7_STOP");   // tuning only: partial K4 (wrong output)

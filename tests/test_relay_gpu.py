@@ -356,3 +356,49 @@ def test_device_batch_unaligned_inputs(engine):
     for t, k, dt in ((outs[2], "deliver", np.uint64), (outs[3], "src", np.uint32), (outs[4], "seq", np.uint64),
                      (outs[5], "pkt", np.uint32)):
         assert np.array_equal(t[:ns].cpu().numpy().view(dt), o["events"][k]), k
+
+
+@pytest.mark.parametrize("loss01", [0.999, 0.3, 0.001])
+@pytest.mark.parametrize("above", [False, True])
+def test_draw_top_bits_at_the_drop_threshold(engine, loss01, above):
+    """K0 keeps a draw's top 32 bits only.  The drop test chance >= reliability is
+    draw >> 11 >= T = ceil(reliability * 2^53), and for reliability = 1f32 - loss with a loss in
+    [0, 1] T is a multiple of 2^21, so the top bits decide it exactly (relay.hip draw_drops).
+    Host 0's first draw is crafted (Xoshiro256++ output solved for s3) to sit just below or at
+    the threshold; the statuses match the oracle's f64 comparison on pipeline 7."""
+    from fractions import Fraction
+    import math
+
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    M = 2**64 - 1
+    lf = np.float32(loss01)
+    q = np.float32(1.0) - lf                         # reliability as Rust computes it (f32)
+    T = math.ceil(Fraction(float(q)) * 2**53)       # chance >= reliability  <=>  draw >> 11 >= T
+    assert T % 2**21 == 0
+    X64 = (T if above else T - 1) << 11
+    s0, s1, s2 = 0x0123456789ABCDEF, 0x0FEDCBA987654321, 0x13579BDF2468ACE0
+    r = (X64 - s0) & M
+    s3 = ((((r >> 23) | (r << 41)) & M) - s0) & M   # rotl(s0 + s3, 23) + s0 == X64
+    H = 4
+    rng0 = synth.host_rng_states(H, 1)
+    rng0[0] = np.array([s0, s1, s2, s3], np.uint64)
+    host_node = np.array([0, 1, 0, 1], np.uint32)
+    lat = np.array([[1000, 5000], [5000, 1000]], np.uint64)
+    loss = np.array([[0, lf], [lf, 0]], np.float32)
+    src_off = np.array([0, 3, 3, 3, 3], np.uint32)   # host 0 sends three packets to host 1
+    t = np.array([10**9, 10**9 + 10, 10**9 + 20], np.uint64)
+    dst = np.array([1, 1, 1], np.uint32)
+    pay = np.array([1448, 1448, 1448], np.uint32)
+    rd = (10**9 + 10**6, 10**12, 0)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    res = rl.round(src_off, t, dst, pay, *rd)
+    orng = rng0.copy()
+    o = corc.relay_round(src_off, t, dst, pay, host_node, lat, loss, orng, np.zeros(H, np.uint64), *rd)
+    assert rl.last_pipeline() == 7
+    assert res.status.tolist() == o["status"].tolist()
+    assert res.status[0] == (1 if above else 2)      # dropped at the threshold, sent just below it
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(res, "ev_" + k), o["events"][k]), k
+    st, _ = rl.host_state()
+    assert np.array_equal(st, orng)
