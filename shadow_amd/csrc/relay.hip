@@ -1693,6 +1693,43 @@ __device__ __forceinline__ void v7_sort_run(uint32_t n, uint32_t lane, const uin
     }
     lo = wave_min_u32(lo, lane);
     pmin = wave_min_u32(pmin, lane);
+    {   // 32-bit keys (deliver - lo) << 8 | e when the run's deliver times span < 2^24 ns: half the
+        // lane exchanges and compares of the 64-bit network.  Equal deliver times would need the
+        // packet order: a run with any is redone on the 64-bit keys below.
+        uint32_t hi = 0;
+#pragma unroll
+        for (int c = 0; c < NPL; ++c)
+            if (lane + 64u * c < n) hi = max(hi, v[c].x);
+        hi = wave_max_u32(hi, lane);
+        if (hi - lo < (1u << 24)) {
+            uint32_t k32[NPL];
+#pragma unroll
+            for (int c = 0; c < NPL; ++c) {
+                const uint32_t e = lane + 64u * c;
+                k32[c] = e < n ? ((v[c].x - lo) << 8) | e : ~0u;
+            }
+            wave_bitonic32<NPL>(k32, lane);
+            // sorted: element r = lane + 64 c; a tie is an equal upper 24 bits in neighbours r, r + 1
+            bool tie = false;
+#pragma unroll
+            for (int c = 0; c < NPL; ++c) {
+                // (both shuffles with every lane active: a read of an inactive lane returns 0)
+                const uint32_t down = (uint32_t)__shfl_down((int)k32[c], 1);
+                const uint32_t first = c + 1 < NPL ? (uint32_t)__shfl((int)k32[c + 1 < NPL ? c + 1 : c], 0) : ~0u;
+                const uint32_t nx = lane == 63 ? first : down;
+                const uint32_t r = lane + 64u * c;
+                if (r + 1 < n && (nx >> 8) == (k32[c] >> 8)) tie = true;
+            }
+            if (__ballot(tie) == 0) {
+#pragma unroll
+                for (int c = 0; c < NPL; ++c) {
+                    const uint32_t rank = lane + 64u * c;
+                    if (rank < n) pm[rank] = ls[k32[c] & 0xFFu];
+                }
+                return;
+            }
+        }
+    }
     uint64_t k[NPL];
 #pragma unroll
     for (int c = 0; c < NPL; ++c) {

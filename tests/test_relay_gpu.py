@@ -402,3 +402,28 @@ def test_draw_top_bits_at_the_drop_threshold(engine, loss01, above):
         assert np.array_equal(getattr(res, "ev_" + k), o["events"][k]), k
     st, _ = rl.host_state()
     assert np.array_equal(st, orng)
+
+
+def test_clamped_deliver_times_tie_everywhere(engine):
+    """Path latencies far below the round's span: almost every event's deliver time clamps to
+    round_end (worker.rs:398-401), so each destination run is one big tie that the EventQueue
+    order breaks by (src host, event id).  The per-destination sorts' 32-bit fast path must see
+    the ties and fall back to the packet order; bit-exact against the C oracle."""
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    H, NN, P = 2000, 30, 200_000
+    lat = np.full((NN, NN), 1000, np.uint64)          # 1 us everywhere
+    loss = np.zeros((NN, NN), np.float32)
+    host_node = synth.c5_host_nodes(H, NN)
+    rng0 = synth.host_rng_states(H, 1)
+    b = synth.packet_batch(H, P, 10**9, 10**9 + 10**6, seed=41)
+    rd = (10**9 + 10**6, 10**12, 0)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, *rd)
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(),
+                         np.zeros(H, np.uint64), *rd)
+    assert rl.last_pipeline() == 7
+    assert (r.ev_deliver == 10**9 + 10**6).mean() > 0.99
+    assert np.array_equal(r.status, o["status"]) and np.array_equal(r.ev_off, o["events"]["off"])
+    for k in ("deliver", "src", "seq", "pkt"):
+        assert np.array_equal(getattr(r, "ev_" + k), o["events"][k]), k
