@@ -62,6 +62,7 @@ struct EqState {   // destination event queues (equeue.hip): a list of sorted ru
     DevBuf bcut;                    // [n_hosts] the batch's first kept event per host
     DevBuf pd, ps, pq, pt;          // the last call's popped events
     DevBuf pop_cnt, keep_cnt, pop_off, next, left, scan_tmp;
+    DevBuf ranges;                  // [n_hosts][kEqMaxRuns + 1] (cursor, cut) pairs of the last count
     int ccur = 0;
     uint32_t n_hosts = 0;
     uint64_t n_pending = 0, n_popped = 0, batches = 0;

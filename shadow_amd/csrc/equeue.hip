@@ -64,6 +64,19 @@ __device__ __forceinline__ uint32_t lower_bound_time(const uint64_t* t, uint32_t
     return b;
 }
 
+// lower_bound from the front: a run's popped prefix is short (C5: ~10 events per host and run),
+// so probing b, b+1, b+3, b+7, ... finds the cut within a line or two of the cursor, where a
+// plain bisection of the whole run touches a line per step
+__device__ __forceinline__ uint32_t lower_bound_gallop(const uint64_t* t, uint32_t b, uint32_t e, uint64_t x) {
+    if (b >= e || !(t[b] < x)) return b;
+    uint32_t prev = b, step = 1;   // t[prev] < x
+    while (step < e - prev && t[prev + step] < x) {
+        prev += step;
+        step <<= 1;
+    }
+    return lower_bound_time(t, prev + 1, min(e, prev + step), x);
+}
+
 // Q.next layout (one read-back per call): [0] unused, [1] popped, [2] kept batch events, [3] head
 // time, [4 + k] events of source k left after the pop; then eqr_count's per-block partials
 constexpr uint32_t kEqWords = 4 + kEqSrcMax;
@@ -79,7 +92,7 @@ constexpr uint32_t kEqPart = 1 + kEqSrcMax;  // partial words per block: head ti
 
 __global__ __launch_bounds__(256) void eqr_count(uint32_t n_hosts, EqSrcs S, uint64_t window_end,
                                                  uint32_t* __restrict__ pop, uint32_t* __restrict__ keep,
-                                                 unsigned long long* __restrict__ part) {
+                                                 unsigned long long* __restrict__ part, uint2* __restrict__ ranges) {
     __shared__ unsigned long long s_w[4][kEqPart];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t total = ((uint64_t)n_hosts + 1) * kEqLanes;
@@ -92,8 +105,9 @@ __global__ __launch_bounds__(256) void eqr_count(uint32_t n_hosts, EqSrcs S, uin
         if (h < n_hosts && k < S.n) {
             const EqSrc& q = S.s[k];
             const uint32_t lo = q.lo ? q.lo[h] : q.off[h], hi = q.off[h + 1];
-            const uint32_t m = lower_bound_time(q.deliver, lo, hi, window_end);
+            const uint32_t m = lower_bound_gallop(q.deliver, lo, hi, window_end);
             q.cut[h] = m;
+            ranges[(size_t)h * kEqSrcMax + k] = make_uint2(lo, m);   // eqr_merge: one line per host
             np = m - lo;
             rem = hi - m;
             if (m < hi) head = q.deliver[m] < head ? q.deliver[m] : head;
@@ -137,13 +151,13 @@ struct EqOut {
 // prefix.  When the host's popped events fit kEqStage, the prefixes are staged in LDS (whole
 // events, source after source, coalesced loads), every lane then takes one staged event and
 // binary-searches the other prefixes in LDS; larger hosts search global memory source by
-// source.  Then the batch's remainder [cut, end) is copied to the new run (nrun), whose cursor
-// starts at its offset.
-constexpr uint32_t kEqStage = 256;
+// source.  Then the batch's remainder [cut, end) is copied to the new run (in the same wave: a
+// separate streaming kernel, alone or beside the merge on the side stream, measured slower).
+constexpr uint32_t kEqStage = 160;   // 17.5 KB per 4-wave workgroup: 8 workgroups (32 waves) per CU
 
 __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, const uint32_t* __restrict__ pop_off,
                                                  EqOut popped, EqOut nrun, const uint32_t* __restrict__ nrun_off,
-                                                 uint32_t* __restrict__ nrun_cur) {
+                                                 uint32_t* __restrict__ nrun_cur, const uint2* __restrict__ ranges) {
     __shared__ uint64_t s_t[4][kEqStage], s_q[4][kEqStage], s_g[4][kEqStage];
     __shared__ uint32_t s_s[4][kEqStage];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -151,13 +165,10 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
     if (h >= n_hosts) return;   // wave-uniform; the kernel has no workgroup barrier
     // lane k < S.n holds source k's popped range and its place in the LDS stage
     uint32_t my_lo = 0, my_m = 0;
-    for (uint32_t k = 0; k < S.n; ++k) {
-        const EqSrc& q = S.s[k];
-        const uint32_t lo = q.lo ? q.lo[h] : q.off[h], m = q.cut[h];
-        if (lane == k) {
-            my_lo = lo;
-            my_m = m;
-        }
+    if (lane < S.n) {   // eqr_count's (cursor, cut) pairs of this host: one line
+        const uint2 r = ranges[(size_t)h * kEqSrcMax + lane];
+        my_lo = r.x;
+        my_m = r.y;
     }
     const uint32_t cnt = my_m - my_lo;
     uint32_t incl = cnt;
@@ -246,7 +257,7 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
             }
         }
     }
-    if (S.b >= 0) {   // the batch's remainder becomes the new run
+    if (S.b >= 0) {   // the batch's remainder becomes the new run, whose cursor starts at its offset
         const EqSrc& q = S.s[S.b];
         const uint32_t m = q.cut[h], e = q.off[h + 1], no = nrun_off[h];
         for (uint32_t j = m + lane; j < e; j += 64) {
@@ -331,14 +342,16 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
     unsigned long long* words = Q.next.as<unsigned long long>();
     unsigned long long* part = words + kEqWords;
     const uint32_t nb = std::min<uint32_t>(kEqCountBlocks, div_up(((uint64_t)H + 1) * kEqLanes, 256));
-    eqr_count<<<nb, 256, 0, s>>>(H, S, window_end, Q.pop_cnt.as<uint32_t>(), Q.keep_cnt.as<uint32_t>(), part);
+    SHD_TRY(Q.ranges.ensure((size_t)H * kEqSrcMax * 8));
+    eqr_count<<<nb, 256, 0, s>>>(H, S, window_end, Q.pop_cnt.as<uint32_t>(), Q.keep_cnt.as<uint32_t>(), part,
+                                 Q.ranges.as<uint2>());
     SHD_HIP(hipGetLastError());
     SHD_TRY(eq_scan(Q, Q.pop_cnt.as<uint32_t>(), out_off, H + 1, s));
     if (nrun) SHD_TRY(eq_scan(Q, Q.keep_cnt.as<uint32_t>(), nrun->off.as<uint32_t>(), H + 1, s));
     const EqOut nr = nrun ? eq_run_out(*nrun) : EqOut{};
     if (n_in)
         eqr_merge<<<div_up(H, 4), 256, 0, s>>>(H, S, out_off, out, nr, nrun ? nrun->off.as<uint32_t>() : nullptr,
-                                               nrun_cur);
+                                               nrun_cur, Q.ranges.as<uint2>());
     SHD_HIP(hipGetLastError());
     eq_totals<<<1, 256, 0, s>>>(H, nb, out_off, nrun ? nrun->off.as<uint32_t>() : nullptr, part, words);
     SHD_HIP(hipMemcpyAsync(ctx->h_pin + kEqPinWord, words, kEqWords * 8, hipMemcpyDeviceToHost, s));
