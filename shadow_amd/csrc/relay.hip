@@ -344,7 +344,10 @@ struct RelayArgs3 {
     uint32_t gs;         // hosts per group of relay_stamp_v6 / relay_bin_hist (<= kS5Hosts)
 };
 
-constexpr uint32_t kDrawSlice = 16;   // draws per host per LDS transpose (16: 43 us vs 47 at 8 on C5)
+#ifndef SHD_DRAW_SLICE
+#define SHD_DRAW_SLICE 16
+#endif
+constexpr uint32_t kDrawSlice = SHD_DRAW_SLICE;   // draws per host per LDS transpose (16: 43 us vs 47 at 8 on C5)
 
 // K0 relay_draws: the only sequential part of the relay -- every source host's Xoshiro256++
 // stream (host.rs:218, worker.rs:365) -- as its own kernel: one lane per host (64 consecutive
@@ -353,7 +356,7 @@ constexpr uint32_t kDrawSlice = 16;   // draws per host per LDS transpose (16: 4
 // host's sends happen in simulated-time order; the stamp checks it), so the drawing sends are a
 // prefix of the host's range, found from its last send (binary search when it is skipped).
 __global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint32_t* __restrict__ draw) {
-    __shared__ uint64_t s[kDrawSlice][65];
+    __shared__ uint32_t s[kDrawSlice][65];   // the draws' top 32 bits (draw_drops)
     __shared__ uint32_t s_beg[64], s_nd[64];
     const uint32_t lane = threadIdx.x, hl = blockIdx.x * 64 + lane, h = a.src_lo + hl;
     uint32_t nd = 0;
@@ -381,15 +384,15 @@ __global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint32_t* __rest
     for (uint32_t j0 = 0; j0 < mx; j0 += kDrawSlice) {
 #pragma unroll
         for (uint32_t k = 0; k < kDrawSlice; ++k)
-            if (j0 + k < nd) s[k][lane] = r.next();
+            if (j0 + k < nd) s[k][lane] = (uint32_t)(r.next() >> 32);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // 8 lanes per host write its kDrawSlice consecutive draws (64 contiguous bytes)
+        // kDrawSlice lanes per host write its kDrawSlice consecutive draws (4 B each)
 #pragma unroll
         for (uint32_t g = 0; g < 64 * kDrawSlice / 64; ++g) {
             const uint32_t hl = g * (64 / kDrawSlice) + lane / kDrawSlice, k = lane % kDrawSlice;
-            if (j0 + k < s_nd[hl]) draw[s_beg[hl] + j0 + k] = (uint32_t)(s[k][hl] >> 32);   // see draw_drops
+            if (j0 + k < s_nd[hl]) draw[s_beg[hl] + j0 + k] = s[k][hl];
         }
         __builtin_amdgcn_wave_barrier();
     }

@@ -8,10 +8,11 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method threa
   tests/test_advice_gpu.py tests/test_configs_gpu.py > gpurun_out/relay_tests.log 2>&1 || { tail -40 gpurun_out/relay_tests.log; exit 1; }
 tail -3 gpurun_out/relay_tests.log
 for v in ${VARIANTS:-DEFAULT=1}; do
+  n=$(echo "$v" | tr '/' '_')
   env "$v" timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv \
-    -d "gpurun_out/relay_cmp_$v" -o run -- python3 tools/relay_only.py 10 > "gpurun_out/relay_cmp_$v.log" 2>&1 || exit 3
-  echo "$v $(tail -1 "gpurun_out/relay_cmp_$v.log")"
-  python3 tools/kstats.py "gpurun_out/relay_cmp_$v"
+    -d "gpurun_out/relay_cmp_$n" -o run -- python3 tools/relay_only.py 10 > "gpurun_out/relay_cmp_$n.log" 2>&1 || exit 3
+  echo "$v $(tail -1 "gpurun_out/relay_cmp_$n.log")"
+  python3 tools/kstats.py "gpurun_out/relay_cmp_$n"
 done
 # bin_sort_v7 phase pricing (SHD_B7_STOP=k returns after phase k: output wrong, timing only)
 if [ -n "$B7_STOPS" ]; then
