@@ -1321,7 +1321,14 @@ __global__ void max_u64_kernel(const uint64_t* __restrict__ d, uint64_t n,
         const uint64_t w = __shfl_xor(m, o);
         m = w > m ? w : m;
     }
-    if ((threadIdx.x & 63) == 0) atomicMax(out, (unsigned long long)m);
+    // one atomic per workgroup: 4 waves per block on one address contend (97 us for 8 MB)
+    __shared__ uint64_t part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) m = part[w] > m ? part[w] : m;
+        atomicMax(out, (unsigned long long)m);
+    }
 }
 
 __global__ void min_u64_kernel(const uint64_t* __restrict__ d, uint64_t n,
@@ -1330,13 +1337,19 @@ __global__ void min_u64_kernel(const uint64_t* __restrict__ d, uint64_t n,
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
         m = d[i] < m ? d[i] : m;
     m = wave_min_u64(m);
-    if ((threadIdx.x & 63) == 0) atomicMin(out, (unsigned long long)m);
+    __shared__ uint64_t part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) m = part[w] < m ? part[w] : m;
+        atomicMin(out, (unsigned long long)m);
+    }
 }
 
 shd_status min_u64_device(shd_ctx* ctx, const uint64_t* d, uint64_t n, uint64_t* out) {
     SHD_TRY(ctx->g_aux.ensure(8));
     SHD_HIP(hipMemsetAsync(ctx->g_aux.p, 0xFF, 8, ctx->stream));
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(2048, (n + 255) / 256);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(1024, (n + 255) / 256);
     min_u64_kernel<<<grid ? grid : 1, 256, 0, ctx->stream>>>(
         d, n, reinterpret_cast<unsigned long long*>(ctx->g_aux.p));
     SHD_HIP(hipMemcpyAsync(out, ctx->g_aux.p, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -2426,7 +2439,7 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
         SHD_TRY(ctx->g_aux.ensure(8));
         SHD_HIP(hipMemsetAsync(ctx->g_aux.p, 0, 8, s));
         const uint64_t nn = (uint64_t)n_nodes * n_nodes;
-        max_u64_kernel<<<(uint32_t)std::min<uint64_t>(2048, (nn + 255) / 256), 256, 0, s>>>(
+        max_u64_kernel<<<(uint32_t)std::min<uint64_t>(1024, (nn + 255) / 256), 256, 0, s>>>(
             tl, nn, reinterpret_cast<unsigned long long*>(ctx->g_aux.p));
         uint64_t mx = 0;
         SHD_HIP(hipMemcpyAsync(&mx, ctx->g_aux.p, 8, hipMemcpyDeviceToHost, s));
