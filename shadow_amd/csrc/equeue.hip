@@ -20,6 +20,7 @@
 // kEqMaxRuns runs are alive, they are first compacted into one (the same merge, every event).
 // Traffic per advance ~ the batch (read + its remainder written) + the popped events (read +
 // written), instead of every pending event read and written each round.
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 
@@ -87,7 +88,9 @@ constexpr uint32_t kEqWords = 4 + kEqSrcMax;
 constexpr uint32_t kEqLanes = 16;
 static_assert(kEqSrcMax <= kEqLanes, "a lane per source");
 
-constexpr uint32_t kEqCountBlocks = 1024;   // eqr_count's grid: per-block partials, no hot atomics
+constexpr uint32_t kEqCountBlocks = 2048;   // eqr_count's grid: per-block partials, no hot atomics
+                                            // (full occupancy for its latency-bound searches: 1024 blocks 64 us, 2048 55)
+constexpr uint32_t kEqCountBlocksMax = 4096;   // partials room (SHD_EQ_COUNT_BLOCKS: tuning)
 constexpr uint32_t kEqPart = 1 + kEqSrcMax;  // partial words per block: head time, left per source
 
 __global__ __launch_bounds__(256) void eqr_count(uint32_t n_hosts, EqSrcs S, uint64_t window_end,
@@ -273,31 +276,38 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
 
 // the call's totals (popped, kept batch events, head time, left per source) from eqr_count's
 // per-block partials, into one word array the host reads with one copy
-__global__ __launch_bounds__(256) void eq_totals(uint32_t n_hosts, uint32_t n_part, const uint32_t* __restrict__ pop_off,
-                                                 const uint32_t* __restrict__ keep_off,
-                                                 const unsigned long long* __restrict__ part,
-                                                 unsigned long long* __restrict__ words) {
-    __shared__ unsigned long long s_v[4][kEqPart];
+__global__ __launch_bounds__(1024) void eq_totals(uint32_t n_hosts, uint32_t n_part, const uint32_t* __restrict__ pop_off,
+                                                  const uint32_t* __restrict__ keep_off,
+                                                  const unsigned long long* __restrict__ part,
+                                                  unsigned long long* __restrict__ words) {
+    __shared__ unsigned long long s_v[16][kEqPart];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (uint32_t j = 0; j < kEqPart; ++j) {
-        unsigned long long v = j == 0 ? ~0ull : 0ull;
-        for (uint32_t b = threadIdx.x; b < n_part; b += 256) {
+    // a thread takes whole partial records (independent loads), then one reduction per word
+    unsigned long long v[kEqPart];
+#pragma unroll
+    for (uint32_t j = 0; j < kEqPart; ++j) v[j] = j == 0 ? ~0ull : 0ull;
+    for (uint32_t b = threadIdx.x; b < n_part; b += 1024) {
+#pragma unroll
+        for (uint32_t j = 0; j < kEqPart; ++j) {
             const unsigned long long x = part[(size_t)b * kEqPart + j];
-            v = j == 0 ? (x < v ? x : v) : v + x;
+            v[j] = j == 0 ? (x < v[j] ? x : v[j]) : v[j] + x;
         }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kEqPart; ++j) {
         for (int o = 32; o > 0; o >>= 1) {
-            const unsigned long long x = __shfl_xor(v, o);
-            v = j == 0 ? (x < v ? x : v) : v + x;
+            const unsigned long long x = __shfl_xor(v[j], o);
+            v[j] = j == 0 ? (x < v[j] ? x : v[j]) : v[j] + x;
         }
-        if (lane == 0) s_v[w][j] = v;
+        if (lane == 0) s_v[w][j] = v[j];
     }
     __syncthreads();
     if (threadIdx.x < kEqPart) {
         const uint32_t j = threadIdx.x;
-        unsigned long long v = s_v[0][j];
-        for (int ww = 1; ww < 4; ++ww) v = j == 0 ? (s_v[ww][j] < v ? s_v[ww][j] : v) : v + s_v[ww][j];
-        if (j == 0) words[3] = v;
-        else words[3 + j] = v;   // words[4 + k] = left of source k
+        unsigned long long t = s_v[0][j];
+        for (int ww = 1; ww < 16; ++ww) t = j == 0 ? (s_v[ww][j] < t ? s_v[ww][j] : t) : t + s_v[ww][j];
+        if (j == 0) words[3] = t;
+        else words[3 + j] = t;   // words[4 + k] = left of source k
     }
     if (threadIdx.x == 0) {
         words[1] = pop_off[n_hosts];
@@ -341,7 +351,12 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
     const uint32_t H = Q.n_hosts;
     unsigned long long* words = Q.next.as<unsigned long long>();
     unsigned long long* part = words + kEqWords;
-    const uint32_t nb = std::min<uint32_t>(kEqCountBlocks, div_up(((uint64_t)H + 1) * kEqLanes, 256));
+    static const uint32_t grid_max = [] {
+        const char* v = std::getenv("SHD_EQ_COUNT_BLOCKS");
+        const unsigned long x = v ? std::strtoul(v, nullptr, 10) : 0ul;
+        return x >= 1 && x <= kEqCountBlocksMax ? (uint32_t)x : kEqCountBlocks;
+    }();
+    const uint32_t nb = std::min<uint32_t>(grid_max, div_up(((uint64_t)H + 1) * kEqLanes, 256));
     SHD_TRY(Q.ranges.ensure((size_t)H * kEqSrcMax * 8));
     eqr_count<<<nb, 256, 0, s>>>(H, S, window_end, Q.pop_cnt.as<uint32_t>(), Q.keep_cnt.as<uint32_t>(), part,
                                  Q.ranges.as<uint2>());
@@ -353,7 +368,7 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
         eqr_merge<<<div_up(H, 4), 256, 0, s>>>(H, S, out_off, out, nr, nrun ? nrun->off.as<uint32_t>() : nullptr,
                                                nrun_cur, Q.ranges.as<uint2>());
     SHD_HIP(hipGetLastError());
-    eq_totals<<<1, 256, 0, s>>>(H, nb, out_off, nrun ? nrun->off.as<uint32_t>() : nullptr, part, words);
+    eq_totals<<<1, 1024, 0, s>>>(H, nb, out_off, nrun ? nrun->off.as<uint32_t>() : nullptr, part, words);
     SHD_HIP(hipMemcpyAsync(ctx->h_pin + kEqPinWord, words, kEqWords * 8, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     return SHD_OK;
@@ -423,7 +438,7 @@ shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_hosts) {
     SHD_TRY(Q.pop_cnt.ensure((size_t)(n_hosts + 1) * 4));
     SHD_TRY(Q.keep_cnt.ensure((size_t)(n_hosts + 1) * 4));
     SHD_TRY(Q.pop_off.ensure((size_t)(n_hosts + 1) * 4));
-    SHD_TRY(Q.next.ensure((kEqWords + (size_t)kEqCountBlocks * kEqPart) * 8));
+    SHD_TRY(Q.next.ensure((kEqWords + (size_t)kEqCountBlocksMax * kEqPart) * 8));
     SHD_HIP(hipMemsetAsync(Q.pop_off.p, 0, (size_t)(n_hosts + 1) * 4, ctx->stream));
     SHD_HIP(hipStreamSynchronize(ctx->stream));
     Q.ccur = 0;
