@@ -156,6 +156,9 @@ struct EqOut {
 // binary-searches the other prefixes in LDS; larger hosts search global memory source by
 // source.  Then the batch's remainder [cut, end) is copied to the new run (in the same wave: a
 // separate streaming kernel, alone or beside the merge on the side stream, measured slower).
+#ifndef SHD_EQ_SEL
+#define SHD_EQ_SEL 1   // staging: lane per staged event (0: source after source, for A/B)
+#endif
 constexpr uint32_t kEqStage = 160;   // 17.5 KB per 4-wave workgroup: 8 workgroups (32 waves) per CU
 
 __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, const uint32_t* __restrict__ pop_off,
@@ -190,11 +193,64 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
         u_sb[k] = __builtin_amdgcn_readlane(my_sb, k);
     }
     const uint32_t po = pop_off[h];
+    // the batch remainder's first 128 events are loaded up front: their latency overlaps the
+    // merge instead of following it (its cut is the batch range's end from eqr_count)
+    uint32_t rb_m = 0, rb_e = 0, rb_no = 0;
+    uint64_t pf_t[2] = {0, 0}, pf_q[2] = {0, 0};
+    uint32_t pf_s[2] = {0, 0}, pf_p[2] = {0, 0};
+    if (S.b >= 0) {
+        const EqSrc& q = S.s[S.b];
+#pragma unroll
+        for (uint32_t k = 0; k < kEqSrcMax; ++k)
+            if ((int32_t)k == S.b) rb_m = u_lo[k] + u_c[k];
+        rb_e = q.off[h + 1];
+        rb_no = nrun_off[h];
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t j = rb_m + lane + 64 * u;
+            if (j < rb_e) {
+                pf_t[u] = q.deliver[j];
+                pf_s[u] = q.src[j];
+                pf_q[u] = q.seq[j];
+                pf_p[u] = q.pkt[j];
+            }
+        }
+    }
     if (npop <= kEqStage) {
         uint64_t* st = s_t[w];
         uint64_t* sq = s_q[w];
         uint64_t* sg = s_g[w];
         uint32_t* ss = s_s[w];
+#if SHD_EQ_SEL
+        // lane i0 loads staged event i0 straight from its source (the source's arrays picked by
+        // selects on wave-uniform values): every source's loads are in flight at once, instead
+        // of one source's round trip after another
+        for (uint32_t i0 = lane; i0 < npop; i0 += 64) {
+            uint32_t at = u_lo[0] + i0;
+            const uint64_t* dl = S.s[0].deliver;
+            const uint64_t* qp = S.s[0].seq;
+            const uint32_t* sp = S.s[0].src;
+            const uint64_t* tp = S.s[0].tag;
+            const uint32_t* pp = S.s[0].pkt;
+            uint64_t bt = S.s[0].batch;
+#pragma unroll
+            for (uint32_t j = 1; j < kEqSrcMax; ++j) {
+                if (j < S.n && u_sb[j] <= i0) {
+                    at = u_lo[j] + (i0 - u_sb[j]);
+                    dl = S.s[j].deliver;
+                    qp = S.s[j].seq;
+                    sp = S.s[j].src;
+                    tp = S.s[j].tag;
+                    pp = S.s[j].pkt;
+                    bt = S.s[j].batch;
+                }
+            }
+            st[i0] = dl[at];
+            sq[i0] = qp[at];
+            ss[i0] = sp[at];
+            sg[i0] = tp ? tp[at] : ((bt << 32) | pp[at]);
+        }
+#else
         for (uint32_t k = 0; k < S.n; ++k) {
             const EqSrc& q = S.s[k];
             const uint32_t lo = u_lo[k], c = u_c[k], sb = u_sb[k];
@@ -205,6 +261,7 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
                 sg[sb + i] = q.tag ? q.tag[lo + i] : ((q.batch << 32) | q.pkt[lo + i]);
             }
         }
+#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -262,15 +319,25 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
     }
     if (S.b >= 0) {   // the batch's remainder becomes the new run, whose cursor starts at its offset
         const EqSrc& q = S.s[S.b];
-        const uint32_t m = q.cut[h], e = q.off[h + 1], no = nrun_off[h];
-        for (uint32_t j = m + lane; j < e; j += 64) {
-            const uint32_t at = no + (j - m);
+#pragma unroll
+        for (uint32_t u = 0; u < 2; ++u) {
+            const uint32_t j = rb_m + lane + 64 * u;
+            if (j < rb_e) {
+                const uint32_t at = rb_no + (j - rb_m);
+                nrun.deliver[at] = pf_t[u];
+                nrun.src[at] = pf_s[u];
+                nrun.seq[at] = pf_q[u];
+                nrun.tag[at] = (q.batch << 32) | pf_p[u];
+            }
+        }
+        for (uint32_t j = rb_m + 128 + lane; j < rb_e; j += 64) {
+            const uint32_t at = rb_no + (j - rb_m);
             nrun.deliver[at] = q.deliver[j];
             nrun.src[at] = q.src[j];
             nrun.seq[at] = q.seq[j];
             nrun.tag[at] = (q.batch << 32) | q.pkt[j];
         }
-        if (lane == 0) nrun_cur[h] = no;
+        if (lane == 0) nrun_cur[h] = rb_no;
     }
 }
 
