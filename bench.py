@@ -501,6 +501,8 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4):
     N.check(eng.lib.shd_relay_setup(eng.ctx, H, N.ptr(rl["host_node"]), 1000, N.ptr(lat_table), N.ptr(loss_table),
                                     N.ptr(rl["rng0"]), N.ptr(np.zeros(H, np.uint64))), "relay_setup")
     N.check(eng.lib.shd_equeue_setup(eng.ctx, H), "equeue_setup")
+    # the relay leg's counters-on run leaves them on: this leg times the default (counters off)
+    N.check(eng.lib.shd_relay_set_counters(eng.ctx, 0), "set_counters")
     st = torch.empty(P, dtype=torch.uint8, device="cuda")
     ev = [torch.empty(H + 1, dtype=torch.int32, device="cuda"), torch.empty(P, dtype=torch.int64, device="cuda"),
           torch.empty(P, dtype=torch.int32, device="cuda"), torch.empty(P, dtype=torch.int64, device="cuda"),
@@ -732,6 +734,8 @@ def main():
             rl_c = relay_leg(eng, world, rank, max(2, ks // 3), 1, r["lat"], r["loss"], counters=True,
                              inputs=inputs)
             rel["counters_on_ms_per_round"] = rl_c["ms_per_step"]
+            if eng.lib.shd_relay_set_counters(eng.ctx, 0) != 0:   # back to the default for what follows
+                raise RuntimeError("shd_relay_set_counters failed")
             ok, e2e = relay_check_and_e2e(eng, rl, r["lat"], r["loss"])
             rel["e2e_host_buffers"] = e2e
             rel["bit_exact_vs_cpu"] = bool(ok)
