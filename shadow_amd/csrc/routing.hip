@@ -760,8 +760,9 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, uint64_t* __restrict__ glab, uint32_t use_bkt, uint32_t use_flat,
     uint32_t* __restrict__ nh_out, uint32_t* __restrict__ gpred, const uint2* __restrict__ arcs8,
-    const float* __restrict__ aq, uint32_t kl) {
+    const float* __restrict__ aq, uint32_t kl, uint32_t* __restrict__ row_ctr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ uint32_t s_next;
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(smem);
     uint32_t* ctl = bits + W;
@@ -776,7 +777,10 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
         const size_t at = ((size_t)((bkt + ((V + 3) / 4) * 4) - smem) + 7) & ~(size_t)7;
         llab = reinterpret_cast<uint64_t*>(smem + at);
     }
-    for (uint32_t row = row_begin + blockIdx.x; row < row_end; row += gridDim.x) {
+    // row_ctr (zeroed before the launch): after its first row a slot takes the next unclaimed row,
+    // so the grid drains together instead of waiting for the slot whose fixed rows ran longest
+    uint32_t row = row_begin + blockIdx.x;
+    while (row < row_end) {
         sssp_row<BLOCK, G, R, false, true, 0, FASTG>(lab, bits, ctl, wq, nullptr, abeg, aend, arcs, V, used,
                                            n_used, row, (size_t)(row - row_begin) * n_used,
                                            diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
@@ -784,6 +788,13 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
                                            gpred ? gpred + (size_t)blockIdx.x * V : nullptr, 0u, arcs8, aq, nullptr,
                                            llab, FASTG ? kl : 0u);
         __syncthreads();   // the next row re-initialises labels and bitmap
+        if (row_ctr) {
+            if (threadIdx.x == 0) s_next = row_begin + gridDim.x + atomicAdd(row_ctr, 1u);
+            __syncthreads();
+            row = s_next;
+        } else {
+            row += gridDim.x;
+        }
     }
 }
 
@@ -1661,6 +1672,12 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
     const uint32_t* usedp = ro ? ctx->g_usedr.as<uint32_t>() : ctx->g_used.as<uint32_t>();
     const uint2* a8 = ro ? ctx->g_arc8r.as<uint2>() : ctx->g_arc8.as<uint2>();
     const float* aqp = ro ? ctx->g_aqr.as<float>() : ctx->g_aq.as<float>();
+    // dynamic row claiming (SHD_SSSP_DYN=0: fixed round-robin rows, for A/B)
+    uint32_t* row_ctr = nullptr;
+    if (env_u32("SHD_SSSP_DYN", 1) != 0) {
+        row_ctr = reinterpret_cast<uint32_t*>(ctx->g_flags.as<char>() + 48);
+        (void)hipMemsetAsync(row_ctr, 0, 4, ctx->stream);
+    }
     hipExtLaunchKernelGGL(
         kern, dim3(grid), dim3(BLOCK), (uint32_t)lds, ctx->stream,
         ctx->time_now ? ctx->ev[2] : nullptr, ctx->time_now ? ctx->ev[3] : nullptr, 0u,
@@ -1669,7 +1686,7 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
         ctx->g_flags.as<uint32_t>(), reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16), delta,
         ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr,
         ctx->g_glab.as<uint64_t>(), use_bkt, use_flat, ctx->nh_out,
-        ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr, a8, aqp, ro ? kl : 0u);
+        ctx->nh_out ? ctx->g_pred.as<uint32_t>() : nullptr, a8, aqp, ro ? kl : 0u, row_ctr);
 }
 
 // Kernel 1b driver: labels in global memory (graphs whose labels exceed the LDS).
