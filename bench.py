@@ -323,10 +323,14 @@ def c4_leg(eng, world, rank, steps, gather=True, cpu=True):
                unit="node-pairs/s", scaling="strong", all_gather=bool(gather),
                roofline=sssp_roofline(r["rows"], arcs, n, kernel_ms))
     if cpu and rank == 0 and world == 1:
-        cb, clat, closs = cpu_rows_baseline(el, (0, 64), n, "C4")
+        # the LAST 64 rows: the persistent kernel's slots take every row past the grid (the first
+        # 2 x n_cu rows) from the row counter, so these are claimed rows, not a slot's first row
+        lo = n - 64
+        cb, clat, closs = cpu_rows_baseline(el, (lo, n), n, "C4")
         lat, loss = r["lat_dev"], r["loss_dev"]
-        cb["bit_exact_vs_gpu"] = bool(np.array_equal(clat, lat[:64].cpu().numpy().view(np.uint64)) and
-                                      np.array_equal(closs.view(np.uint32), loss[:64].cpu().numpy().view(np.uint32)))
+        cb["bit_exact_vs_gpu"] = bool(np.array_equal(clat, lat[lo:].cpu().numpy().view(np.uint64)) and
+                                      np.array_equal(closs.view(np.uint32), loss[lo:].cpu().numpy().view(np.uint32)))
+        cb["rows_checked"] = [lo, n]
         out["cpu_baseline"] = cb
     del r
     torch.cuda.empty_cache()

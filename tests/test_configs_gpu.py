@@ -41,6 +41,24 @@ def test_c4_row_slices_bit_exact(engine, c4, rows):
         _assert_rows(t, lat, loss)
 
 
+def test_c4_claimed_rows_bit_exact(engine, c4):
+    """C4 rows [0, 2048) in one launch: the 2 x n_cu slots (512 on MI355X) take their first rows by
+    index and every later row from the row counter, so rows 1536-1599 and 1984-2047 are claimed
+    rows of the same kernel that runs the benchmarked build -- compared against the row-range
+    oracle (graph/mod.rs:185-230)."""
+    el, g, used = c4
+    t = g.compute_shortest_paths(used, engine, algo=3, rows=(0, 2048))
+    info = engine.last_info()
+    assert info["algo_used"] == 3 and info["wide_latency"] == 0
+    for lo, hi in ((1536, 1600), (1984, 2048)):
+        code, lat, loss, _ = corc.routing(50_000, el.src, el.dst, el.latency_ns, el.packet_loss, False,
+                                          used, rows=(lo, hi))
+        assert code == "OK"
+        assert np.array_equal(t.lat[lo:hi], lat)
+        assert np.array_equal(t.loss[lo:hi].view(np.uint32), loss.view(np.uint32))
+    del t
+
+
 def test_c3_full_table_bit_exact(engine):
     from shadow_amd import synth
     el = synth.barabasi_albert(10_000, 3, 2)

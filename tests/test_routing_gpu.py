@@ -201,6 +201,63 @@ def test_global_label_kernel_large_graph(engine, algo):
     _assert_table(t, lat, loss.view(np.uint32))
 
 
+def _tie_heavy_ba(n, m, seed, directed):
+    """BA graph with integer-ms latencies in [1, 6] (many equal-latency paths, so the loss
+    tie-break decides); directed: every undirected edge becomes two arcs with their own draws."""
+    from shadow_amd import synth
+    el = synth.barabasi_albert(n, m, seed)
+    rng = np.random.default_rng(seed + 100)
+    s, d = el.src.copy(), el.dst.copy()
+    if directed:
+        keep = s != d
+        s = np.concatenate([s, d[keep]])
+        d = np.concatenate([d, el.src[keep]])
+    lat = rng.integers(1, 7, size=len(s)).astype(np.uint64) * np.uint64(1_000_000)
+    loss = rng.uniform(0, 0.2, size=len(s)).astype(np.float32)
+    loss[rng.random(len(s)) < 0.1] = np.float32(0.0)
+    return el.node_ids, s, d, lat, loss, directed
+
+
+@pytest.mark.parametrize("directed", [False, True])
+@pytest.mark.parametrize("slots", ["2", "1"])
+def test_global_label_kernel_claimed_rows(engine, directed, slots, monkeypatch):
+    """Every row of a 3,000-node tie-heavy graph on the persistent global-label kernel, built as
+    C4 is (locality order + LDS labels for the hubs, SHD_SSSP_REORDER=1).  The grid holds
+    slots x n_cu (256 CUs: 512 or 256) slots, so rows past it -- most of the table -- are taken
+    from the row counter (sssp_global_group's dynamic claiming), and every one of them is compared
+    against the C restatement (graph/mod.rs:185-230)."""
+    from shadow_amd.routing import NetworkGraph
+    monkeypatch.setenv("SHD_SSSP_GLOBAL", "1")
+    monkeypatch.setenv("SHD_SSSP_REORDER", "1")
+    monkeypatch.setenv("SHD_SSSP_SLOTS", slots)
+    n = 3000
+    ids, s, d, l, p, directed = _tie_heavy_ba(n, 3, 31 + int(slots), directed)
+    used = np.arange(n, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(n, s, d, l, p, directed, used)
+    assert code == "OK"
+    g = NetworkGraph(ids, s, d, l, p, directed)
+    for algo in (1, 3):
+        t = g.compute_shortest_paths(used, engine, algo=algo)
+        assert engine.last_info()["algo_used"] == algo
+        _assert_table(t, lat, loss.view(np.uint32))
+
+
+def test_global_label_kernel_claimed_rows_sub_range(engine, monkeypatch):
+    """A row range that does not start at 0 (a rank's shard): claimed rows are offset by
+    row_begin + grid, so rows [1000, 2900) of a 3,000-node graph, every one compared."""
+    from shadow_amd.routing import NetworkGraph
+    monkeypatch.setenv("SHD_SSSP_GLOBAL", "1")
+    monkeypatch.setenv("SHD_SSSP_REORDER", "1")
+    n = 3000
+    ids, s, d, l, p, directed = _tie_heavy_ba(n, 2, 77, False)
+    used = np.random.default_rng(3).permutation(n).astype(np.uint32)
+    rows = (1000, 2900)
+    code, lat, loss, _ = corc.routing(n, s, d, l, p, directed, used, rows=rows)
+    assert code == "OK"
+    t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=3, rows=rows)
+    _assert_table(t, lat, loss.view(np.uint32))
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_global_label_kernel_forced(engine, seed, monkeypatch):
     """The global-label kernel on small tie-heavy graphs (forced with SHD_SSSP_GLOBAL=1)."""
