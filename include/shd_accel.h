@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SHD_ABI_VERSION 1
+#define SHD_ABI_VERSION 2
 
 typedef enum shd_status {
     SHD_OK = 0,
@@ -164,9 +164,18 @@ shd_status shd_routing_last_info(const shd_ctx* ctx, shd_routing_info* info);
  * spread by sampling. */
 shd_status shd_routing_set_timing(shd_ctx* ctx, uint32_t every);
 
-/* Look up one pair of the resident table (row index relative to row_begin of the last build). */
+/* Look up one pair of the resident table (row index relative to row_begin of the last build).
+ * After shd_routing_mirror the lookup reads the pinned host mirror (no device round trip: what a
+ * worker_getLatency-rate caller -- worker.rs:660-670, tcp.c:451-452 -- needs); otherwise it copies
+ * the pair from the device. */
 shd_status shd_routing_lookup(shd_ctx* ctx, uint32_t src_row, uint32_t dst_col,
                               uint64_t* latency_ns, float* packet_loss);
+/* n lookups in one device gather and one copy (host arrays; any output may be NULL). */
+shd_status shd_routing_lookup_batch(shd_ctx* ctx, uint64_t n, const uint32_t* src_row, const uint32_t* dst_col,
+                                    uint64_t* latency_ns, float* packet_loss);
+/* Keep a pinned host copy of the resident table (rows x cols x 12 B) for host-side lookups; it is
+ * dropped with the resident table (the next build or prepare).  enable = 0 drops it. */
+shd_status shd_routing_mirror(shd_ctx* ctx, int32_t enable);
 shd_status shd_routing_smallest_latency(shd_ctx* ctx, uint64_t* latency_ns);
 
 /*
@@ -240,6 +249,10 @@ typedef struct shd_relay_out {
     uint64_t min_deliver;
     uint64_t min_latency;
     uint64_t n_sent;
+    uint32_t n_dst;      /* destination hosts ev_off covers (ev_off has n_dst + 1 entries): written by
+                            the relay calls; a caller building this struct for shd_equeue_advance
+                            sets it (the queues check it against their host count) */
+    uint32_t reserved;
 } shd_relay_out;
 
 shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round* round,
@@ -249,19 +262,6 @@ shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round
  * ev_* must hold n_packets entries).  Used by the multi-GPU driver and the benchmark. */
 shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const shd_round* round,
                                   shd_relay_out* d_out);
-
-/*
- * Multi-GPU receive side (device buffers).  n_runs event chunks laid end to end (chunk r starts
- * at d_run_base[r]; d_run_base[n_runs] = n_events); chunk r is grouped by destination with local
- * offsets d_run_off[r*(n_dst+1) + d] and each destination's run in EventQueue order, as
- * shd_relay_round_device returns it.  Senders must own disjoint source-host ranges.  Writes the
- * merged events (again in EventQueue order per destination) and d_out->ev_off[n_dst+1].
- */
-shd_status shd_events_merge_device(shd_ctx* ctx, uint32_t n_runs, uint32_t n_dst,
-                                   const uint32_t* d_run_base, const uint32_t* d_run_off,
-                                   const uint64_t* d_deliver, const uint32_t* d_src,
-                                   const uint64_t* d_seq, const uint32_t* d_pkt,
-                                   uint64_t n_events, shd_relay_out* d_out);
 
 /* ---------------------------------------------------------------- multi-GPU */
 /*
@@ -335,6 +335,10 @@ typedef struct shd_equeue_out {
                                    minimum over the hosts); UINT64_MAX when none is left */
 } shd_equeue_out;
 
+/* n_hosts = all hosts.  Under a communicator of > 1 ranks the queues hold this rank's destination
+ * shard [lo, hi) = shd_shard_range(n_hosts) -- the hosts whose events shd_relay_round_sharded
+ * returns here -- and every per-host array (the batch's ev_off, the popped off[]) covers those
+ * hi - lo hosts.  A batch whose n_dst differs from the queues' host count is SHD_ERR_INVALID. */
 shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_hosts);
 shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64_t window_end,
                               shd_equeue_out* out);
@@ -344,6 +348,37 @@ shd_status shd_equeue_copy_popped(shd_ctx* ctx, uint32_t* off, uint64_t* deliver
 /* Host copy of the pending queues (same layout; any pointer may be NULL). */
 shd_status shd_equeue_pending(shd_ctx* ctx, uint32_t* off, uint64_t* deliver, uint32_t* src,
                               uint64_t* seq, uint64_t* tag, uint64_t* n_pending);
+
+/* ---------------------------------------------------------------- round window */
+/*
+ * Runahead (src/main/core/scheduler/runahead.rs:12-115) kept in the context, and the next
+ * scheduling window (SimController::manager_finished_current_round, controller.rs:86-111) from
+ * the engine's own state.  shd_runahead_setup = Runahead::new(is_runahead_dynamic,
+ * min_possible_latency, min_runahead_config) (manager.rs:246-251): min_possible_latency_ns = 0
+ * takes RoutingInfo::get_smallest_latency_ns of the resident table; min_runahead_config_ns = 0
+ * is None.  Every committed relay round (single or sharded; its min_latency reduced over all
+ * ranks) then updates the lowest used latency when dynamic (update_lowest_used_latency,
+ * worker.rs:380).  shd_round_window takes the caller's earliest non-packet event time
+ * (UINT64_MAX: none) and the experiment end, and returns the window [start, end) the reference's
+ * manager would open next: start = the minimum over that time, the pending queues' heads and the
+ * last relay output not yet merged (manager.rs:430-464; UINT64_MAX = none, which is
+ * EmulatedTime::MAX), end = min(start + runahead (saturating at EmulatedTime::MAX), end_time);
+ * *running = start < end.  Under a communicator the minimum is reduced over all ranks: a
+ * collective (every rank calls it, and every rank gets the same window).
+ */
+shd_status shd_runahead_setup(shd_ctx* ctx, int32_t dynamic, uint64_t min_possible_latency_ns,
+                              uint64_t min_runahead_config_ns);
+shd_status shd_runahead_get(const shd_ctx* ctx, uint64_t* runahead_ns);
+shd_status shd_round_window(shd_ctx* ctx, uint64_t cpu_next_event_time, uint64_t end_time,
+                            uint64_t* window_start, uint64_t* window_end, int32_t* running);
+/* The window arithmetic alone (no context, no GPU): controller.rs:92-111 for a given minimum
+ * next event time and runahead. */
+shd_status shd_window_compute(uint64_t min_next_event_time, uint64_t runahead_ns, uint64_t end_time,
+                              uint64_t* window_start, uint64_t* window_end, int32_t* running);
+
+/* Copy bytes from an engine-owned device array (e.g. shd_equeue_out, a sharded relay output) to
+ * host memory on the context's stream; returns when the copy is complete. */
+shd_status shd_copy_to_host(shd_ctx* ctx, void* dst, const void* d_src, size_t bytes);
 
 /* Read back the per-host RNG states / next event ids (e.g. to hand RNG use back to the CPU).
  * A sharded context's own hosts carry their current state, the others their setup state. */

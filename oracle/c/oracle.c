@@ -349,17 +349,22 @@ static ev_t evq_pop(evq_t* q) {
  * Returns number of SENT packets; fills status[n], deliver[n], seq[n], min_deliver, min_latency.
  * rng/next_id are updated in place.  chance (nullable) replaces the draws.
  */
-int64_t orc_relay_round(uint32_t n_hosts, const uint32_t* src_off, const uint64_t* send_time,
-                        const uint32_t* dst_host, const uint32_t* payload, const double* chance,
-                        const uint32_t* host_node, uint32_t n_nodes, const uint64_t* lat,
-                        const float* loss, uint64_t* rng, uint64_t* next_id,
-                        uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end,
-                        int threads, uint8_t* status, uint64_t* deliver, uint64_t* seq,
-                        uint64_t* min_deliver, uint64_t* min_latency,
-                        uint32_t* out_off, uint64_t* out_deliver, uint32_t* out_src,
-                        uint64_t* out_seq, uint32_t* out_pkt) {
-    evq_t* q = (evq_t*)calloc(n_hosts, sizeof(evq_t));
-    for (uint32_t h = 0; h < n_hosts; h++) pthread_mutex_init(&q[h].mu, NULL);
+int orc_eq_push_one(void* p, uint32_t dst, uint64_t t, uint32_t src, uint64_t seq, uint64_t tag);
+
+/* eq != NULL (orc_relay_round_eq): every SENT packet goes into the persistent destination queues
+ * of oracle/c/equeue.c instead (tag = batch_no << 32 | packet index); out_* are then unused. */
+static int64_t relay_round_impl(uint32_t n_hosts, const uint32_t* src_off, const uint64_t* send_time,
+                                const uint32_t* dst_host, const uint32_t* payload, const double* chance,
+                                const uint32_t* host_node, uint32_t n_nodes, const uint64_t* lat,
+                                const float* loss, uint64_t* rng, uint64_t* next_id,
+                                uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end,
+                                int threads, uint8_t* status, uint64_t* deliver, uint64_t* seq,
+                                uint64_t* min_deliver, uint64_t* min_latency,
+                                uint32_t* out_off, uint64_t* out_deliver, uint32_t* out_src,
+                                uint64_t* out_seq, uint32_t* out_pkt, void* eq, uint64_t batch_no) {
+    evq_t* q = eq ? NULL : (evq_t*)calloc(n_hosts, sizeof(evq_t));
+    if (q)
+        for (uint32_t h = 0; h < n_hosts; h++) pthread_mutex_init(&q[h].mu, NULL);
     uint64_t gmin_d = ~0ULL, gmin_l = ~0ULL;
     int64_t n_sent = 0;
     if (threads > 0) omp_set_num_threads(threads);
@@ -390,14 +395,19 @@ int64_t orc_relay_round(uint32_t n_hosts, const uint32_t* src_off, const uint64_
                 ev_t e = {t, h, 0, id, i, 0};
                 id++;
                 n_sent++;
-                pthread_mutex_lock(&q[d].mu);
-                evq_push(&q[d], e);
-                pthread_mutex_unlock(&q[d].mu);
+                if (eq) {
+                    orc_eq_push_one(eq, d, t, h, e.seq, (batch_no << 32) | i);
+                } else {
+                    pthread_mutex_lock(&q[d].mu);
+                    evq_push(&q[d], e);
+                    pthread_mutex_unlock(&q[d].mu);
+                }
             }
             next_id[h] = id;
         }
     }
     *min_deliver = gmin_d; *min_latency = gmin_l;
+    if (!q) return n_sent;
     if (out_off) {
         out_off[0] = 0;
         for (uint32_t h = 0; h < n_hosts; h++) out_off[h + 1] = out_off[h] + q[h].n;
@@ -414,6 +424,33 @@ int64_t orc_relay_round(uint32_t n_hosts, const uint32_t* src_off, const uint64_
     for (uint32_t h = 0; h < n_hosts; h++) { free(q[h].a); pthread_mutex_destroy(&q[h].mu); }
     free(q);
     return n_sent;
+}
+
+int64_t orc_relay_round(uint32_t n_hosts, const uint32_t* src_off, const uint64_t* send_time,
+                        const uint32_t* dst_host, const uint32_t* payload, const double* chance,
+                        const uint32_t* host_node, uint32_t n_nodes, const uint64_t* lat,
+                        const float* loss, uint64_t* rng, uint64_t* next_id,
+                        uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end,
+                        int threads, uint8_t* status, uint64_t* deliver, uint64_t* seq,
+                        uint64_t* min_deliver, uint64_t* min_latency,
+                        uint32_t* out_off, uint64_t* out_deliver, uint32_t* out_src,
+                        uint64_t* out_seq, uint32_t* out_pkt) {
+    return relay_round_impl(n_hosts, src_off, send_time, dst_host, payload, chance, host_node, n_nodes, lat, loss,
+                            rng, next_id, round_end, sim_end, bootstrap_end, threads, status, deliver, seq,
+                            min_deliver, min_latency, out_off, out_deliver, out_src, out_seq, out_pkt, NULL, 0);
+}
+
+/* send_packet for a round with push_packet_to_host into persistent destination queues (orc_eq_new) */
+int64_t orc_relay_round_eq(uint32_t n_hosts, const uint32_t* src_off, const uint64_t* send_time,
+                           const uint32_t* dst_host, const uint32_t* payload, const double* chance,
+                           const uint32_t* host_node, uint32_t n_nodes, const uint64_t* lat,
+                           const float* loss, uint64_t* rng, uint64_t* next_id,
+                           uint64_t round_end, uint64_t sim_end, uint64_t bootstrap_end,
+                           int threads, uint8_t* status, uint64_t* deliver, uint64_t* seq,
+                           uint64_t* min_deliver, uint64_t* min_latency, void* eq, uint64_t batch_no) {
+    return relay_round_impl(n_hosts, src_off, send_time, dst_host, payload, chance, host_node, n_nodes, lat, loss,
+                            rng, next_id, round_end, sim_end, bootstrap_end, threads, status, deliver, seq,
+                            min_deliver, min_latency, NULL, NULL, NULL, NULL, NULL, eq, batch_no);
 }
 
 int orc_max_threads(void) { return omp_get_max_threads(); }

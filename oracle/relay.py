@@ -94,17 +94,44 @@ def relay_round(send_time, src_host, dst_host, payload, host_node, lat, loss,
                        np.array(eid, np.uint64), events, min_deliver, min_latency, counts)
 
 
-def next_window(min_next_event_time: int, runahead: int, end_time: int):
-    """``SimController::manager_finished_current_round`` (controller.rs:86-111)."""
-    start = min_next_event_time
-    stop = min(start + runahead, end_time)
+EMUTIME_MAX = U64_MAX - 1   # EmulatedTime::MAX (emulated_time.rs:27,47)
+
+
+def next_window(min_next_event_time, runahead: int, end_time: int):
+    """``SimController::manager_finished_current_round`` (controller.rs:86-111).  ``None`` as the
+    minimum is the manager's ``unwrap_or(EmulatedTime::MAX)`` (manager.rs:459-464);
+    ``checked_add`` fails past ``EMUTIME_MAX`` (``from_c_emutime``) and then gives ``MAX``."""
+    assert runahead != 0
+    start = EMUTIME_MAX if min_next_event_time is None else min(int(min_next_event_time), EMUTIME_MAX)
+    end = start + runahead
+    if end > EMUTIME_MAX:
+        end = EMUTIME_MAX
+    stop = min(end, end_time)
     return (start, stop) if start < stop else None
 
 
-def runahead(min_used_latency, min_possible_latency: int, runahead_config: int) -> int:
-    """``Runahead::get`` (runahead.rs:43-56)."""
+def runahead(min_used_latency, min_possible_latency: int, runahead_config) -> int:
+    """``Runahead::get`` (runahead.rs:43-56); ``runahead_config`` None is ``ZERO``."""
     r = min_possible_latency if min_used_latency is None else min_used_latency
-    return max(r, runahead_config)
+    return max(r, runahead_config or 0)
+
+
+class RunaheadState:
+    """``Runahead`` with ``update_lowest_used_latency`` (runahead.rs:58-115): the lowest latency of
+    every sent packet, kept only when dynamic."""
+
+    def __init__(self, dynamic: bool, min_possible_latency: int, runahead_config=None):
+        assert min_possible_latency > 0
+        self.dynamic, self.min_possible, self.cfg = dynamic, min_possible_latency, runahead_config
+        self.min_used = None
+
+    def update_lowest_used_latency(self, latency: int):
+        assert latency > 0
+        if self.dynamic and (self.min_used is None or latency < self.min_used):
+            self.min_used = latency
+
+    def get(self) -> int:
+        return runahead(self.min_used, self.min_possible, self.cfg)
 
 
 class EventQueues:

@@ -25,7 +25,7 @@ EXPORTED = [
     "shd_routing_build", "shd_routing_prepare", "shd_routing_run", "shd_routing_build_device",
     "shd_routing_last_info", "shd_routing_set_timing",
     "shd_routing_lookup", "shd_routing_smallest_latency", "shd_relay_setup", "shd_relay_round",
-    "shd_relay_round_device", "shd_events_merge_device", "shd_relay_get_host_state",
+    "shd_relay_round_device", "shd_relay_get_host_state",
     "shd_relay_set_counters", "shd_relay_last_pipeline",
     "shd_path_packet_counts",
     "shd_gml_parse", "shd_gml_graph", "shd_gml_node_bandwidth", "shd_gml_free",
@@ -35,6 +35,8 @@ EXPORTED = [
     "shd_shard_range", "shd_routing_run_sharded", "shd_relay_round_sharded",
     "shd_equeue_setup", "shd_equeue_advance", "shd_equeue_copy_popped", "shd_equeue_pending",
     "shd_routing_run_next_hops", "shd_assign_ips", "shd_gml_load",
+    "shd_runahead_setup", "shd_runahead_get", "shd_round_window", "shd_window_compute", "shd_copy_to_host",
+    "shd_routing_lookup_batch", "shd_routing_mirror",
 ]
 COMM_ID_BYTES = 128
 
@@ -77,7 +79,8 @@ class Batch(C.Structure):
 class RelayOut(C.Structure):
     _fields_ = [("status", C.c_void_p), ("ev_off", C.c_void_p), ("ev_deliver", C.c_void_p),
                 ("ev_src", C.c_void_p), ("ev_seq", C.c_void_p), ("ev_pkt", C.c_void_p),
-                ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64)]
+                ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64),
+                ("n_dst", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class EqueueOut(C.Structure):
@@ -147,7 +150,6 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_relay_get_host_state": (I32, [P, P, P]),
         "shd_relay_set_counters": (I32, [P, I32]),
         "shd_relay_last_pipeline": (I32, [P, P]),
-        "shd_events_merge_device": (I32, [P, U32, U32, P, P, P, P, P, P, U64, P]),
         "shd_path_packet_counts": (I32, [P, P]),
         "shd_gml_parse": (I32, [P, C.c_size_t, P, P, C.c_size_t]),
         "shd_gml_graph": (I32, [P, P]),
@@ -174,6 +176,13 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_equeue_advance": (I32, [P, P, U64, P]),
         "shd_equeue_copy_popped": (I32, [P, P, P, P, P, P]),
         "shd_equeue_pending": (I32, [P, P, P, P, P, P, P]),
+        "shd_runahead_setup": (I32, [P, I32, U64, U64]),
+        "shd_runahead_get": (I32, [P, P]),
+        "shd_round_window": (I32, [P, U64, U64, P, P, P]),
+        "shd_window_compute": (I32, [U64, U64, U64, P, P, P]),
+        "shd_copy_to_host": (I32, [P, P, P, C.c_size_t]),
+        "shd_routing_lookup_batch": (I32, [P, U64, P, P, P, P]),
+        "shd_routing_mirror": (I32, [P, I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

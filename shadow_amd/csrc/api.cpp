@@ -18,7 +18,17 @@ using namespace shd;
 
 // The resident table is about to be rebuilt or replaced: nothing may keep reading it.  A relay
 // set up on the resident table (shd_relay_setup with NULL tables) must be set up again.
+namespace shd {
+void drop_mirror(shd_ctx* ctx) {
+    if (ctx->h_mirror_lat) (void)hipHostFree(ctx->h_mirror_lat);
+    if (ctx->h_mirror_loss) (void)hipHostFree(ctx->h_mirror_loss);
+    ctx->h_mirror_lat = nullptr;
+    ctx->h_mirror_loss = nullptr;
+}
+}  // namespace shd
+
 static void drop_resident_table(shd_ctx* ctx) {
+    drop_mirror(ctx);
     ctx->t_rows = 0;
     ctx->t_full = false;
     if (ctx->relay.ready && !ctx->relay.own_table) ctx->relay.ready = false;
@@ -112,6 +122,7 @@ void shd_close(shd_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+    drop_mirror(ctx);
     if (ctx->own_stream && ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;  // DevBuf destructors free device memory
 }
@@ -292,15 +303,19 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
             rbytes[2 * q] = q == C.rank ? 0 : (size_t)theirs * n * 8;
             rbytes[2 * q + 1] = q == C.rank ? 0 : (size_t)theirs * n * 4;
         }
-        SHD_TRY(C.exchange(2, sp.data(), sb.data(), rp.data(), rbytes.data(), ctx->side));
+        // a failed exchange is carried into the status agreement below, never returned between
+        // two collectives (the peers would wait in the next chunk's exchange)
+        const shd_status xs = C.exchange(2, sp.data(), sb.data(), rp.data(), rbytes.data(), ctx->side);
+        if (xs != SHD_OK && st == SHD_OK) st = xs;
     }
-    if (n_chunks > 1) SHD_HIP(hipStreamSynchronize(ctx->side));
-    SHD_TRY(ctx->comm_scratch.ensure((size_t)(C.size + 1) * 16));
+    if (n_chunks > 1 && hipStreamSynchronize(ctx->side) != hipSuccess && st == SHD_OK) st = SHD_ERR_HIP;
+    // status agreement (comm_scratch was sized by shd_comm_init*)
     uint64_t* w = ctx->comm_scratch.as<uint64_t>();
     ctx->h_pin[40] = ((uint64_t)(uint32_t)st << 32) | (uint32_t)e.code;
     ctx->h_pin[41] = ((uint64_t)e.node_a << 32) | e.node_b;
-    SHD_HIP(hipMemcpyAsync(w + 2 * C.size, ctx->h_pin + 40, 16, hipMemcpyHostToDevice, s));
-    SHD_TRY(C.all_gather(w + 2 * C.size, w, 16, s));
+    if (hipMemcpyAsync(w + 2 * C.size, ctx->h_pin + 40, 16, hipMemcpyHostToDevice, s) != hipSuccess && st == SHD_OK)
+        st = SHD_ERR_HIP;
+    SHD_TRY(C.all_gather(w + 2 * C.size, w, 16, s));   // LocalComm agrees; an RCCL failure is fatal
     std::vector<uint64_t> all(2 * (size_t)C.size);
     SHD_HIP(hipMemcpyAsync(all.data(), w, all.size() * 8, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
@@ -329,21 +344,6 @@ shd_status shd_routing_set_timing(shd_ctx* ctx, uint32_t every) {
 shd_status shd_routing_last_info(const shd_ctx* ctx, shd_routing_info* info) {
     if (!ctx || !info) return SHD_ERR_INVALID;
     *info = ctx->info;
-    return SHD_OK;
-}
-
-shd_status shd_routing_lookup(shd_ctx* ctx, uint32_t src_row, uint32_t dst_col,
-                              uint64_t* latency_ns, float* packet_loss) {
-    if (!ctx) return SHD_ERR_INVALID;
-    if (ctx->t_rows == 0) return SHD_ERR_STATE;
-    if (src_row >= ctx->t_rows || dst_col >= ctx->t_cols) return SHD_ERR_INVALID;
-    SHD_HIP(hipSetDevice(ctx->device));
-    const size_t i = (size_t)src_row * ctx->t_cols + dst_col;
-    if (latency_ns)
-        SHD_HIP(hipMemcpyAsync(latency_ns, ctx->t_lat.as<uint64_t>() + i, 8, hipMemcpyDeviceToHost, ctx->stream));
-    if (packet_loss)
-        SHD_HIP(hipMemcpyAsync(packet_loss, ctx->t_loss.as<float>() + i, 4, hipMemcpyDeviceToHost, ctx->stream));
-    SHD_HIP(hipStreamSynchronize(ctx->stream));
     return SHD_OK;
 }
 

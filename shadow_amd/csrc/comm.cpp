@@ -39,11 +39,15 @@ struct RcclComm final : Comm {
     }
     shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes, void* const* recv,
                         const size_t* recv_bytes, hipStream_t s) override {
+        // the group is posted whatever happens to the own part: the peers' sends and receives
+        // must meet theirs
+        shd_status st = SHD_OK;
         for (int k = 0; k < n_parts; ++k) {   // own part: a device copy
             const size_t i = (size_t)rank * n_parts + k;
-            if (send_bytes[i] != recv_bytes[i]) return SHD_ERR_INVALID;
-            if (send_bytes[i])
-                SHD_HIP(hipMemcpyAsync(recv[i], send[i], send_bytes[i], hipMemcpyDeviceToDevice, s));
+            if (send_bytes[i] != recv_bytes[i]) st = SHD_ERR_INVALID;
+            else if (send_bytes[i] &&
+                     hipMemcpyAsync(recv[i], send[i], send_bytes[i], hipMemcpyDeviceToDevice, s) != hipSuccess)
+                st = SHD_ERR_HIP;
         }
         SHD_NCCL(ncclGroupStart());
         for (int r = 0; r < size; ++r) {
@@ -55,7 +59,7 @@ struct RcclComm final : Comm {
             }
         }
         SHD_NCCL(ncclGroupEnd());
-        return SHD_OK;
+        return st;
     }
     shd_status all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
         if (bytes) SHD_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, comm, s));
@@ -73,6 +77,7 @@ struct LocalGroup {
     std::vector<int> device;
     std::vector<const void*> ptr;     // published per rank (exchange: n * n * parts pointers)
     std::vector<size_t> bytes;
+    std::vector<int> pre, post;       // per rank: status on entry (with its pointers), on exit
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
         const uint64_t g = gen;
@@ -89,61 +94,79 @@ struct LocalGroup {
 struct LocalComm final : Comm {
     std::shared_ptr<LocalGroup> g;
     int device = 0;
-    // every collective: the rank's inputs are complete (stream sync), pointers are published
-    // (barrier), each rank pulls what it receives onto its own stream, syncs, and a second
-    // barrier keeps the senders' buffers alive until every pull has finished
+    // every collective: the rank's inputs are complete (stream sync), pointers and the entry
+    // status are published (barrier), each rank pulls what it receives onto its own stream --
+    // nothing from a rank that entered failed -- syncs, and the exit statuses are agreed (the
+    // lowest failing rank's wins, on every rank); the last barrier keeps the senders' buffers
+    // alive until every pull has finished and the statuses have been read
     shd_status copy(void* dst, const void* src, int src_dev, size_t n, hipStream_t s) {
         if (!n) return SHD_OK;
-        if (src_dev == device) SHD_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, s));
-        else SHD_HIP(hipMemcpyPeerAsync(dst, device, src, src_dev, n, s));
-        return SHD_OK;
+        const hipError_t e = src_dev == device ? hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, s)
+                                               : hipMemcpyPeerAsync(dst, device, src, src_dev, n, s);
+        return e == hipSuccess ? SHD_OK : SHD_ERR_HIP;
+    }
+    shd_status enter(hipStream_t s) {
+        const shd_status st = hipStreamSynchronize(s) == hipSuccess ? SHD_OK : SHD_ERR_HIP;
+        g->pre[rank] = (int)st;
+        return st;
+    }
+    shd_status leave(shd_status st, hipStream_t s) {
+        if (hipStreamSynchronize(s) != hipSuccess && st == SHD_OK) st = SHD_ERR_HIP;
+        g->post[rank] = (int)st;
+        g->barrier();
+        shd_status all = SHD_OK;
+        for (int q = 0; q < size && all == SHD_OK; ++q) all = (shd_status)g->post[q];
+        g->barrier();
+        return all;
     }
     shd_status all_to_all_u64(const uint64_t* send, uint64_t* recv, size_t count, hipStream_t s) override {
-        SHD_HIP(hipStreamSynchronize(s));
+        shd_status st = enter(s);
         g->ptr[rank] = send;
         g->barrier();
-        shd_status st = SHD_OK;
         for (int q = 0; q < size && st == SHD_OK; ++q)
-            st = copy(recv + (size_t)q * count, static_cast<const uint64_t*>(g->ptr[q]) + (size_t)rank * count,
-                      g->device[q], count * 8, s);
-        const hipError_t e = hipStreamSynchronize(s);
-        g->barrier();
-        return st != SHD_OK ? st : e == hipSuccess ? SHD_OK : SHD_ERR_HIP;
+            st = g->pre[q] != SHD_OK ? (shd_status)g->pre[q]
+                                     : copy(recv + (size_t)q * count,
+                                            static_cast<const uint64_t*>(g->ptr[q]) + (size_t)rank * count,
+                                            g->device[q], count * 8, s);
+        return leave(st, s);
     }
     shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes, void* const* recv,
                         const size_t* recv_bytes, hipStream_t s) override {
-        if (n_parts < 1 || n_parts > 4) return SHD_ERR_INVALID;   // the group's pointer slots
-        SHD_HIP(hipStreamSynchronize(s));
+        shd_status st = n_parts < 1 || n_parts > 4 ? SHD_ERR_INVALID : SHD_OK;   // the group's pointer slots
+        const shd_status e0 = enter(s);
+        if (st == SHD_OK) st = e0;
+        else g->pre[rank] = (int)st;
         const size_t per_rank = (size_t)size * n_parts;
-        for (size_t i = 0; i < per_rank; ++i) {
-            g->ptr[rank * per_rank + i] = send[i];
-            g->bytes[rank * per_rank + i] = send_bytes[i];
-        }
+        if (st == SHD_OK)
+            for (size_t i = 0; i < per_rank; ++i) {
+                g->ptr[rank * per_rank + i] = send[i];
+                g->bytes[rank * per_rank + i] = send_bytes[i];
+            }
         g->barrier();
-        shd_status st = SHD_OK;
-        for (int q = 0; q < size && st == SHD_OK; ++q)
+        for (int q = 0; q < size && st == SHD_OK; ++q) {
+            if (g->pre[q] != SHD_OK) {
+                st = (shd_status)g->pre[q];
+                break;
+            }
             for (int k = 0; k < n_parts && st == SHD_OK; ++k) {
                 const size_t from = (size_t)q * per_rank + (size_t)rank * n_parts + k;   // q's part k to me
                 const size_t to = (size_t)q * n_parts + k;
                 if (g->bytes[from] != recv_bytes[to]) st = SHD_ERR_INVALID;
                 else st = copy(recv[to], g->ptr[from], g->device[q], recv_bytes[to], s);
             }
-        const hipError_t e = hipStreamSynchronize(s);
-        g->barrier();
-        return st != SHD_OK ? st : e == hipSuccess ? SHD_OK : SHD_ERR_HIP;
+        }
+        return leave(st, s);
     }
     shd_status all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
-        SHD_HIP(hipStreamSynchronize(s));
+        shd_status st = enter(s);
         g->ptr[rank] = send;
         g->barrier();
-        shd_status st = SHD_OK;
         for (int q = 0; q < size && st == SHD_OK; ++q) {
             char* dst = static_cast<char*>(recv) + (size_t)q * bytes;
-            if (dst != g->ptr[q]) st = copy(dst, g->ptr[q], g->device[q], bytes, s);
+            if (g->pre[q] != SHD_OK) st = (shd_status)g->pre[q];
+            else if (dst != g->ptr[q]) st = copy(dst, g->ptr[q], g->device[q], bytes, s);
         }
-        const hipError_t e = hipStreamSynchronize(s);
-        g->barrier();
-        return st != SHD_OK ? st : e == hipSuccess ? SHD_OK : SHD_ERR_HIP;
+        return leave(st, s);
     }
 };
 
@@ -167,6 +190,9 @@ shd_status shd_comm_init(shd_ctx* ctx, int32_t n_ranks, int32_t rank, const uint
     SHD_HIP(hipSetDevice(ctx->device));
     auto c = std::unique_ptr<RcclComm>(new (std::nothrow) RcclComm());
     if (!c) return SHD_ERR_NOMEM;
+    // the sharded calls' status-agreement words: sized here, so no rank can fail to allocate them
+    // between two collectives
+    SHD_TRY(ctx->comm_scratch.ensure(comm_scratch_bytes(n_ranks)));
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
     SHD_NCCL(ncclCommInitRank(&c->comm, n_ranks, u, rank));
@@ -174,6 +200,7 @@ shd_status shd_comm_init(shd_ctx* ctx, int32_t n_ranks, int32_t rank, const uint
     c->size = n_ranks;
     ctx->comm = std::move(c);
     ctx->relay.ready = false;   // the relay's source shard follows the communicator: set up again
+    ctx->eq.ready = false;      // so do the queues' destination shard
     return SHD_OK;
 }
 
@@ -181,12 +208,18 @@ shd_status shd_comm_init_local(shd_ctx** ctxs, int32_t n_ranks) {
     if (!ctxs || n_ranks < 1) return SHD_ERR_INVALID;
     for (int r = 0; r < n_ranks; ++r)
         if (!ctxs[r]) return SHD_ERR_INVALID;
+    for (int r = 0; r < n_ranks; ++r) {
+        SHD_HIP(hipSetDevice(ctxs[r]->device));
+        SHD_TRY(ctxs[r]->comm_scratch.ensure(comm_scratch_bytes(n_ranks)));
+    }
     auto g = std::make_shared<LocalGroup>();
     g->n = n_ranks;
     g->device.resize(n_ranks);
     const size_t slots = (size_t)n_ranks * n_ranks * 4;   // exchange: up to 4 parts per peer
     g->ptr.assign(slots, nullptr);
     g->bytes.assign(slots, 0);
+    g->pre.assign(n_ranks, 0);
+    g->post.assign(n_ranks, 0);
     for (int r = 0; r < n_ranks; ++r) g->device[r] = ctxs[r]->device;
     for (int r = 0; r < n_ranks; ++r) {
         auto c = std::unique_ptr<LocalComm>(new (std::nothrow) LocalComm());
@@ -197,6 +230,7 @@ shd_status shd_comm_init_local(shd_ctx** ctxs, int32_t n_ranks) {
         c->size = n_ranks;
         ctxs[r]->comm = std::move(c);
         ctxs[r]->relay.ready = false;
+        ctxs[r]->eq.ready = false;
     }
     return SHD_OK;
 }
@@ -213,6 +247,7 @@ shd_status shd_comm_destroy(shd_ctx* ctx) {
     SHD_HIP(hipSetDevice(ctx->device));
     if (ctx->stream) SHD_HIP(hipStreamSynchronize(ctx->stream));
     if (ctx->comm && ctx->relay.sharded) ctx->relay.ready = false;
+    if (ctx->comm && ctx->comm->size > 1) ctx->eq.ready = false;
     ctx->comm.reset();
     return SHD_OK;
 }

@@ -15,6 +15,10 @@
 
 namespace shd {
 
+// Status contract: a collective either returns the same status on every rank (LocalComm agrees
+// on the lowest failing rank's status before it returns) or, for an RCCL enqueue failure, leaves
+// the communicator unusable (RCCL's own rule).  Callers therefore never return between two
+// collectives on a local error: they carry it into the next status agreement instead.
 struct Comm {
     int rank = 0, size = 1;
     virtual ~Comm() = default;
@@ -30,6 +34,10 @@ struct Comm {
     // send == recv + rank * bytes)
     virtual shd_status all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
 };
+
+// device words of shd_ctx::comm_scratch: the sharded routing build's status agreement (16 B
+// per rank + this rank's 16 B) and the sharded relay's growth agreement (8 B per rank)
+inline size_t comm_scratch_bytes(int n_ranks) { return ((size_t)n_ranks + 1) * 16 + (size_t)n_ranks * 8 + 64; }
 
 // Row / host shard of rank r among n ranks: contiguous blocks of ceil(total / n).
 inline void shard_range(uint32_t total, int n, int r, uint32_t* lo, uint32_t* hi) {

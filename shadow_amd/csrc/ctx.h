@@ -64,9 +64,22 @@ struct EqState {   // destination event queues (equeue.hip): a list of sorted ru
     DevBuf pop_cnt, keep_cnt, pop_off, next, left, scan_tmp;
     DevBuf ranges;                  // [n_hosts][kEqMaxRuns + 1] (cursor, cut) pairs of the last count
     int ccur = 0;
-    uint32_t n_hosts = 0;
+    uint32_t n_hosts = 0;           // queues held here: all hosts, or a sharded rank's [host_lo, host_lo + n_hosts)
+    uint32_t host_lo = 0, n_total = 0;
     uint64_t n_pending = 0, n_popped = 0, batches = 0;
+    uint64_t head = ~0ull;          // earliest pending deliver time after the last advance (local)
+    uint32_t scan_epoch = 0;        // eq_scan2's look-back state epoch
     bool ready = false;
+};
+
+// Runahead (src/main/core/scheduler/runahead.rs:12-115) and the round window
+// (controller.rs:86-111) for shd_round_window.
+struct RoundState {
+    bool ready = false;
+    bool dynamic = false;
+    uint64_t min_possible = 0, cfg = 0;   // Runahead::min_possible_latency, min_runahead_config (0: None)
+    uint64_t min_used = ~0ull;            // Runahead::min_used_latency (UINT64_MAX: None)
+    uint64_t batch_min_deliver = ~0ull;   // relay output not yet merged into the queues: its earliest deliver
 };
 
 struct TbState {   // token-bucket relays (tbucket.hip)
@@ -106,6 +119,7 @@ struct RelayState {
     // sharded rounds: packed outgoing events, exchange words, per-peer offset blocks, what was
     // received, and the merged events of this rank's destinations (engine-owned outputs)
     DevBuf x_rec, x_words, x_off, x_roff, x_rrec, m_off, m_deliver, m_src, m_seq, m_pkt;
+    uint64_t x_cap = 0;   // events x_rrec and m_* hold (grown with a growth agreement, never between collectives)
 };
 
 struct PreparedGraph {
@@ -135,6 +149,15 @@ struct PreparedGraph {
 
 }  // namespace shd
 
+struct shd_ctx;
+namespace shd {
+// a committed relay round's (all-rank) reductions: the runahead update (runahead.rs:60-115) and
+// the earliest deliver time of the relay output that the queues have not merged yet (rounds.cpp)
+void round_note(shd_ctx* ctx, uint64_t min_deliver, uint64_t min_latency);
+// free the host mirror of the resident table (it follows the table)
+void drop_mirror(shd_ctx* ctx);
+}  // namespace shd
+
 struct shd_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -150,6 +173,9 @@ struct shd_ctx {
     shd::DevBuf t_lat, t_loss;
     uint32_t t_rows = 0, t_cols = 0, t_row_begin = 0;
     bool t_full = false;
+    uint64_t* h_mirror_lat = nullptr;   // pinned host copy of the resident table (shd_routing_mirror)
+    float* h_mirror_loss = nullptr;
+    shd::DevBuf lk_scratch;             // shd_routing_lookup_batch
     shd_routing_info info{};
     uint32_t time_every = 1, time_calls = 0;   // shd_routing_set_timing
     bool time_now = true;                      // this build records ev[2] / ev[3]
@@ -168,6 +194,7 @@ struct shd_ctx {
 
     shd::RelayState relay;
     shd::EqState eq;
+    shd::RoundState rnd;
     shd::CodelState codel;
     shd::TbState tb;
 };

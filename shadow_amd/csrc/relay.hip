@@ -1262,46 +1262,6 @@ __device__ __forceinline__ bool ev3_less(uint64_t ta, uint32_t sa, uint64_t qa, 
     return qa < qb;
 }
 
-__global__ __launch_bounds__(256) void merge_runs(
-    uint32_t n_runs, uint32_t n_dst, const uint32_t* __restrict__ base,   // [n_runs+1] chunk starts
-    const uint32_t* __restrict__ off,                                     // [n_runs][n_dst+1]
-    const uint64_t* __restrict__ in_t, const uint32_t* __restrict__ in_s,
-    const uint64_t* __restrict__ in_q, const uint32_t* __restrict__ in_p,
-    const uint32_t* __restrict__ out_off,                                 // [n_dst+1]
-    uint64_t* __restrict__ out_t, uint32_t* __restrict__ out_s, uint64_t* __restrict__ out_q,
-    uint32_t* __restrict__ out_p) {
-    const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= base[n_runs]) return;
-    uint32_t r = 0;
-    while (r + 1 < n_runs && base[r + 1] <= e) ++r;
-    const uint32_t le = e - base[r];
-    const uint32_t* o = off + (size_t)r * (n_dst + 1);
-    uint32_t lo = 0, hi = n_dst;   // d with o[d] <= le < o[d+1]
-    while (hi - lo > 1) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (o[m] <= le) lo = m; else hi = m;
-    }
-    const uint32_t d = lo;
-    const uint64_t t = in_t[e], q = in_q[e];
-    const uint32_t sv = in_s[e];
-    uint32_t rank = le - o[d];
-    for (uint32_t r2 = 0; r2 < n_runs; ++r2) {
-        if (r2 == r) continue;
-        const uint32_t* o2 = off + (size_t)r2 * (n_dst + 1);
-        uint32_t a = base[r2] + o2[d], b = base[r2] + o2[d + 1];
-        while (a < b) {   // count of run r2's events less than this one
-            const uint32_t m = (a + b) >> 1;
-            if (ev3_less(in_t[m], in_s[m], in_q[m], t, sv, q)) a = m + 1; else b = m;
-        }
-        rank += a - (base[r2] + o2[d]);
-    }
-    const uint32_t pos = out_off[d] + rank;
-    out_t[pos] = t;
-    out_s[pos] = sv;
-    out_q[pos] = q;
-    out_p[pos] = in_p[e];
-}
-
 __global__ __launch_bounds__(256) void merge_offsets(uint32_t n_runs, uint32_t n_dst,
                                                      const uint32_t* __restrict__ off,
                                                      uint32_t* __restrict__ out_off) {
@@ -2154,7 +2114,10 @@ static shd_status relay_commit(shd_ctx* ctx, shd_relay_out* o) {
 static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
                                shd_relay_out* o) {
     SHD_TRY(relay_run(ctx, b, rd, o));
-    return relay_commit(ctx, o);
+    SHD_TRY(relay_commit(ctx, o));
+    o->n_dst = ctx->relay.n_hosts;
+    round_note(ctx, o->min_deliver, o->min_latency);
+    return SHD_OK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2163,22 +2126,27 @@ static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round
 // over ALL hosts; the events bound for rank r's hosts are one contiguous slice.  Per round:
 //   1. local pipeline (as one GPU) -> events grouped by destination, in EventQueue order;
 //   2. pack them as 24-byte records (deliver, seq, src, packet) and write, per peer, the
-//      peer's per-destination offsets; one all-to-all of 5 words per peer carries the event
-//      count for that peer and this rank's (status, min deliver, min latency, sent) -- the
-//      round's reductions ride on the sizing exchange, no separate all-reduce;
+//      peer's per-destination offsets; one all-gather of every rank's sizing row -- its status,
+//      reductions, receive capacity and event count per peer -- so every rank sees the whole
+//      count matrix: the round's reductions ride on it, and whether any rank must grow its
+//      receive buffers is known to all (then a second, one-word agreement follows the growth);
 //   3. one host sync: sizes, and every rank's status (a failed round on any rank fails the
 //      round everywhere, no host state is committed);
 //   4. one grouped point-to-point exchange (offsets + records to every peer);
 //   5. device k-way merge of the per-sender runs into this rank's destinations' events: the
 //      senders own disjoint source ranges, so the merge by (deliver, src, seq) is EventQueue
 //      order again (event.rs:84-155).
+// No rank returns between two collectives on a local failure: allocations that depend on the
+// round are folded into the status of the next agreement, the rest is sized at setup.
 // ------------------------------------------------------------------------------------------
 struct Ev24 {
     uint64_t deliver, seq;
     uint32_t src, pkt;
 };
 static_assert(sizeof(Ev24) == 24, "24-byte event record");
-constexpr uint32_t kXWords = 5;   // per peer: count, status, min deliver, min latency, sent
+// sizing row of a rank: [0] status [1] min deliver [2] min latency [3] sent [4] receive
+// capacity (events) [5..7] spare, then [kXHead + r] = events for rank r
+constexpr uint32_t kXHead = 8;
 
 __global__ __launch_bounds__(256) void pack_events24(uint64_t n, const uint64_t* __restrict__ t,
                                                      const uint64_t* __restrict__ q, const uint32_t* __restrict__ sv,
@@ -2195,18 +2163,17 @@ __device__ __forceinline__ void shard_of(uint32_t total, uint32_t world, uint32_
 }
 
 __global__ __launch_bounds__(64) void shard_words(uint32_t world, uint32_t H, const uint32_t* __restrict__ ev_off,
-                                                  uint64_t st, uint64_t md, uint64_t ml, uint64_t ns,
-                                                  uint64_t* __restrict__ words) {
-    const uint32_t r = threadIdx.x;
-    if (r >= world) return;
-    uint32_t lo, hi;
-    shard_of(H, world, r, &lo, &hi);
-    uint64_t* w = words + (size_t)r * kXWords;
-    w[0] = ev_off ? (uint64_t)(ev_off[hi] - ev_off[lo]) : 0ull;
-    w[1] = st;
-    w[2] = md;
-    w[3] = ml;
-    w[4] = ns;
+                                                  uint64_t st, uint64_t md, uint64_t ml, uint64_t ns, uint64_t cap,
+                                                  uint64_t* __restrict__ w) {
+    for (uint32_t r = threadIdx.x; r < world; r += 64) {
+        uint32_t lo, hi;
+        shard_of(H, world, r, &lo, &hi);
+        w[kXHead + r] = ev_off ? (uint64_t)(ev_off[hi] - ev_off[lo]) : 0ull;
+    }
+    if (threadIdx.x < kXHead) {
+        const uint64_t v[kXHead] = {st, md, ml, ns, cap, 0, 0, 0};
+        w[threadIdx.x] = v[threadIdx.x];
+    }
 }
 
 // peer r's block: its destinations' offsets relative to the slice start, at stage[lo_r + r ..]
@@ -2259,20 +2226,48 @@ __global__ __launch_bounds__(256) void merge_runs24(uint32_t n_runs, uint32_t n_
     out_p[pos] = x.pkt;
 }
 
+// sharded rounds' buffers that depend only on the host count and the ranks (shd_relay_setup)
+static shd_status relay_shard_alloc(shd_ctx* ctx) {
+    RelayState& R = ctx->relay;
+    const uint32_t world = (uint32_t)ctx->comm->size, H = R.n_hosts;
+    uint32_t own_lo = 0, own_hi = 0;
+    shard_range(H, (int)world, ctx->comm->rank, &own_lo, &own_hi);
+    const size_t n_own = own_hi - own_lo;
+    SHD_TRY(R.x_words.ensure((size_t)world * (kXHead + world) * 8 + (size_t)world * 8 + 64));
+    SHD_TRY(R.x_off.ensure(((size_t)H + world) * 4));
+    SHD_TRY(R.x_roff.ensure((size_t)world * (n_own + 1) * 4 + (size_t)(world + 1) * 4));
+    SHD_TRY(R.m_off.ensure((n_own + 1) * 4));
+    SHD_TRY(R.ev_off.ensure(((size_t)H + 1) * 4));
+    R.x_cap = 0;
+    return SHD_OK;
+}
+
+// receive side of a sharded round for n events (records, merged arrays), with headroom
+static shd_status relay_recv_grow(RelayState& R, uint64_t n) {
+    const uint64_t m = std::max<uint64_t>(n + n / 2, 1024);
+    SHD_TRY(R.x_rrec.ensure(m * 24));
+    SHD_TRY(R.m_deliver.ensure(m * 8));
+    SHD_TRY(R.m_src.ensure(m * 4));
+    SHD_TRY(R.m_seq.ensure(m * 8));
+    SHD_TRY(R.m_pkt.ensure(m * 4));
+    R.x_cap = m;
+    return SHD_OK;
+}
+
 static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
                                       shd_relay_out* d_out) {
     RelayState& R = ctx->relay;
     Comm& C = *ctx->comm;
     hipStream_t s = ctx->stream;
-    const uint32_t H = R.n_hosts, world = (uint32_t)C.size;
+    const uint32_t H = R.n_hosts, world = (uint32_t)C.size, WR = kXHead + world;
     const uint64_t n = b->n_packets;
     const size_t nn = std::max<uint64_t>(n, 1);
-    // 1. the local pipeline into internal buffers (the caller's status array)
+    // 1. the local pipeline into internal buffers (the caller's status array); a failure here is
+    //    this rank's status in the sizing row, not a return
     shd_status st = SHD_OK;
     shd_relay_out lo{};
-    if (R.ev_off.ensure((size_t)(H + 1) * 4) != SHD_OK || R.ev_deliver.ensure(nn * 8) != SHD_OK ||
-        R.ev_src.ensure(nn * 4) != SHD_OK || R.ev_seq.ensure(nn * 8) != SHD_OK ||
-        R.ev_pkt.ensure(nn * 4) != SHD_OK || R.x_rec.ensure(nn * 24) != SHD_OK)
+    if (R.ev_deliver.ensure(nn * 8) != SHD_OK || R.ev_src.ensure(nn * 4) != SHD_OK ||
+        R.ev_seq.ensure(nn * 8) != SHD_OK || R.ev_pkt.ensure(nn * 4) != SHD_OK || R.x_rec.ensure(nn * 24) != SHD_OK)
         st = SHD_ERR_NOMEM;
     if (st == SHD_OK) {
         lo.status = d_out->status;
@@ -2283,70 +2278,81 @@ static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const sh
         lo.ev_pkt = R.ev_pkt.as<uint32_t>();
         st = relay_run(ctx, b, rd, &lo);
     }
-    // 2. records, per-peer offset blocks, the sizing words (with this rank's reductions)
-    SHD_TRY(R.x_words.ensure((size_t)world * kXWords * 16));
-    SHD_TRY(R.x_off.ensure(((size_t)H + world) * 4));
-    uint64_t* w_send = R.x_words.as<uint64_t>();
-    uint64_t* w_recv = w_send + (size_t)world * kXWords;
+    // 2. records, per-peer offset blocks, this rank's sizing row (buffers sized at setup)
+    uint64_t* rows = R.x_words.as<uint64_t>();            // [world][WR] after the all-gather
+    uint64_t* agree = rows + (size_t)world * WR;           // [world] growth agreement
     const uint64_t ns_local = st == SHD_OK ? R.red_host[2] : 0;
     if (st == SHD_OK && ns_local)
         pack_events24<<<div_up(ns_local, 256), 256, 0, s>>>(ns_local, lo.ev_deliver, lo.ev_seq, lo.ev_src,
                                                             lo.ev_pkt, R.x_rec.as<Ev24>());
     shard_words<<<1, 64, 0, s>>>(world, H, st == SHD_OK ? lo.ev_off : nullptr, (uint64_t)st,
                                  st == SHD_OK ? R.red_host[0] : ~0ull, st == SHD_OK ? R.red_host[1] : ~0ull,
-                                 ns_local, w_send);
+                                 ns_local, R.x_cap, rows + (size_t)C.rank * WR);
     if (st == SHD_OK)
         shard_offsets<<<dim3(div_up((uint64_t)(H + world - 1) / world + 1, 256), world), 256, 0, s>>>(
             world, H, lo.ev_off, R.x_off.as<uint32_t>());
-    SHD_HIP(hipGetLastError());
-    SHD_TRY(C.all_to_all_u64(w_send, w_recv, kXWords, s));
-    // 3. one host sync: what every peer sends here, and every rank's outcome
-    std::vector<uint64_t> w(2 * (size_t)world * kXWords);
-    SHD_HIP(hipMemcpyAsync(w.data(), w_send, w.size() * 8, hipMemcpyDeviceToHost, s));
+    if (hipGetLastError() != hipSuccess && st == SHD_OK) st = SHD_ERR_HIP;
+    SHD_TRY(C.all_gather(rows + (size_t)C.rank * WR, rows, (size_t)WR * 8, s));   // agreed (LocalComm) / fatal (RCCL)
+    // 3. one host sync: the count matrix, every rank's outcome and capacity
+    std::vector<uint64_t> w((size_t)world * WR);
+    SHD_HIP(hipMemcpyAsync(w.data(), rows, w.size() * 8, hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
-    const uint64_t* ws = w.data();
-    const uint64_t* wr = w.data() + (size_t)world * kXWords;
+    auto row = [&](uint32_t q) { return w.data() + (size_t)q * WR; };
     uint64_t md = ~0ull, ml = ~0ull, ns = 0;
+    for (uint32_t q = 0; q < world; ++q)
+        if ((shd_status)row(q)[0] != SHD_OK) return (shd_status)row(q)[0];   // the lowest failing rank's
     for (uint32_t q = 0; q < world; ++q) {
-        const uint64_t* x = wr + (size_t)q * kXWords;
-        if ((shd_status)x[1] != SHD_OK) return (shd_status)x[1];   // the lowest failing rank's
-        md = std::min<uint64_t>(md, x[2]);
-        ml = std::min<uint64_t>(ml, x[3]);
-        ns += x[4];
+        md = std::min<uint64_t>(md, row(q)[1]);
+        ml = std::min<uint64_t>(ml, row(q)[2]);
+        ns += row(q)[3];
     }
-    // 4. the exchange: part 0 = offsets block, part 1 = records
+    // receive totals of every rank: whether any rank must grow is known to all of them
+    bool grow = false;
+    for (uint32_t r = 0; r < world; ++r) {
+        uint64_t t = 0;
+        for (uint32_t q = 0; q < world; ++q) t += row(q)[kXHead + r];
+        grow = grow || t > row(r)[4];
+    }
     uint32_t own_lo = 0, own_hi = 0;
     shard_range(H, (int)world, C.rank, &own_lo, &own_hi);
     const uint32_t n_own = own_hi - own_lo;
     std::vector<uint32_t> rbase(world + 1, 0);
-    for (uint32_t q = 0; q < world; ++q) rbase[q + 1] = rbase[q] + (uint32_t)wr[(size_t)q * kXWords];
+    for (uint32_t q = 0; q < world; ++q) rbase[q + 1] = rbase[q] + (uint32_t)row(q)[kXHead + C.rank];
     const uint64_t n_recv = rbase[world];
-    SHD_TRY(R.x_roff.ensure((size_t)world * (n_own + 1) * 4 + (size_t)(world + 1) * 4));
-    SHD_TRY(R.x_rrec.ensure(std::max<uint64_t>(n_recv, 1) * 24));
+    if (grow) {   // every rank takes this branch: one more agreement, on the growth's outcome
+        shd_status gs = n_recv > R.x_cap ? relay_recv_grow(R, n_recv) : SHD_OK;
+        ctx->h_pin[44] = (uint64_t)gs;
+        if (hipMemcpyAsync(agree + C.rank, ctx->h_pin + 44, 8, hipMemcpyHostToDevice, s) != hipSuccess && gs == SHD_OK)
+            gs = SHD_ERR_HIP;   // (the row still goes out: the peers wait for it)
+        SHD_TRY(C.all_gather(agree + C.rank, agree, 8, s));
+        std::vector<uint64_t> a(world);
+        SHD_HIP(hipMemcpyAsync(a.data(), agree, world * 8, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipStreamSynchronize(s));
+        for (uint32_t q = 0; q < world; ++q)
+            if ((shd_status)a[q] != SHD_OK) return (shd_status)a[q];
+        if (gs != SHD_OK) return gs;
+    }
+    // 4. the exchange: part 0 = offsets block, part 1 = records
     std::vector<const void*> sp(2 * world);
     std::vector<void*> rp(2 * world);
     std::vector<size_t> sb(2 * world), rb(2 * world);
     uint64_t sent_before = 0;
+    const uint64_t* mine = row((uint32_t)C.rank);
     for (uint32_t r = 0; r < world; ++r) {
         uint32_t a = 0, z = 0;
         shard_range(H, (int)world, (int)r, &a, &z);
         sp[2 * r] = R.x_off.as<uint32_t>() + a + r;
         sb[2 * r] = (size_t)(z - a + 1) * 4;
         sp[2 * r + 1] = R.x_rec.as<Ev24>() + sent_before;
-        sb[2 * r + 1] = (size_t)ws[(size_t)r * kXWords] * 24;
-        sent_before += ws[(size_t)r * kXWords];
+        sb[2 * r + 1] = (size_t)mine[kXHead + r] * 24;
+        sent_before += mine[kXHead + r];
         rp[2 * r] = R.x_roff.as<uint32_t>() + (size_t)r * (n_own + 1);
         rb[2 * r] = (size_t)(n_own + 1) * 4;
         rp[2 * r + 1] = R.x_rrec.as<Ev24>() + rbase[r];
-        rb[2 * r + 1] = (size_t)wr[(size_t)r * kXWords] * 24;
+        rb[2 * r + 1] = (size_t)row(r)[kXHead + C.rank] * 24;
     }
-    SHD_TRY(C.exchange(2, sp.data(), sb.data(), rp.data(), rb.data(), s));
-    // 5. merge the per-sender runs
-    SHD_TRY(R.m_off.ensure((size_t)(n_own + 1) * 4));
-    SHD_TRY(R.m_deliver.ensure(std::max<uint64_t>(n_recv, 1) * 8));
-    SHD_TRY(R.m_src.ensure(std::max<uint64_t>(n_recv, 1) * 4));
-    SHD_TRY(R.m_seq.ensure(std::max<uint64_t>(n_recv, 1) * 8));
-    SHD_TRY(R.m_pkt.ensure(std::max<uint64_t>(n_recv, 1) * 4));
+    SHD_TRY(C.exchange(2, sp.data(), sb.data(), rp.data(), rb.data(), s));   // agreed (LocalComm) / fatal (RCCL)
+    // 5. merge the per-sender runs (no collective follows: a HIP failure from here on is local)
     uint32_t* d_base = R.x_roff.as<uint32_t>() + (size_t)world * (n_own + 1);
     SHD_HIP(hipMemcpyAsync(d_base, rbase.data(), (world + 1) * 4, hipMemcpyHostToDevice, s));
     merge_offsets<<<div_up((uint64_t)n_own + 1, 256), 256, 0, s>>>(world, n_own, R.x_roff.as<uint32_t>(),
@@ -2367,6 +2373,8 @@ static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const sh
     d_out->min_deliver = md;
     d_out->min_latency = ml;
     d_out->n_sent = ns;
+    d_out->n_dst = n_own;
+    round_note(ctx, md, ml);
     R.last_recv = n_recv;
     return SHD_OK;
 }
@@ -2434,6 +2442,7 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
     SHD_HIP(hipStreamSynchronize(s));
     R.n_hosts = n_hosts;
     R.n_nodes = n_nodes;
+    if (ctx->comm) SHD_TRY(relay_shard_alloc(ctx));   // shd_relay_round_sharded at any rank count
     {   // v2 needs every path latency < 2^32 ns (max over the table)
         const uint64_t* tl = R.own_table ? R.lat.as<uint64_t>() : ctx->t_lat.as<uint64_t>();
         SHD_TRY(ctx->g_aux.ensure(8));
@@ -2551,6 +2560,7 @@ shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round
     out->min_deliver = dout.min_deliver;
     out->min_latency = dout.min_latency;
     out->n_sent = ns;
+    out->n_dst = H;
     return SHD_OK;
 }
 
@@ -2563,6 +2573,7 @@ shd_status shd_relay_round_sharded(shd_ctx* ctx, const shd_batch* d_batch, const
                                                      !d_batch->payload)))
         return SHD_ERR_INVALID;
     if (d_batch->n_packets && !d_out->status) return SHD_ERR_INVALID;
+    if (!ctx->relay.x_words.p || !ctx->relay.x_roff.p) return SHD_ERR_STATE;   // set up before the communicator
     SHD_HIP(hipSetDevice(ctx->device));
     return relay_round_sharded(ctx, d_batch, round, d_out);
 }
@@ -2577,29 +2588,6 @@ shd_status shd_relay_get_host_state(shd_ctx* ctx, uint64_t* rng_state, uint64_t*
     if (next_event_id)
         SHD_HIP(hipMemcpyAsync(next_event_id, R.next_id.p, (size_t)R.n_hosts * 8, hipMemcpyDeviceToHost, ctx->stream));
     SHD_HIP(hipStreamSynchronize(ctx->stream));
-    return SHD_OK;
-}
-
-shd_status shd_events_merge_device(shd_ctx* ctx, uint32_t n_runs, uint32_t n_dst,
-                                   const uint32_t* d_run_base, const uint32_t* d_run_off,
-                                   const uint64_t* d_deliver, const uint32_t* d_src,
-                                   const uint64_t* d_seq, const uint32_t* d_pkt,
-                                   uint64_t n_events, shd_relay_out* d_out) {
-    if (!ctx || n_runs == 0 || !d_run_base || !d_run_off || !d_out || !d_out->ev_off) return SHD_ERR_INVALID;
-    if (n_events && (!d_deliver || !d_src || !d_seq || !d_pkt || !d_out->ev_deliver ||
-                     !d_out->ev_src || !d_out->ev_seq || !d_out->ev_pkt))
-        return SHD_ERR_INVALID;
-    SHD_HIP(hipSetDevice(ctx->device));
-    hipStream_t s = ctx->stream;
-    merge_offsets<<<div_up((uint64_t)n_dst + 1, 256), 256, 0, s>>>(n_runs, n_dst, d_run_off, d_out->ev_off);
-    if (n_events)
-        merge_runs<<<div_up(n_events, 256), 256, 0, s>>>(n_runs, n_dst, d_run_base, d_run_off, d_deliver,
-                                                        d_src, d_seq, d_pkt, d_out->ev_off,
-                                                        d_out->ev_deliver, d_out->ev_src, d_out->ev_seq,
-                                                        d_out->ev_pkt);
-    SHD_HIP(hipGetLastError());
-    SHD_HIP(hipStreamSynchronize(s));
-    d_out->n_sent = n_events;
     return SHD_OK;
 }
 

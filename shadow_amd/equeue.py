@@ -33,9 +33,21 @@ class Popped:
 
 
 class EventQueues:
+    """``n_hosts`` = all hosts.  Under an engine communicator of > 1 ranks the queues hold this
+    rank's destination shard [lo, hi) (shd_shard_range), and every per-host array -- a batch's
+    ev_off, the popped ``off`` -- covers those hi - lo hosts (``self.n_local``)."""
+
     def __init__(self, engine, n_hosts: int):
         self.eng = engine
         self.n_hosts = int(n_hosts)
+        w, r = C.c_int32(0), C.c_int32(0)
+        N.check(engine.lib.shd_comm_info(engine.ctx, C.byref(w), C.byref(r)), "shd_comm_info")
+        lo, hi = C.c_uint32(0), C.c_uint32(self.n_hosts)
+        if w.value > 1:
+            N.check(engine.lib.shd_shard_range(self.n_hosts, w.value, r.value, C.byref(lo), C.byref(hi)),
+                    "shd_shard_range")
+        self.lo, self.hi = lo.value, hi.value
+        self.n_local = self.hi - self.lo
         N.check(engine.lib.shd_equeue_setup(engine.ctx, self.n_hosts), "shd_equeue_setup")
 
     def advance_device(self, d_batch: N.RelayOut | None, window_end: int) -> N.EqueueOut:
@@ -54,14 +66,14 @@ class EventQueues:
             dev = lambda a, np_dt, dt: torch.from_numpy(np.ascontiguousarray(a, np_dt).view(dt)).cuda()  # noqa: E731
             keep = [dev(ev_off, np.uint32, np.int32), dev(deliver, np.uint64, np.int64),
                     dev(src, np.uint32, np.int32), dev(seq, np.uint64, np.int64), dev(pkt, np.uint32, np.int32)]
-            batch = N.RelayOut(None, *(N.ptr(t).value for t in keep), 0, 0, n)
+            batch = N.RelayOut(None, *(N.ptr(t).value for t in keep), 0, 0, n, len(ev_off) - 1, 0)
         out = self.advance_device(batch, window_end)
         del keep
         return self.popped(out)
 
     def popped(self, out: N.EqueueOut) -> Popped:
         n = out.n_popped
-        off = np.zeros(self.n_hosts + 1, np.uint32)
+        off = np.zeros(self.n_local + 1, np.uint32)
         d = np.zeros(n, np.uint64); s = np.zeros(n, np.uint32)
         q = np.zeros(n, np.uint64); t = np.zeros(n, np.uint64)
         N.check(self.eng.lib.shd_equeue_copy_popped(self.eng.ctx, N.ptr(off), N.ptr(d), N.ptr(s), N.ptr(q),
@@ -73,7 +85,7 @@ class EventQueues:
         N.check(self.eng.lib.shd_equeue_pending(self.eng.ctx, None, None, None, None, None, C.byref(n)),
                 "shd_equeue_pending")
         k = n.value
-        off = np.zeros(self.n_hosts + 1, np.uint32)
+        off = np.zeros(self.n_local + 1, np.uint32)
         d = np.zeros(k, np.uint64); s = np.zeros(k, np.uint32)
         q = np.zeros(k, np.uint64); t = np.zeros(k, np.uint64)
         N.check(self.eng.lib.shd_equeue_pending(self.eng.ctx, N.ptr(off), N.ptr(d), N.ptr(s), N.ptr(q), N.ptr(t),

@@ -96,6 +96,31 @@ class Relay:
         return RoundResult(status, ev_off, ev_deliver[:ns], ev_src[:ns], ev_seq[:ns], ev_pkt[:ns],
                            out.min_deliver, out.min_latency, ns)
 
+    def device_buffers(self, n_packets: int):
+        """Device output tensors for ``round_device`` (torch, on the engine's GPU)."""
+        import torch
+        n = max(int(n_packets), 1)
+        return dict(status=torch.empty(n, dtype=torch.uint8, device="cuda"),
+                    ev_off=torch.empty(self.n_hosts + 1, dtype=torch.int32, device="cuda"),
+                    ev_deliver=torch.empty(n, dtype=torch.int64, device="cuda"),
+                    ev_src=torch.empty(n, dtype=torch.int32, device="cuda"),
+                    ev_seq=torch.empty(n, dtype=torch.int64, device="cuda"),
+                    ev_pkt=torch.empty(n, dtype=torch.int32, device="cuda"))
+
+    def round_device(self, d_off, d_time, d_dst, d_pay, round_end: int, sim_end: int, bootstrap_end: int,
+                     bufs) -> N.RelayOut:
+        """``shd_relay_round_device``: batch and outputs stay on the GPU (torch tensors); the
+        returned RelayOut holds the device pointers, n_sent and the reductions -- the form
+        ``EventQueues.advance_device`` takes."""
+        n = int(d_time.numel())
+        b = N.Batch(n, N.ptr(d_off).value, N.ptr(d_time).value, N.ptr(d_dst).value, N.ptr(d_pay).value, None)
+        out = N.RelayOut(*(N.ptr(bufs[k]).value for k in ("status", "ev_off", "ev_deliver", "ev_src", "ev_seq",
+                                                           "ev_pkt")), 0, 0, 0, 0, 0)
+        rd = N.Round(round_end, sim_end, bootstrap_end)
+        N.check(self.eng.lib.shd_relay_round_device(self.eng.ctx, C.byref(b), C.byref(rd), C.byref(out)),
+                "shd_relay_round_device")
+        return out
+
     def host_state(self):
         rng = np.zeros((self.n_hosts, 4), np.uint64)
         nid = np.zeros(self.n_hosts, np.uint64)

@@ -214,3 +214,82 @@ def test_rccl_world_one(engine):
         assert np.array_equal(ls.cpu().numpy().view(np.uint32), loss.view(np.uint32))
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("dynamic", [True, False])
+def test_local_two_ranks_relay_into_queues_with_window(engine, dynamic):
+    """The north star's relay path at N = 2 through the C ABI alone, round after round: each rank's
+    sharded relay output (its destination shard) goes into its own device queues
+    (shd_equeue_setup under the communicator), the next window comes from shd_round_window (the
+    runahead updated by every round's min latency, the minimum over both ranks' queues), and each
+    rank pops its hosts' events below that window.  Compared per round with one process:
+    the C restatement's relay into persistent per-host heaps, Runahead and the controller's window
+    (manager.rs:404-464, runahead.rs:43-115, controller.rs:86-111)."""
+    import torch
+    from oracle.relay import RunaheadState, next_window
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd.equeue import EventQueues
+    from shadow_amd.rounds import Runahead, next_window as eng_window
+    from shadow_amd.routing import Engine
+    H, NN, P = 4000, 40, 200_000
+    _, lat, loss, host_node, rng0 = _case(H, NN, 11)
+    engines = [Engine(0), Engine(0)]
+    try:
+        D.comm_init_local(engines)
+        rels = [D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss) for e in engines]
+        queues = [EventQueues(e, H) for e in engines]
+        assert [(q.lo, q.hi) for q in queues] == [(r.lo, r.hi) for r in rels]
+        min_possible = int(lat.min())
+        cfg = 2 * 10**6 if not dynamic else None
+        for e in engines:
+            Runahead(e, dynamic, min_possible, cfg)
+        ora = RunaheadState(dynamic, min_possible, cfg)
+        oq = corc.EventQueues(H)
+        orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+        end_time = 10**9 + 400 * 10**6
+        ws, we = 10**9, 10**9 + ora.get()
+        for rnd in range(5):
+            b = synth.packet_batch(H, P, ws, we, seed=120 + rnd)
+            rd = (we, end_time, 0)
+            o = corc.relay_round_eq(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, orng, onid,
+                                    *rd, queues=oq, batch_no=rnd)
+            if o["min_latency"] != 2**64 - 1:
+                ora.update_lowest_used_latency(o["min_latency"])
+            want_win = next_window(min(oq.pop(0, want=False)["next_time"], 2**64 - 1), ora.get(), end_time)
+            parts = [_slice_batch(b, r.lo, r.hi) for r in rels]
+
+            def rank_round(i):
+                r, p, e = rels[i], parts[i], engines[i]
+                d = [_dev(p[0], np.int32), _dev(p[1], np.int64), _dev(p[2], np.int32), _dev(p[3], np.int32)]
+                st = torch.empty(max(len(p[1]), 1), dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                out = r.round_device(*d, rd, st)
+                win = eng_window(e, None, end_time)
+                qo = queues[i].advance_device(out, win[1] if win else 2**63)
+                return win, queues[i].popped(qo)
+            res = _run_ranks([lambda i=i: rank_round(i) for i in range(2)])
+            assert res[0][0] == res[1][0] == want_win, (rnd, res[0][0], want_win)
+            op = oq.pop(want_win[1])
+            for (win, p), q in zip(res, queues):
+                a, z = int(op["off"][q.lo]), int(op["off"][q.hi])
+                assert np.array_equal(p.off.astype(np.int64), op["off"][q.lo:q.hi + 1].astype(np.int64) - a)
+                assert np.array_equal(p.deliver, op["deliver"][a:z])
+                assert np.array_equal(p.src, op["src"][a:z])
+                assert np.array_equal(p.seq, op["seq"][a:z])
+                # tag: batch << 32 | the packet's index in its SENDER rank's batch
+                base = np.array([parts[0][4], parts[1][4]], np.int64)
+                sender = (p.src >= rels[1].lo).astype(np.int64)
+                glob = (p.tag & np.uint64(0xFFFFFFFF)).astype(np.int64) + base[sender]
+                assert np.array_equal(glob, (op["tag"][a:z] & np.uint64(0xFFFFFFFF)).astype(np.int64))
+                assert np.array_equal(p.tag >> np.uint64(32), op["tag"][a:z] >> np.uint64(32))
+            assert sum(p.n_pending for _, p in res) == op["n_pending"]
+            ws, we = want_win
+    finally:
+        for e in engines:
+            e.close()
+
+
+def _dev(a, dt):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()

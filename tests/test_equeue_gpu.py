@@ -124,3 +124,58 @@ def test_run_compaction_and_pending_vs_oracle(engine):
                 assert got == sorted(oq.q[h]), h
         start += win
     assert p.n_pending > 0
+
+
+def _cmp_popped(p, op):
+    assert p.n_pending == op["n_pending"] and p.next_time == op["next_time"]
+    assert np.array_equal(p.off, op["off"])
+    assert np.array_equal(p.deliver, op["deliver"])
+    assert np.array_equal(p.src, op["src"])
+    assert np.array_equal(p.seq, op["seq"])
+    assert np.array_equal(p.tag, op["tag"])
+
+
+def test_c5_scale_rounds_vs_c_queues(engine):
+    """BASELINE config 5 at full size: 100k hosts x 10M packets per round on the C2 table (1-300
+    ms paths), 1 ms windows for 4 rounds -- the queues then hold ~40M pending events in up to 5
+    runs -- and a drain in two windows.  Every popped event of every host, the pending count and
+    the next event time are compared with the C restatement of the per-host EventQueues
+    (oracle/c/equeue.c: push_packet_to_host into each destination's heap during the relay round,
+    then the pop loop of Host::execute, host.rs:697-706)."""
+    from shadow_amd import synth
+    from shadow_amd.equeue import EventQueues
+    from shadow_amd.relay import Relay
+    import torch
+    H, P = 100_000, 10_000_000
+    el = synth.complete_graph(1000, 1)
+    used = np.arange(1000, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(1000, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    host_node = synth.c5_host_nodes(H, 1000)
+    rng0 = synth.host_rng_states(H, 1)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    q = EventQueues(engine, H)
+    oq = corc.EventQueues(H)
+    orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+    bufs = rl.device_buffers(P)
+    start, win, end = synth.SIM_START + 10**9, 10**6, synth.SIM_START + 10**12
+    dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()  # noqa: E731
+    for rnd in range(4):
+        b = synth.packet_batch(H, P, start, start + win, seed=140 + rnd)
+        d = [dev(b.src_off, np.int32), dev(b.send_time, np.int64), dev(b.dst_host, np.int32),
+             dev(b.payload, np.int32)]
+        torch.cuda.synchronize()
+        out = rl.round_device(*d, start + win, end, 0, bufs)
+        o = corc.relay_round_eq(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, orng, onid,
+                                start + win, end, 0, queues=oq, batch_no=rnd, threads=corc.max_threads())
+        assert out.n_sent == o["n_sent"] and out.min_deliver == o["min_deliver"]
+        p = q.popped(q.advance_device(out, start + 2 * win))
+        op = oq.pop(start + 2 * win, threads=corc.max_threads())
+        _cmp_popped(p, op)
+        assert p.n_pending > 10_000_000 * rnd
+        start += win
+        del d
+    for w_end in (start + 100 * win, 2**63):
+        p = q.popped(q.advance_device(None, w_end))
+        _cmp_popped(p, oq.pop(w_end, threads=corc.max_threads()))
+    assert p.n_pending == 0

@@ -136,6 +136,29 @@ def test_resident_table_lookups(engine):
     assert engine.smallest_latency_ns() == int(lat.min())
     st = engine.lib.shd_routing_lookup(engine.ctx, 700, 0, C.byref(C.c_uint64()), C.byref(C.c_float()))
     assert st == 5   # out of range: SHD_ERR_INVALID
+    # batched: 100k pairs in one gather
+    rows = rng.integers(0, 700, 100_000).astype(np.uint32)
+    cols = rng.integers(0, 700, 100_000).astype(np.uint32)
+    bl, bp = np.zeros(100_000, np.uint64), np.zeros(100_000, np.float32)
+    N.check(engine.lib.shd_routing_lookup_batch(engine.ctx, 100_000, N.ptr(rows), N.ptr(cols), N.ptr(bl), N.ptr(bp)),
+            "lookup_batch")
+    assert np.array_equal(bl, lat[rows, cols]) and np.array_equal(bp.view(np.uint32), loss[rows, cols].view(np.uint32))
+    # the host mirror: single lookups are host reads, identical answers
+    N.check(engine.lib.shd_routing_mirror(engine.ctx, 1), "mirror")
+    for k in range(0, 100_000, 997):
+        lv, pv = C.c_uint64(0), C.c_float(0)
+        N.check(engine.lib.shd_routing_lookup(engine.ctx, int(rows[k]), int(cols[k]), C.byref(lv), C.byref(pv)),
+                "lookup")
+        assert lv.value == int(bl[k]) and np.float32(pv.value).view(np.uint32) == bp[k].view(np.uint32)
+    bl2 = np.zeros(100_000, np.uint64)
+    N.check(engine.lib.shd_routing_lookup_batch(engine.ctx, 100_000, N.ptr(rows), N.ptr(cols), N.ptr(bl2), None),
+            "lookup_batch (mirror)")
+    assert np.array_equal(bl2, bl)
+    # a new build drops the mirror with the resident table it copied
+    g.compute_shortest_paths(used, engine)
+    N.check(engine.lib.shd_routing_lookup(engine.ctx, 3, 4, C.byref(lv), C.byref(pv)), "lookup")
+    assert lv.value == int(lat[3, 4])
+    N.check(engine.lib.shd_routing_mirror(engine.ctx, 0), "mirror off")
 
 
 def test_kernel_timing_sampling(engine):
