@@ -495,10 +495,20 @@ def cpu_baseline_relay(rl, lat_table, loss_table, budget_s=8.0):
                        f"mutex + binary-heap push, OpenMP over source hosts)")
 
 
-def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4):
-    """a14: the relay round plus the merge of its events into the device-resident destination
-    queues and the pop of the next window (shd_equeue_advance), round after round on C5 (1 ms
-    windows, 1-300 ms paths: events stay pending for many rounds)."""
+EQ_BYTES_BATCH = 24    # a batch event read once (deliver 8, src 4, seq 8, packet 4)
+EQ_BYTES_KEPT = 28     # a batch event written once: to its new run or to the popped output (deliver, src, seq, tag)
+EQ_BYTES_POPPED = 56   # an older run's popped event read and written to the output
+
+
+def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4, cpu=False):
+    """The north star's whole relay path, round after round on C5 (1 ms windows, 1-300 ms paths:
+    events stay pending for many rounds): the relay round, then shd_equeue_advance -- the merge of
+    its events into the device-resident destination queues and the pop of the next window.
+    Roofline bytes = the relay's SURVEY 8(d) bytes + the merge's (24 B per batch event read, 28 B
+    per kept event written, 56 B per popped event read + written).  CPU baseline: the C
+    restatement doing the same rounds -- send_packet with push_packet_to_host into persistent
+    per-host heaps, then every host's pop loop below the window (oracle/c/equeue.c) -- and the last
+    round's popped events compared with the GPU's."""
     import torch
     from shadow_amd import _native as N
     H, P = rl["H"], rl["P"]
@@ -511,19 +521,21 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4):
     ev = [torch.empty(H + 1, dtype=torch.int32, device="cuda"), torch.empty(P, dtype=torch.int64, device="cuda"),
           torch.empty(P, dtype=torch.int32, device="cuda"), torch.empty(P, dtype=torch.int64, device="cuda"),
           torch.empty(P, dtype=torch.int32, device="cuda")]
-    out = N.RelayOut(N.ptr(st).value, *(N.ptr(t).value for t in ev), 0, 0, 0)
+    out = N.RelayOut(N.ptr(st).value, *(N.ptr(t).value for t in ev), 0, 0, 0, 0, 0)
     qo = N.EqueueOut()
-    start = rl["start"]
+    start0 = start = rl["start"]
     t_relay = t_adv = 0.0
-    pops = pend = 0
+    pops = pend = bytes_merge = n_sent_t = 0
     b = rl["batch"]
     d = [_dev(b.src_off, np.int32), _dev(b.send_time, np.int64), _dev(b.dst_host, np.int32),
          _dev(b.payload, np.int32)]
     t_base = d[1].clone()
+    end = start + 10**12
+    last = None
     for k in range(rounds):
         d[1].copy_(t_base + k * 10**6)   # the same sends, one window later each round
         batch = N.Batch(P, *(N.ptr(t).value for t in d), None)
-        rnd = N.Round(start + 10**6, start + 10**12, 0)
+        rnd = N.Round(start + 10**6, end, 0)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         N.check(eng.lib.shd_relay_round_device(eng.ctx, C.byref(batch), C.byref(rnd), C.byref(out)), "relay")
@@ -535,11 +547,63 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4):
             t_adv += t2 - t1
             pops += qo.n_popped
             pend += qo.n_pending
+            n_sent_t += out.n_sent
+            # every batch event is read once and written once (to its new run, or popped); popped
+            # events of older runs are read and written; at most min(n_sent, n_popped) popped
+            # events came from the batch, so this is a lower bound
+            bytes_merge += (EQ_BYTES_BATCH + EQ_BYTES_KEPT) * out.n_sent + \
+                EQ_BYTES_POPPED * max(0, qo.n_popped - out.n_sent)
         start += 10**6
-    return {"workload": "C5 rounds: relay + shd_equeue_advance (merge into the pending destination queues, pop "
-                        "the next 1 ms window)", "rounds": rounds, "timed_rounds": timed,
-            "relay_ms_per_round": t_relay / timed * 1e3, "advance_ms_per_round": t_adv / timed * 1e3,
-            "popped_per_round": pops / timed, "pending_mean": pend / timed}
+        if k == rounds - 1:
+            n = qo.n_popped
+            last = dict(off=np.zeros(H + 1, np.uint32), deliver=np.zeros(n, np.uint64), src=np.zeros(n, np.uint32),
+                        seq=np.zeros(n, np.uint64), tag=np.zeros(n, np.uint64), n_pending=qo.n_pending,
+                        next_time=qo.next_time)
+            N.check(eng.lib.shd_equeue_copy_popped(eng.ctx, *(N.ptr(last[x]) for x in ("off", "deliver", "src", "seq",
+                                                                                        "tag"))), "copy_popped")
+    ms = (t_relay + t_adv) / timed * 1e3
+    relay_bytes = RELAY_BYTES_PER_PACKET * P + RELAY_BYTES_PER_HOST * H
+    algo = relay_bytes + bytes_merge / timed
+    ach = algo / (ms * 1e-3) / 1e9
+    res = {"workload": "C5 rounds: relay + shd_equeue_advance (merge into the pending destination queues, pop "
+                       "the next 1 ms window)", "rounds": rounds, "timed_rounds": timed,
+           "relay_ms_per_round": t_relay / timed * 1e3, "advance_ms_per_round": t_adv / timed * 1e3,
+           "ms_per_round": ms, "value": P / (ms * 1e-3), "unit": "packets relayed + merged/s",
+           "popped_per_round": pops / timed, "pending_mean": pend / timed,
+           "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ach / HBM_PEAK_GBS, "bytes_per_round": algo,
+                        "work": "relay 84 B/packet + 80 B/host (SURVEY 8(d)) + merge 52 B per batch event (read "
+                                "24, written 28) + 56 B per popped event of an older run (lower bound)"}}
+    if cpu:
+        from oracle import corc
+        threads = corc.max_threads()
+        oq = corc.EventQueues(H)
+        rng, nid = rl["rng0"].copy(), np.zeros(H, np.uint64)
+        start = start0
+        tb = b.send_time.copy()
+        t_cpu = 0.0
+        for k in range(rounds):
+            times = tb + np.uint64(k * 10**6)
+            t0 = time.perf_counter()
+            corc.relay_round_eq(b.src_off, times, b.dst_host, b.payload, rl["host_node"], lat_table, loss_table, rng,
+                                nid, start + 10**6, end, 0, queues=oq, batch_no=k, threads=threads)
+            o = oq.pop(start + 2 * 10**6, threads=threads, want=k == rounds - 1)
+            dt = time.perf_counter() - t0
+            if k >= rounds - timed:
+                t_cpu += dt
+            if k == rounds - 1:
+                op = o
+            start += 10**6
+        cms = t_cpu / timed * 1e3
+        same = last is not None and all(np.array_equal(last[x], op[x]) for x in ("off", "deliver", "src", "seq", "tag")) \
+            and (last["n_pending"], last["next_time"]) == (op["n_pending"], op["next_time"])
+        res["cpu_baseline"] = {"value": P / (cms * 1e-3), "unit": "packets relayed + merged/s", "cores": threads,
+                               "kind": "port", "ms_per_round": cms,
+                               "sample": f"the same {rounds} C5 rounds through oracle/c (send_packet + "
+                                         f"push_packet_to_host into per-host binary heaps under per-destination "
+                                         f"mutexes, then every host's pop loop), last {timed} timed",
+                               "bit_exact_vs_gpu": bool(same)}
+    return res
 
 
 def codel_leg(eng, steps=5, cpu=True):
@@ -747,7 +811,7 @@ def main():
             rel["cpu_baseline"] = cpu_baseline_relay(rl, r["lat"], r["loss"])
             rel["cpu_baseline"]["bit_exact_vs_gpu"] = rel["bit_exact_vs_cpu"]
         if world == 1 and not args.no_equeue:
-            rel["equeue"] = equeue_leg(eng, rl, r["lat"], r["loss"])
+            rel["equeue"] = equeue_leg(eng, rl, r["lat"], r["loss"], cpu=cpu)
         res["relay"] = rel
     if world == 1 and not args.no_c3:
         res["c3"] = c3_leg(eng, cpu=cpu)

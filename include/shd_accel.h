@@ -249,10 +249,12 @@ typedef struct shd_relay_out {
     uint64_t min_deliver;
     uint64_t min_latency;
     uint64_t n_sent;
-    uint32_t n_dst;      /* destination hosts ev_off covers (ev_off has n_dst + 1 entries): written by
-                            the relay calls; a caller building this struct for shd_equeue_advance
-                            sets it (the queues check it against their host count) */
-    uint32_t reserved;
+    uint32_t n_dst;      /* destination hosts ev_off covers (ev_off has n_dst + 1 entries) */
+    uint32_t n_events;   /* events in ev_* (= ev_off[n_dst]): n_sent on one GPU; a sharded round's
+                            n_sent is the all-rank total, n_events what this rank received.  Both
+                            are written by the relay calls; a caller building this struct for
+                            shd_equeue_advance sets them (the queues check n_dst against their
+                            host count and merge n_events events) */
 } shd_relay_out;
 
 shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round* round,

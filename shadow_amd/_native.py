@@ -80,7 +80,7 @@ class RelayOut(C.Structure):
     _fields_ = [("status", C.c_void_p), ("ev_off", C.c_void_p), ("ev_deliver", C.c_void_p),
                 ("ev_src", C.c_void_p), ("ev_seq", C.c_void_p), ("ev_pkt", C.c_void_p),
                 ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64),
-                ("n_dst", C.c_uint32), ("reserved", C.c_uint32)]
+                ("n_dst", C.c_uint32), ("n_events", C.c_uint32)]
 
 
 class EqueueOut(C.Structure):

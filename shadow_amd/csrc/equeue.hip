@@ -666,8 +666,8 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     EqState& Q = ctx->eq;
     if (!Q.ready) return SHD_ERR_STATE;
     const bool has_b = d_batch != nullptr;
-    if (has_b && (!d_batch->ev_off || (d_batch->n_sent && (!d_batch->ev_deliver || !d_batch->ev_src ||
-                                                          !d_batch->ev_seq || !d_batch->ev_pkt))))
+    if (has_b && (!d_batch->ev_off || (d_batch->n_events && (!d_batch->ev_deliver || !d_batch->ev_src ||
+                                                            !d_batch->ev_seq || !d_batch->ev_pkt))))
         return SHD_ERR_INVALID;
     if (has_b && Q.batches >= 0xFFFFFFFFull) return SHD_ERR_INVALID;   // tag bits exhausted
     // the batch must cover exactly these queues' hosts (ev_off has n_dst + 1 entries): a sharded
@@ -676,7 +676,7 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     if (has_b && d_batch->n_dst != Q.n_hosts) return SHD_ERR_INVALID;
     SHD_HIP(hipSetDevice(ctx->device));
     const uint32_t H = Q.n_hosts;
-    const uint64_t n_b = has_b ? d_batch->n_sent : 0;
+    const uint64_t n_b = has_b ? d_batch->n_events : 0;   // this context's events (a sharded round: received)
     const uint64_t n_in = Q.n_pending + n_b;
     if (n_in >= 0xFFFFFFFFull) return SHD_ERR_INVALID;   // 32-bit positions
     int live = 0;
@@ -711,7 +711,7 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     uint64_t left = 0;
     for (uint32_t k = 0; k < S.n; ++k) left += wd[4 + k];
     if (n_pop + left != n_in || (has_b && wd[4 + S.b] != n_keep))
-        return SHD_ERR_INVALID;   // batch ev_off / n_sent disagree
+        return SHD_ERR_INVALID;   // batch ev_off / n_events disagree
     // commit: cursors moved to the cut buffer; drained runs dropped; the batch's remainder is a run
     for (uint32_t k = 0; k < n_runs; ++k) {
         EqRunBuf& R = Q.run[slots[k]];

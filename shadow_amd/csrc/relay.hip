@@ -2116,6 +2116,7 @@ static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round
     SHD_TRY(relay_run(ctx, b, rd, o));
     SHD_TRY(relay_commit(ctx, o));
     o->n_dst = ctx->relay.n_hosts;
+    o->n_events = (uint32_t)o->n_sent;
     round_note(ctx, o->min_deliver, o->min_latency);
     return SHD_OK;
 }
@@ -2374,6 +2375,7 @@ static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const sh
     d_out->min_latency = ml;
     d_out->n_sent = ns;
     d_out->n_dst = n_own;
+    d_out->n_events = (uint32_t)n_recv;
     round_note(ctx, md, ml);
     R.last_recv = n_recv;
     return SHD_OK;
@@ -2561,6 +2563,7 @@ shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round
     out->min_latency = dout.min_latency;
     out->n_sent = ns;
     out->n_dst = H;
+    out->n_events = (uint32_t)ns;
     return SHD_OK;
 }
 

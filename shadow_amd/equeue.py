@@ -66,7 +66,7 @@ class EventQueues:
             dev = lambda a, np_dt, dt: torch.from_numpy(np.ascontiguousarray(a, np_dt).view(dt)).cuda()  # noqa: E731
             keep = [dev(ev_off, np.uint32, np.int32), dev(deliver, np.uint64, np.int64),
                     dev(src, np.uint32, np.int32), dev(seq, np.uint64, np.int64), dev(pkt, np.uint32, np.int32)]
-            batch = N.RelayOut(None, *(N.ptr(t).value for t in keep), 0, 0, n, len(ev_off) - 1, 0)
+            batch = N.RelayOut(None, *(N.ptr(t).value for t in keep), 0, 0, n, len(ev_off) - 1, n)
         out = self.advance_device(batch, window_end)
         del keep
         return self.popped(out)

@@ -275,10 +275,11 @@ class IpAssignmentError(Exception):
     (sim_config.rs:407-409)."""
 
 
-def assign_ips(node_gml_ids, ips=None):
+def assign_ips(node_gml_ids, ips=None, host_names=None):
     """``assign_ips`` (sim_config.rs:399-420) over ``IpAssignment`` (graph/mod.rs:354-422), in the
     native host code (``shd_assign_ips``).  ``node_gml_ids[h]`` is host h's network node id (hosts
-    in HostId order), ``ips[h]`` its configured IPv4 address as an int (0 / None = none).
+    in HostId order), ``ips[h]`` its configured IPv4 address as an int (0 / None = none),
+    ``host_names[h]`` its name (for the error context; the host's index when absent).
     Returns (ip per host, used node ids ascending = IpAssignment::get_nodes, each host's column
     in that list = the relay's host -> node map)."""
     lib = N.load()
@@ -295,8 +296,11 @@ def assign_ips(node_gml_ids, ips=None):
     if st == 5 and ip_in is not None and n:
         h = bad.value
         ip = ip_in[h]
+        name = host_names[h] if host_names is not None else str(h)
+        # anyhow context over IpPreviouslyAssignedError ("{:#}"): the reference's two messages
         raise IpAssignmentError(f"Failed to assign IP address {ip >> 24}.{(ip >> 16) & 255}.{(ip >> 8) & 255}."
-                                f"{ip & 255} for host {h} to node '{ids[h]}': IP address has already been assigned")
+                                f"{ip & 255} for host '{name}' to node '{ids[h]}': IP address has already been "
+                                f"assigned")
     N.check(st, "shd_assign_ips")
     return ip_out, used[:n_used.value].copy(), col[:n].copy()
 

@@ -249,6 +249,7 @@ def test_local_two_ranks_relay_into_queues_with_window(engine, dynamic):
         orng, onid = rng0.copy(), np.zeros(H, np.uint64)
         end_time = 10**9 + 400 * 10**6
         ws, we = 10**9, 10**9 + ora.get()
+        bases = np.zeros((5, 2), np.int64)   # per round: each sender rank's batch base in the whole batch
         for rnd in range(5):
             b = synth.packet_batch(H, P, ws, we, seed=120 + rnd)
             rd = (we, end_time, 0)
@@ -258,6 +259,7 @@ def test_local_two_ranks_relay_into_queues_with_window(engine, dynamic):
                 ora.update_lowest_used_latency(o["min_latency"])
             want_win = next_window(min(oq.pop(0, want=False)["next_time"], 2**64 - 1), ora.get(), end_time)
             parts = [_slice_batch(b, r.lo, r.hi) for r in rels]
+            bases[rnd] = [parts[0][4], parts[1][4]]
 
             def rank_round(i):
                 r, p, e = rels[i], parts[i], engines[i]
@@ -277,10 +279,10 @@ def test_local_two_ranks_relay_into_queues_with_window(engine, dynamic):
                 assert np.array_equal(p.deliver, op["deliver"][a:z])
                 assert np.array_equal(p.src, op["src"][a:z])
                 assert np.array_equal(p.seq, op["seq"][a:z])
-                # tag: batch << 32 | the packet's index in its SENDER rank's batch
-                base = np.array([parts[0][4], parts[1][4]], np.int64)
+                # tag: batch << 32 | the packet's index in its SENDER rank's batch of that round
                 sender = (p.src >= rels[1].lo).astype(np.int64)
-                glob = (p.tag & np.uint64(0xFFFFFFFF)).astype(np.int64) + base[sender]
+                batch = (p.tag >> np.uint64(32)).astype(np.int64)
+                glob = (p.tag & np.uint64(0xFFFFFFFF)).astype(np.int64) + bases[batch, sender]
                 assert np.array_equal(glob, (op["tag"][a:z] & np.uint64(0xFFFFFFFF)).astype(np.int64))
                 assert np.array_equal(p.tag >> np.uint64(32), op["tag"][a:z] >> np.uint64(32))
             assert sum(p.n_pending for _, p in res) == op["n_pending"]

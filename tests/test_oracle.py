@@ -342,6 +342,13 @@ def test_native_assign_ips_matches_ip_assignment(seed):
     if dup is not None:
         with pytest.raises(IpAssignmentError, match="already been assigned"):
             assign_ips(ids, ips)
+        ip = ips[dup]
+        names = [f"host{h}" for h in range(n)]
+        want_msg = (f"Failed to assign IP address 11.{(ip >> 16) & 255}.{(ip >> 8) & 255}.{ip & 255} for host "
+                    f"'host{dup}' to node '{ids[dup]}': IP address has already been assigned")
+        with pytest.raises(IpAssignmentError) as e:   # sim_config.rs:407-409 context + graph/mod.rs:349
+            assign_ips(ids, ips, host_names=names)
+        assert str(e.value) == want_msg
         return
     for h in range(n):
         if not ips[h]:
