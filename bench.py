@@ -85,6 +85,23 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
+def all_ranks_ok(ok, world):
+    """True iff every rank's check passed (MIN over the ranks)."""
+    if world == 1:
+        return bool(ok)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def table_checksum(lat, loss):
+    """Order-sensitive 64-bit checksum of a (lat u64, loss f32) table (host arrays)."""
+    w = np.arange(1, lat.size + 1, dtype=np.uint64).reshape(lat.shape)
+    return int(((lat * w).sum(dtype=np.uint64) ^ (loss.view(np.uint32).astype(np.uint64) * w).sum(dtype=np.uint64)))
+
+
 def load_pmc(name):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(p):
@@ -322,6 +339,18 @@ def c4_leg(eng, world, rank, steps, gather=True, cpu=True):
                sssp_kernel_ms_per_rank=kernel_ms, value=n * n / (r["ms_per_step"] * 1e-3),
                unit="node-pairs/s", scaling="strong", all_gather=bool(gather),
                roofline=sssp_roofline(r["rows"], arcs, n, kernel_ms))
+    if world > 1:   # the rank holding the last 64 rows (claimed rows of its slots) checks them
+        from oracle import corc
+        lo = n - 64
+        lat, loss = r["lat_dev"], r["loss_dev"]
+        ok = True
+        if rank == (0 if gather else world - 1):
+            at = lo if gather else lo - r["rb"]
+            code, clat, closs, _ = corc.routing(el.n_nodes, el.src, el.dst, el.latency_ns, el.packet_loss, el.directed,
+                                                np.arange(n, dtype=np.uint32), rows=(lo, n), threads=corc.max_threads())
+            ok = code == "OK" and np.array_equal(clat, lat[at:at + 64].cpu().numpy().view(np.uint64)) and \
+                np.array_equal(closs.view(np.uint32), loss[at:at + 64].cpu().numpy().view(np.uint32))
+        out["check"] = all_ranks_ok(ok, world)
     if cpu and rank == 0 and world == 1:
         # the LAST 64 rows: the persistent kernel's slots take every row past the grid (the first
         # 2 x n_cu rows) from the row counter, so these are claimed rows, not a slot's first row
@@ -410,6 +439,35 @@ def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=F
     N.check(eng.lib.shd_relay_last_pipeline(eng.ctx, C.byref(pipe)), "last_pipeline")
     return dict(H=H, P=P, dt=dt, ms_per_step=dt / steps * 1e3, n_sent=int(n_sent), batch=b,
                 pipeline=int(pipe.value), host_node=host_node, rng0=rng0, start=start, rd=rd)
+
+
+def relay_check_sharded(eng, world, rank, rl, lat_table, loss_table):
+    """N > 1: one sharded round from the setup state, every rank's statuses and destination events
+    against the C restatement of the whole round (the RCCL exchange's own test at this size)."""
+    import torch
+    from oracle import corc
+    from shadow_amd import dist as D
+    b, H = rl["batch"], rl["H"]
+    rel = D.ShardedRelay(eng, rl["host_node"], rl["rng0"], np.zeros(H, np.uint64), lat_table, loss_table)
+    lo, hi = rel.lo, rel.hi
+    a, e = int(b.src_off[lo]), int(b.src_off[hi])
+    status, ev, md, ml, ns = rel.round((b.src_off[lo:hi + 1] - b.src_off[lo]).astype(np.uint32), b.send_time[a:e],
+                                       b.dst_host[a:e], b.payload[a:e], rl["rd"])
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, rl["host_node"], lat_table, loss_table,
+                         rl["rng0"].copy(), np.zeros(H, np.uint64), *rl["rd"], threads=corc.max_threads())
+    oe = o["events"]
+    s0, s1 = int(oe["off"][lo]), int(oe["off"][hi])
+    bounds = [D.shard_range(H, world, q) for q in range(world)]
+    base = np.array([int(b.src_off[x]) for x, _ in bounds], np.int64)
+    sender = np.searchsorted(np.array([y for _, y in bounds]), ev["src"], side="right")
+    ok = (np.array_equal(status, o["status"][a:e]) and
+          np.array_equal(ev["off"].astype(np.int64), oe["off"][lo:hi + 1].astype(np.int64) - s0) and
+          all(np.array_equal(ev[k], oe[k][s0:s1]) for k in ("deliver", "src", "seq")) and
+          np.array_equal(ev["pkt"].astype(np.int64) + base[sender], oe["pkt"][s0:s1].astype(np.int64)) and
+          (md, ml, ns) == (o["min_deliver"], o["min_latency"], o["n_sent"]))
+    del rel
+    torch.cuda.empty_cache()
+    return all_ranks_ok(ok, world)
 
 
 def relay_check_and_e2e(eng, rl, lat_table, loss_table, reps=3):
@@ -772,6 +830,15 @@ def main():
         cb, lat_cpu = cpu_baseline_routing(r["el"])
         cb["bit_exact_vs_gpu"] = bool(np.array_equal(lat_cpu, r["lat"]))
         res["cpu_baseline"] = cb
+    checks = {}
+    if world > 1:   # the multi-GPU run checks itself: every rank's whole table against the C restatement
+        from oracle import corc
+        el = r["el"]
+        code, olat, oloss, _ = corc.routing(el.n_nodes, el.src, el.dst, el.latency_ns, el.packet_loss, el.directed,
+                                            np.arange(el.n_nodes, dtype=np.uint32), threads=corc.max_threads())
+        checks["c2_table_bit_exact_all_ranks"] = all_ranks_ok(
+            code == "OK" and np.array_equal(r["lat"], olat) and
+            np.array_equal(r["loss"].view(np.uint32), oloss.view(np.uint32)), world)
     if world == 1 and not args.no_e2e:
         res["routing_e2e"] = routing_e2e(eng, r["el"])
         res["c2_engines"] = c2_engines(eng, r["el"])
@@ -812,11 +879,17 @@ def main():
             rel["cpu_baseline"]["bit_exact_vs_gpu"] = rel["bit_exact_vs_cpu"]
         if world == 1 and not args.no_equeue:
             rel["equeue"] = equeue_leg(eng, rl, r["lat"], r["loss"], cpu=cpu)
+        if world > 1:
+            checks["relay_round_bit_exact_all_ranks"] = relay_check_sharded(eng, world, rank, rl, r["lat"], r["loss"])
         res["relay"] = rel
     if world == 1 and not args.no_c3:
         res["c3"] = c3_leg(eng, cpu=cpu)
     if not args.no_c4:
         res["c4"] = c4_leg(eng, world, rank, args.c4_steps, gather=not args.c4_no_gather, cpu=cpu)
+        if "check" in res["c4"]:
+            checks["c4_last_rows_bit_exact"] = res["c4"].pop("check")
+    if checks:
+        res["parity_check"] = checks
     if world == 1 and not args.no_codel:
         res["codel"] = codel_leg(eng, cpu=cpu)
     if world == 1 and not args.no_tbucket:
