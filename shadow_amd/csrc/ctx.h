@@ -42,6 +42,11 @@ struct DevBuf {
     }
 };
 
+struct ScanScratch {   // look-back states of the hand-written scans (scan.h)
+    DevBuf state;       // [tiles][2] u64
+    uint32_t epoch = 0;
+};
+
 struct CodelState {   // CoDel router queues (codel.hip)
     DevBuf st, flags, ring, status;
     uint32_t n_hosts = 0, cap = 0;
@@ -61,14 +66,14 @@ struct EqState {   // destination event queues (equeue.hip): a list of sorted ru
     DevBuf curs[2];                 // [kEqMaxRuns + 1][n_hosts] u32 cursors (first unpopped), double-buffered
     DevBuf bcut;                    // [n_hosts] the batch's first kept event per host
     DevBuf pd, ps, pq, pt;          // the last call's popped events
-    DevBuf pop_cnt, keep_cnt, pop_off, next, left, scan_tmp;
+    DevBuf pop_cnt, keep_cnt, pop_off, next, left;
     DevBuf ranges;                  // [n_hosts][kEqMaxRuns + 1] (cursor, cut) pairs of the last count
     int ccur = 0;
     uint32_t n_hosts = 0;           // queues held here: all hosts, or a sharded rank's [host_lo, host_lo + n_hosts)
     uint32_t host_lo = 0, n_total = 0;
     uint64_t n_pending = 0, n_popped = 0, batches = 0;
     uint64_t head = ~0ull;          // earliest pending deliver time after the last advance (local)
-    uint32_t scan_epoch = 0;        // eq_scan2's look-back state epoch
+    ScanScratch scan;               // the advance's look-back scans (scan.h)
     bool ready = false;
 };
 
@@ -114,8 +119,11 @@ struct RelayState {
         counts_round;
     // per-round scratch
     DevBuf pk_off, pk_time, pk_dst, pk_pay, pk_chance, st, ev_key, ev_key2, ev_val, ev_val2,
-        ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, scan_tmp, red, rec, brec, tmp, draws,
+        ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, red, rec, brec, tmp, draws,
         bin_cnt, bin_base, bin_lb;
+    ScanScratch scan;     // pipeline 1's destination offsets (scan.h)
+    DevBuf rs_counts;     // pipeline 3's radix sort: per-tile digit counts
+    ScanScratch rs_scan;
     // sharded rounds: packed outgoing events, exchange words, per-peer offset blocks, what was
     // received, and the merged events of this rank's destinations (engine-owned outputs)
     DevBuf x_rec, x_words, x_off, x_roff, x_rrec, m_off, m_deliver, m_src, m_seq, m_pkt;

@@ -24,7 +24,7 @@
 #include <algorithm>
 #include <cstring>
 
-#include "ctx.h"
+#include "scan.h"
 
 namespace shd {
 
@@ -380,147 +380,6 @@ __global__ __launch_bounds__(1024) void eq_totals(uint32_t n_hosts, uint32_t n_p
     }
 }
 
-// Exclusive scans of the popped counts and the batch's kept counts (H + 1 entries each) in ONE
-// launch: a tile of 8192 entries per 1024-thread workgroup (8 per thread, two 16-byte loads),
-// a block scan, then a decoupled look-back over the earlier tiles' published sums (tiles wait
-// only on lower workgroup indices, dispatched before them).  Each tile's state word is
-// epoch << 34 | flag << 32 | value (flag 1: the tile's own sum, 2: the inclusive prefix); the
-// epoch changes every launch, so the states are never cleared between launches.
-constexpr uint32_t kScanT = 1024, kScanV = 8, kScanTile = kScanT * kScanV;
-
-__device__ __forceinline__ void scan_load8(const uint32_t* in, uint64_t at, uint32_t n, uint32_t* v) {
-    if (in && at + kScanV <= n) {
-        const uint4 x = *reinterpret_cast<const uint4*>(in + at);
-        const uint4 y = *reinterpret_cast<const uint4*>(in + at + 4);
-        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-        v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
-    } else {
-#pragma unroll
-        for (uint32_t i = 0; i < kScanV; ++i) v[i] = in && at + i < n ? in[at + i] : 0u;
-    }
-}
-
-// the sum of array k over tiles [0, tile): walk back over the published states until a tile
-// with its inclusive prefix (flag 2); a tile not yet published (or of an older epoch) is waited on
-__device__ __forceinline__ uint32_t scan_lookback(const unsigned long long* state, uint32_t tile, uint32_t k,
-                                                  uint32_t epoch) {
-    uint32_t x = 0;
-    for (int64_t p = (int64_t)tile - 1; p >= 0;) {
-        const unsigned long long v =
-            __hip_atomic_load(&state[(size_t)p * 2 + k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t f = (uint32_t)(v >> 32) & 3u;
-        if ((uint32_t)(v >> 34) != epoch || f == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        x += (uint32_t)v;
-        if (f == 2) break;
-        --p;
-    }
-    return x;
-}
-
-__global__ __launch_bounds__(1024) void eq_scan2(uint32_t n, const uint32_t* __restrict__ a_in, uint32_t* __restrict__ a_out,
-                                                 const uint32_t* __restrict__ b_in, uint32_t* __restrict__ b_out,
-                                                 unsigned long long* __restrict__ state, uint32_t epoch) {
-    __shared__ uint32_t s_w[16][2];
-    __shared__ uint32_t s_pref[2];
-    const uint32_t tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint64_t at = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanV;
-    uint32_t va[kScanV], vb[kScanV];
-    scan_load8(a_in, at, n, va);
-    scan_load8(b_in, at, n, vb);
-    uint32_t sa = 0, sb = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kScanV; ++i) {
-        sa += va[i];
-        sb += vb[i];
-    }
-    uint32_t ia = sa, ib = sb;   // inclusive within the wave
-#pragma unroll
-    for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t ya = __shfl_up(ia, o), yb = __shfl_up(ib, o);
-        if (lane >= o) {
-            ia += ya;
-            ib += yb;
-        }
-    }
-    if (lane == 63) {
-        s_w[w][0] = ia;
-        s_w[w][1] = ib;
-    }
-    __syncthreads();
-    uint32_t wa = 0, wb = 0, ta = 0, tb = 0;   // waves before this one; the tile's total
-#pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) {
-        const uint32_t xa = s_w[k][0], xb = s_w[k][1];
-        if (k < w) {
-            wa += xa;
-            wb += xb;
-        }
-        ta += xa;
-        tb += xb;
-    }
-    if (tid == 0) {
-        unsigned long long* st = state + (size_t)tile * 2;
-        const unsigned long long tag = (unsigned long long)epoch << 34;
-        if (tile == 0) {
-            __hip_atomic_store(&st[0], tag | (2ull << 32) | ta, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&st[1], tag | (2ull << 32) | tb, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            s_pref[0] = s_pref[1] = 0;
-        } else {
-            __hip_atomic_store(&st[0], tag | (1ull << 32) | ta, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&st[1], tag | (1ull << 32) | tb, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t ea = scan_lookback(state, tile, 0, epoch), eb = scan_lookback(state, tile, 1, epoch);
-            __hip_atomic_store(&st[0], tag | (2ull << 32) | (uint32_t)(ea + ta), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&st[1], tag | (2ull << 32) | (uint32_t)(eb + tb), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            s_pref[0] = ea;
-            s_pref[1] = eb;
-        }
-    }
-    __syncthreads();
-    uint32_t ra = s_pref[0] + wa + ia - sa, rb = s_pref[1] + wb + ib - sb;   // exclusive prefix of this thread
-    uint32_t oa[kScanV], ob[kScanV];
-#pragma unroll
-    for (uint32_t i = 0; i < kScanV; ++i) {
-        oa[i] = ra;
-        ob[i] = rb;
-        ra += va[i];
-        rb += vb[i];
-    }
-    if (at + kScanV <= n) {
-        *reinterpret_cast<uint4*>(a_out + at) = make_uint4(oa[0], oa[1], oa[2], oa[3]);
-        *reinterpret_cast<uint4*>(a_out + at + 4) = make_uint4(oa[4], oa[5], oa[6], oa[7]);
-        if (b_out) {
-            *reinterpret_cast<uint4*>(b_out + at) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
-            *reinterpret_cast<uint4*>(b_out + at + 4) = make_uint4(ob[4], ob[5], ob[6], ob[7]);
-        }
-    } else {
-#pragma unroll
-        for (uint32_t i = 0; i < kScanV; ++i)
-            if (at + i < n) {
-                a_out[at + i] = oa[i];
-                if (b_out) b_out[at + i] = ob[i];
-            }
-    }
-}
-
-// the two exclusive scans of an advance (b_in / b_out may be null: one array)
-static shd_status eq_scans(EqState& Q, const uint32_t* a_in, uint32_t* a_out, const uint32_t* b_in, uint32_t* b_out,
-                           uint32_t n, hipStream_t s) {
-    const uint32_t tiles = div_up(n, kScanTile);
-    if ((size_t)tiles * 16 > Q.scan_tmp.bytes) return SHD_ERR_STATE;   // sized by shd_equeue_setup
-    if (++Q.scan_epoch >= (1u << 30)) {   // epochs wrap: clear the states once
-        SHD_HIP(hipMemsetAsync(Q.scan_tmp.p, 0, Q.scan_tmp.bytes, s));
-        Q.scan_epoch = 1;
-    }
-    eq_scan2<<<tiles, kScanT, 0, s>>>(n, a_in, a_out, b_in, b_out, Q.scan_tmp.as<unsigned long long>(), Q.scan_epoch);
-    SHD_HIP(hipGetLastError());
-    return SHD_OK;
-}
-
 // a stored run's event arrays for n events (the ensure keeps growth headroom: slots are reused
 // round after round)
 static shd_status eq_run_alloc(EqRunBuf& r, uint32_t n_hosts, uint64_t n) {
@@ -559,8 +418,9 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
     eqr_count<<<nb, 256, 0, s>>>(H, S, window_end, Q.pop_cnt.as<uint32_t>(), Q.keep_cnt.as<uint32_t>(), part,
                                  Q.ranges.as<uint2>());
     SHD_HIP(hipGetLastError());
-    SHD_TRY(eq_scans(Q, Q.pop_cnt.as<uint32_t>(), out_off, nrun ? Q.keep_cnt.as<uint32_t>() : nullptr,
-                     nrun ? nrun->off.as<uint32_t>() : nullptr, H + 1, s));
+    // the popped offsets and the new run's offsets: one hand-written look-back scan launch (scan.h)
+    SHD_TRY(scan_excl2(Q.scan, Q.pop_cnt.as<uint32_t>(), out_off, nrun ? Q.keep_cnt.as<uint32_t>() : nullptr,
+                       nrun ? nrun->off.as<uint32_t>() : nullptr, H + 1, s));
     const EqOut nr = nrun ? eq_run_out(*nrun) : EqOut{};
     if (n_in)
         eqr_merge<<<div_up(H, 4), 256, 0, s>>>(H, S, out_off, out, nr, nrun ? nrun->off.as<uint32_t>() : nullptr,
@@ -643,9 +503,6 @@ shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_total) {
     SHD_TRY(Q.keep_cnt.ensure((size_t)(n_hosts + 1) * 4));
     SHD_TRY(Q.pop_off.ensure((size_t)(n_hosts + 1) * 4));
     SHD_TRY(Q.next.ensure((kEqWords + (size_t)kEqCountBlocksMax * kEqPart) * 8));
-    SHD_TRY(Q.scan_tmp.ensure((size_t)div_up((uint64_t)n_hosts + 1, kScanTile) * 16));
-    SHD_HIP(hipMemsetAsync(Q.scan_tmp.p, 0, Q.scan_tmp.bytes, ctx->stream));
-    Q.scan_epoch = 0;
     SHD_HIP(hipMemsetAsync(Q.pop_off.p, 0, (size_t)(n_hosts + 1) * 4, ctx->stream));
     SHD_HIP(hipStreamSynchronize(ctx->stream));
     Q.ccur = 0;

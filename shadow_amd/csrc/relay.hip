@@ -22,11 +22,10 @@
 #include <cstdlib>
 #include <cstring>
 
-#include <rocprim/rocprim.hpp>
 
 #include <vector>
 
-#include "ctx.h"
+#include "scan.h"
 
 namespace shd {
 
@@ -1362,12 +1361,9 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.red = R.red.as<unsigned long long>();
     relay_stamp<<<div_up(std::max<uint32_t>(R.n_src, 1), 256), 256, 0, s>>>(a);
     SHD_HIP(hipGetLastError());
-    size_t tmp_bytes = 0;
-    SHD_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off, 0u,
-                                    (size_t)H + 1, rocprim::plus<uint32_t>(), s));
-    SHD_TRY(R.scan_tmp.ensure(tmp_bytes));
-    SHD_HIP(rocprim::exclusive_scan(R.scan_tmp.p, tmp_bytes, R.dst_cnt.as<uint32_t>(), o->ev_off,
-                                    0u, (size_t)H + 1, rocprim::plus<uint32_t>(), s));
+    // destination offsets: one hand-written look-back scan launch (scan.h); ev_off must be
+    // 16-byte aligned (the relay's own buffers are; a caller's device array from hipMalloc too)
+    SHD_TRY(scan_excl2(R.scan, R.dst_cnt.as<uint32_t>(), o->ev_off, nullptr, nullptr, (uint64_t)H + 1, s));
     if (n)
         relay_scatter<<<div_up(n, 256), 256, 0, s>>>(n, R.n_src, R.src_lo, b->src_off, o->status, b->dst_host,
                                                      R.ev_val.as<uint32_t>(), R.ev_key.as<uint64_t>(),
@@ -1392,8 +1388,6 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
     return SHD_OK;
 }
 
-// rocPRIM onesweep by destination: RB bits per pass (the default for this key/value pair on
-// gfx950 is 8 -> three passes for 100k hosts; 9 bits covers 2^18 hosts in two passes)
 
 // ==========================================================================================
 // Pipeline v7: destination-bin placement instead of a radix sort.  The stamp writes every
@@ -1834,23 +1828,6 @@ __global__ __launch_bounds__(kB7Threads) void bin_sort_v7(uint32_t n_hosts, uint
     for (uint32_t p = tid; p < S; p += kB7Threads) v7_emit(o, (size_t)excl + p, x[pm[p]]);
 }
 
-template <unsigned RB>
-using DstSortCfg = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 6>, rocprim::kernel_config<1024, 6>,
-                                        RB, rocprim::block_radix_rank_algorithm::match>>;
-
-template <unsigned RB>
-static shd_status sort_by_dst(RelayState& R, rocprim::double_buffer<uint32_t>& kb,
-                              rocprim::double_buffer<uint4>& vb, size_t n, uint32_t bits,
-                              hipStream_t s) {
-    size_t tmp_bytes = 0;
-    SHD_HIP((rocprim::radix_sort_pairs<DstSortCfg<RB>>(nullptr, tmp_bytes, kb, vb, n, 0u, bits, s)));
-    SHD_TRY(R.scan_tmp.ensure(tmp_bytes));
-    if (n) SHD_HIP((rocprim::radix_sort_pairs<DstSortCfg<RB>>(R.scan_tmp.p, tmp_bytes, kb, vb, n, 0u, bits, s)));
-    return SHD_OK;
-}
-
 // Narrow pipeline: K1 stamp, K2 radix sort by destination, K3 offsets, K4 per-run sort; one
 // host sync (for the round reductions).
 // the round's reductions: [0] min deliver, [1] min latency, [2] sent, [3] first bad index,
@@ -1924,19 +1901,16 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
         relay_stamp_v5<<<div_up(R.n_src, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint32_t>());
     }
     SHD_HIP(hipGetLastError());
-    // stable LSD radix sort of the records by destination (keys <= H)
+    // stable LSD radix sort of the records by destination (keys <= H), hand-written (scan.h)
     uint32_t bits = 1;
     while (bits < 32 && (H >> bits) != 0) ++bits;
-    rocprim::double_buffer<uint32_t> kb(R.ev_val.as<uint32_t>(), R.ev_key.as<uint32_t>());
-    rocprim::double_buffer<uint4> vb(R.rec.as<uint4>(), R.brec.as<uint4>());
-    const char* ev = std::getenv("SHD_RADIX_BITS");   // tuning override (results identical)
-    const uint32_t rb = ev && *ev ? (uint32_t)std::atoi(ev) : (bits > 16 && bits <= 18 ? 9u : 8u);
-    if (rb == 11) SHD_TRY(sort_by_dst<11>(R, kb, vb, (size_t)n, bits, s));
-    else if (rb == 9) SHD_TRY(sort_by_dst<9>(R, kb, vb, (size_t)n, bits, s));
-    else SHD_TRY(sort_by_dst<8>(R, kb, vb, (size_t)n, bits, s));
-    uint4* sorted = vb.current();
-    uint4* spare = sorted == R.rec.as<uint4>() ? R.brec.as<uint4>() : R.rec.as<uint4>();
-    bucket_offsets<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(kb.current(), n, H, o->ev_off);
+    bool first = true;
+    SHD_TRY(radix_sort_pairs(R.rs_counts, R.rs_scan, R.ev_val.as<uint32_t>(), R.rec.as<uint4>(),
+                             R.ev_key.as<uint32_t>(), R.brec.as<uint4>(), n, bits, &first, s));
+    uint4* sorted = first ? R.rec.as<uint4>() : R.brec.as<uint4>();
+    uint4* spare = first ? R.brec.as<uint4>() : R.rec.as<uint4>();
+    const uint32_t* skeys = first ? R.ev_val.as<uint32_t>() : R.ev_key.as<uint32_t>();
+    bucket_offsets<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(skeys, n, H, o->ev_off);
     segment_sort_v5<<<div_up(H, kSegDst), 256, 0, s>>>(
         H, o->ev_off, sorted, rd->round_end, seq_base, o->ev_deliver, o->ev_src,
         o->ev_seq, o->ev_pkt, R.ev_val2.as<uint32_t>());
@@ -2057,7 +2031,6 @@ static shd_status relay_run(shd_ctx* ctx, const shd_batch* b, const shd_round* r
     const uint64_t nn = (uint64_t)R.n_nodes * R.n_nodes;
     SHD_TRY(R.red.ensure(64));
     SHD_TRY(R.dst_cnt.ensure((size_t)(H + 1) * 4));
-    SHD_TRY(R.scan_tmp.ensure(64));
     // every pipeline attempt counts into a zeroed per-round buffer; only the committed attempt
     // reaches the counters (a rerun or a failed round must not count)
     auto zero_counts = [&]() -> shd_status {
