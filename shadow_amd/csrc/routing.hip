@@ -343,7 +343,7 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
             uint2 a[kFlatR];
             uint32_t lu[kFlatR], k[kFlatR], cl[kFlatR];
             float qu[kFlatR];
-            bool ok[kFlatR];
+            bool ok[kFlatR], sure[kFlatR];
 #pragma unroll
             for (int r = 0; r < kFlatR; ++r) {
                 const uint32_t t = t0 + r * 64 + lane;
@@ -365,14 +365,19 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
                 cl[r] = lu[r] + a[r].y;
                 const bool fit = cl[r] >= lu[r] && cl[r] != kLat32Inf;
                 if (ok[r] && !fit) ovf = true;   // leaves u32: wide rerun
-                // bucket-byte filter (see expand_flat): a higher bucket cannot improve the label
-                ok[r] = ok[r] && fit && bucket_of(cl[r], inv_delta) <= bkt[a[r].x];
+                // bucket-byte filter (see expand_flat): a higher bucket cannot improve the label;
+                // a strictly lower one surely does (bkt >= the label's bucket), so its atomic
+                // goes out without the filtering read -- one global round trip less on the
+                // flush's chain (C4 rows 0-4095: 19.3 -> 17.6 ms)
+                const uint32_t bq = bucket_of(cl[r], inv_delta), bv = bkt[a[r].x];
+                ok[r] = ok[r] && fit && bq <= bv;
+                sure[r] = bq < bv;
             }
             uint64_t cur[kFlatR];
             float qa[kFlatR];
 #pragma unroll
             for (int r = 0; r < kFlatR; ++r) {
-                cur[r] = !ok[r] ? 0ull : a[r].x < kl ? llab[a[r].x] : ld_lab<true>(&lab[a[r].x]);
+                cur[r] = !ok[r] ? 0ull : a[r].x < kl ? llab[a[r].x] : sure[r] ? kKeyInf : ld_lab<true>(&lab[a[r].x]);
                 qa[r] = ok[r] ? aq[k[r]] : 0.0f;
             }
 #pragma unroll
@@ -388,7 +393,7 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
                                     : atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[r].x]), (unsigned long long)cand);
                     if (cand < old) {
                         dirty = true;
-                        const uint8_t bk = bucket_of(cl[r], inv_delta);
+                        const uint8_t bk = (uint8_t)bucket_of(cl[r], inv_delta);
                         bkt[a[r].x] = bk;
                         mnext = min(mnext, (uint32_t)(bk >> kBktShift));
                         atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));

@@ -29,4 +29,4 @@ for algo in algos:
     h = (int(lat.sum().item()), int(loss.view(torch.int32).to(torch.int64).sum().item()))
     ref = ref or h
     print(f"algo={algo} rows={re-rb} ms_main={i['ms_main']:.2f} wall={dt*1e3:.2f} per_row_us={i['ms_main']*1e3/(re-rb):.1f} "
-          f"same={h == ref} env={ {k: v for k, v in os.environ.items() if k.startswith('SHD_')} }", flush=True)
+          f"same={h == ref} hash={h} env={ {k: v for k, v in os.environ.items() if k.startswith('SHD_')} }", flush=True)
