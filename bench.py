@@ -553,15 +553,15 @@ def cpu_baseline_relay(rl, lat_table, loss_table, budget_s=8.0):
                        f"mutex + binary-heap push, OpenMP over source hosts)")
 
 
-EQ_BYTES_BATCH = 24    # a batch event read once (deliver 8, src 4, seq 8, packet 4)
-EQ_BYTES_KEPT = 28     # a batch event written once: to its new run or to the popped output (deliver, src, seq, tag)
-EQ_BYTES_POPPED = 56   # an older run's popped event read and written to the output
+EQ_BYTES_POPPED = 52   # a popped event read from its run (deliver 8, src 4, seq 8, packet 4) and written
+                       # to the output (deliver, src, seq, tag 8)
 
 
-def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4, cpu=False):
+def equeue_leg(eng, rl, lat_table, loss_table, rounds=16, timed=8, cpu=False):
     """The north star's whole relay path, round after round on C5 (1 ms windows, 1-300 ms paths:
     events stay pending for many rounds): the relay round, then shd_equeue_advance -- the merge of
-    its events into the device-resident destination queues and the pop of the next window.
+    its events into the device-resident destination queues and the pop of the next window.  The
+    timed rounds include a compaction (the run limit is reached at round 8).
     Roofline bytes = the relay's SURVEY 8(d) bytes + the merge's (24 B per batch event read, 28 B
     per kept event written, 56 B per popped event read + written).  CPU baseline: the C
     restatement doing the same rounds -- send_packet with push_packet_to_host into persistent
@@ -576,10 +576,9 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4, cpu=False):
     # the relay leg's counters-on run leaves them on: this leg times the default (counters off)
     N.check(eng.lib.shd_relay_set_counters(eng.ctx, 0), "set_counters")
     st = torch.empty(P, dtype=torch.uint8, device="cuda")
-    ev = [torch.empty(H + 1, dtype=torch.int32, device="cuda"), torch.empty(P, dtype=torch.int64, device="cuda"),
-          torch.empty(P, dtype=torch.int32, device="cuda"), torch.empty(P, dtype=torch.int64, device="cuda"),
-          torch.empty(P, dtype=torch.int32, device="cuda")]
-    out = N.RelayOut(N.ptr(st).value, *(N.ptr(t).value for t in ev), 0, 0, 0, 0, 0)
+    # the relay writes each round into the queue slot shd_equeue_batch_buffers hands out, and the
+    # advance adopts it as a stored run: the round's events are written once, never copied
+    out = N.RelayOut()
     qo = N.EqueueOut()
     start0 = start = rl["start"]
     t_relay = t_adv = 0.0
@@ -596,6 +595,8 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4, cpu=False):
         rnd = N.Round(start + 10**6, end, 0)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        N.check(eng.lib.shd_equeue_batch_buffers(eng.ctx, P, C.byref(out)), "equeue_batch_buffers")
+        out.status = N.ptr(st).value
         N.check(eng.lib.shd_relay_round_device(eng.ctx, C.byref(batch), C.byref(rnd), C.byref(out)), "relay")
         t1 = time.perf_counter()
         N.check(eng.lib.shd_equeue_advance(eng.ctx, C.byref(out), start + 2 * 10**6, C.byref(qo)), "advance")
@@ -606,11 +607,9 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4, cpu=False):
             pops += qo.n_popped
             pend += qo.n_pending
             n_sent_t += out.n_sent
-            # every batch event is read once and written once (to its new run, or popped); popped
-            # events of older runs are read and written; at most min(n_sent, n_popped) popped
-            # events came from the batch, so this is a lower bound
-            bytes_merge += (EQ_BYTES_BATCH + EQ_BYTES_KEPT) * out.n_sent + \
-                EQ_BYTES_POPPED * max(0, qo.n_popped - out.n_sent)
+            # the batch is adopted where the relay wrote it (its bytes are the relay's own); every
+            # popped event is read from its run and written to the output
+            bytes_merge += EQ_BYTES_POPPED * qo.n_popped
         start += 10**6
         if k == rounds - 1:
             n = qo.n_popped
@@ -630,8 +629,8 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4, cpu=False):
            "popped_per_round": pops / timed, "pending_mean": pend / timed,
            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": ach / HBM_PEAK_GBS, "bytes_per_round": algo,
-                        "work": "relay 84 B/packet + 80 B/host (SURVEY 8(d)) + merge 52 B per batch event (read "
-                                "24, written 28) + 56 B per popped event of an older run (lower bound)"}}
+                        "work": "relay 84 B/packet + 80 B/host (SURVEY 8(d)) + merge 52 B per popped event (read "
+                                "24, written 28); the round's events are adopted where the relay wrote them"}}
     if cpu:
         from oracle import corc
         threads = corc.max_threads()
@@ -662,6 +661,50 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=8, timed=4, cpu=False):
                                          f"mutexes, then every host's pop loop), last {timed} timed",
                                "bit_exact_vs_gpu": bool(same)}
     return res
+
+
+def equeue_leg_sharded(eng, world, rank, rl, lat_table, loss_table, rounds=6, timed=3):
+    """N > 1: the whole relay path per round over the engine communicator -- each rank's sharded
+    relay round (its source hosts; events exchanged to their destination ranks), the agreed next
+    window (shd_round_window, a collective), and the merge + pop into the rank's own destination
+    queues (shd_equeue_advance).  Time per round = the max over the ranks."""
+    import torch
+    from shadow_amd import _native as N
+    from shadow_amd import dist as D
+    from shadow_amd.equeue import EventQueues
+    from shadow_amd.rounds import Runahead, next_window
+    H, b = rl["H"], rl["batch"]
+    rel = D.ShardedRelay(eng, rl["host_node"], rl["rng0"], np.zeros(H, np.uint64), lat_table, loss_table)
+    N.check(eng.lib.shd_relay_set_counters(eng.ctx, 0), "set_counters")
+    q = EventQueues(eng, H)
+    Runahead(eng, False, int(lat_table.min()), 10**6)   # fixed 1 ms windows, as the 1-GPU leg
+    lo, hi = rel.lo, rel.hi
+    a, e = int(b.src_off[lo]), int(b.src_off[hi])
+    d_off = _dev((b.src_off[lo:hi + 1] - b.src_off[lo]).astype(np.uint32), np.int32)
+    d_time, d_dst = _dev(b.send_time[a:e], np.int64), _dev(b.dst_host[a:e], np.int32)
+    d_pay = _dev(b.payload[a:e], np.int32)
+    t_base = d_time.clone()
+    st = torch.empty(max(e - a, 1), dtype=torch.uint8, device="cuda")
+    start, end = rl["start"], rl["start"] + 10**12
+    t_tot, pops = 0.0, 0
+    barrier_sync(world)
+    for k in range(rounds):
+        d_time.copy_(t_base + k * 10**6)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = rel.round_device(d_off, d_time, d_dst, d_pay, (start + 10**6, end, 0), st)
+        win = next_window(eng, None, end)
+        qo = q.advance_device(out, win[1] if win else 2**63)
+        dt = time.perf_counter() - t0
+        if k >= rounds - timed:
+            t_tot += dt
+            pops += qo.n_popped
+        start += 10**6
+    ms = max_over_ranks(t_tot / timed * 1e3, world)
+    return {"workload": f"C5 rounds over {world} ranks: shd_relay_round_sharded + shd_round_window + "
+                        f"shd_equeue_advance into each rank's destination queues", "rounds": rounds,
+            "timed_rounds": timed, "ms_per_round": ms, "value": rl["P"] / (ms * 1e-3),
+            "unit": "packets relayed + merged/s", "popped_per_round_rank0": pops / timed}
 
 
 def codel_leg(eng, steps=5, cpu=True):
@@ -881,6 +924,8 @@ def main():
             rel["equeue"] = equeue_leg(eng, rl, r["lat"], r["loss"], cpu=cpu)
         if world > 1:
             checks["relay_round_bit_exact_all_ranks"] = relay_check_sharded(eng, world, rank, rl, r["lat"], r["loss"])
+            if not args.no_equeue:
+                rel["equeue"] = equeue_leg_sharded(eng, world, rank, rl, r["lat"], r["loss"])
         res["relay"] = rel
     if world == 1 and not args.no_c3:
         res["c3"] = c3_leg(eng, cpu=cpu)

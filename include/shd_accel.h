@@ -344,6 +344,11 @@ typedef struct shd_equeue_out {
 shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_hosts);
 shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64_t window_end,
                               shd_equeue_out* out);
+/* Engine-owned device arrays (ev_off, ev_deliver, ev_src, ev_seq, ev_pkt; n_dst set) for up to
+ * max_events events of the next round's relay output: pass them as the shd_relay_round_device
+ * output (with the caller's status array), then to shd_equeue_advance, which adopts the batch as
+ * a stored run without copying any of it.  Valid until that advance (or the next call). */
+shd_status shd_equeue_batch_buffers(shd_ctx* ctx, uint64_t max_events, shd_relay_out* out);
 /* Host copies of the last advance's popped events (any pointer may be NULL). */
 shd_status shd_equeue_copy_popped(shd_ctx* ctx, uint32_t* off, uint64_t* deliver, uint32_t* src,
                                   uint64_t* seq, uint64_t* tag);

@@ -36,7 +36,7 @@ EXPORTED = [
     "shd_equeue_setup", "shd_equeue_advance", "shd_equeue_copy_popped", "shd_equeue_pending",
     "shd_routing_run_next_hops", "shd_assign_ips", "shd_gml_load",
     "shd_runahead_setup", "shd_runahead_get", "shd_round_window", "shd_window_compute", "shd_copy_to_host",
-    "shd_routing_lookup_batch", "shd_routing_mirror",
+    "shd_routing_lookup_batch", "shd_routing_mirror", "shd_equeue_batch_buffers",
 ]
 COMM_ID_BYTES = 128
 
@@ -183,6 +183,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_copy_to_host": (I32, [P, P, P, C.c_size_t]),
         "shd_routing_lookup_batch": (I32, [P, U64, P, P, P, P]),
         "shd_routing_mirror": (I32, [P, I32]),
+        "shd_equeue_batch_buffers": (I32, [P, U64, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

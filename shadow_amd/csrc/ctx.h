@@ -54,16 +54,21 @@ struct CodelState {   // CoDel router queues (codel.hip)
 };
 
 constexpr int kEqMaxRuns = 8;   // stored runs of the event queues before they are compacted
+constexpr int kEqSlots = kEqMaxRuns + 2;   // + the compaction target + a batch slot handed out for adoption
 
 struct EqRunBuf {   // one stored run of the event queues: a CSR of per-host sorted events
     DevBuf off, deliver, src, seq, tag;
+    DevBuf pkt;                 // an adopted relay output keeps ev_pkt: tag = batch << 32 | pkt
+    bool has_pkt = false;
+    uint64_t batch = 0;
     uint64_t n = 0, left = 0;   // events stored / not yet popped
     bool live = false;
 };
 
 struct EqState {   // destination event queues (equeue.hip): a list of sorted runs (one per batch)
-    EqRunBuf run[kEqMaxRuns + 1];   // slots; one more than kEqMaxRuns for the compaction target
-    DevBuf curs[2];                 // [kEqMaxRuns + 1][n_hosts] u32 cursors (first unpopped), double-buffered
+    EqRunBuf run[kEqSlots];         // slots
+    int lend = -1;                  // the slot handed out by shd_equeue_batch_buffers (not live yet)
+    DevBuf curs[2];                 // [kEqSlots][n_hosts] u32 cursors (first unpopped), double-buffered
     DevBuf bcut;                    // [n_hosts] the batch's first kept event per host
     DevBuf pd, ps, pq, pt;          // the last call's popped events
     DevBuf pop_cnt, keep_cnt, pop_off, next, left;

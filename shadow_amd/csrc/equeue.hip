@@ -389,6 +389,7 @@ static shd_status eq_run_alloc(EqRunBuf& r, uint32_t n_hosts, uint64_t n) {
     SHD_TRY(r.src.ensure(m * 4));
     SHD_TRY(r.seq.ensure(m * 8));
     SHD_TRY(r.tag.ensure(m * 8));
+    r.has_pkt = false;
     return SHD_OK;
 }
 
@@ -436,44 +437,62 @@ static uint32_t* eq_cursor(EqState& Q, int buf, int slot) {
     return Q.curs[buf].as<uint32_t>() + (size_t)slot * Q.n_hosts;
 }
 
-// the live runs as sources, from their cursors; cuts into the other cursor buffer
-static EqSrcs eq_sources(EqState& Q, int* slots) {
+// the live runs as sources, from their cursors; cuts into the other cursor buffer.  pick
+// (optional) selects a subset of the live slots.
+static EqSrcs eq_sources(EqState& Q, int* slots, const bool* pick = nullptr) {
     EqSrcs S{};
     S.b = -1;
-    for (int r = 0; r <= kEqMaxRuns; ++r) {
+    for (int r = 0; r < kEqSlots; ++r) {
         EqRunBuf& R = Q.run[r];
-        if (!R.live) continue;
+        if (!R.live || (pick && !pick[r])) continue;
         slots[S.n] = r;
         S.s[S.n++] = EqSrc{R.off.as<uint32_t>(), eq_cursor(Q, Q.ccur, r), eq_cursor(Q, 1 - Q.ccur, r),
                            R.deliver.as<uint64_t>(), R.src.as<uint32_t>(), R.seq.as<uint64_t>(),
-                           R.tag.as<uint64_t>(), nullptr, 0};
+                           R.has_pkt ? nullptr : R.tag.as<uint64_t>(), R.has_pkt ? R.pkt.as<uint32_t>() : nullptr,
+                           R.batch};
     }
     return S;
 }
 
 static int eq_free_slot(const EqState& Q) {
-    for (int r = 0; r <= kEqMaxRuns; ++r)
-        if (!Q.run[r].live) return r;
+    for (int r = 0; r < kEqSlots; ++r)
+        if (!Q.run[r].live && r != Q.lend) return r;
     return -1;
 }
 
-// every pending event into one fresh run (cursor at its start); the old runs are dropped
-static shd_status eq_compact(shd_ctx* ctx) {
+// Pending events of several runs into one fresh run (cursor at its start); those runs are
+// dropped, the others keep their cursors.  all = false: the half of the live runs holding the
+// fewest pending events -- the oldest, mostly drained ones -- so a compaction forced by the run
+// limit costs what those runs still hold, not every pending event (C5: runs drain over hundreds
+// of rounds, the pending set is many rounds' worth).
+static shd_status eq_compact(shd_ctx* ctx, bool all) {
     EqState& Q = ctx->eq;
+    bool pick[kEqSlots] = {};
+    int live[kEqSlots], nl = 0;
+    for (int r = 0; r < kEqSlots; ++r)
+        if (Q.run[r].live) live[nl++] = r;
+    if (nl == 0) return SHD_OK;
+    std::sort(live, live + nl, [&](int a, int b) { return Q.run[a].left < Q.run[b].left; });
+    const int take = all ? nl : std::max(2, (nl + 1) / 2);
+    uint64_t n = 0;
+    for (int k = 0; k < take && k < nl; ++k) {
+        pick[live[k]] = true;
+        n += Q.run[live[k]].left;
+    }
     int slots[kEqSrcMax];
-    EqSrcs S = eq_sources(Q, slots);
+    EqSrcs S = eq_sources(Q, slots, pick);
     if (S.n == 0) return SHD_OK;
     const int t = eq_free_slot(Q);
     EqRunBuf& T = Q.run[t];
-    SHD_TRY(eq_run_alloc(T, Q.n_hosts, Q.n_pending));
-    SHD_TRY(eq_pass(ctx, S, ~0ull, T.off.as<uint32_t>(), eq_run_out(T), nullptr, nullptr, Q.n_pending));
-    if (ctx->h_pin[kEqPinWord + 1] != Q.n_pending) return SHD_ERR_INVALID;
-    SHD_HIP(hipMemcpyAsync(eq_cursor(Q, 1 - Q.ccur, t), T.off.p, (size_t)Q.n_hosts * 4, hipMemcpyDeviceToDevice,
+    SHD_TRY(eq_run_alloc(T, Q.n_hosts, n));
+    SHD_TRY(eq_pass(ctx, S, ~0ull, T.off.as<uint32_t>(), eq_run_out(T), nullptr, nullptr, n));
+    if (ctx->h_pin[kEqPinWord + 1] != n) return SHD_ERR_INVALID;
+    // the new run's cursor goes to the CURRENT cursor buffer: the runs left out keep theirs there
+    SHD_HIP(hipMemcpyAsync(eq_cursor(Q, Q.ccur, t), T.off.p, (size_t)Q.n_hosts * 4, hipMemcpyDeviceToDevice,
                            ctx->stream));
     for (uint32_t k = 0; k < S.n; ++k) Q.run[slots[k]].live = false;
-    Q.ccur = 1 - Q.ccur;
-    T.live = Q.n_pending > 0;
-    T.n = T.left = Q.n_pending;
+    T.live = n > 0;
+    T.n = T.left = n;
     return SHD_OK;
 }
 
@@ -493,11 +512,12 @@ shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_total) {
     if (ctx->comm && ctx->comm->size > 1) shard_range(n_total, ctx->comm->size, ctx->comm->rank, &lo, &hi);
     const uint32_t n_hosts = hi - lo;
     if (n_hosts == 0) return SHD_ERR_INVALID;
-    for (int r = 0; r <= kEqMaxRuns; ++r) {
+    for (int r = 0; r < kEqSlots; ++r) {
         Q.run[r].live = false;
         Q.run[r].n = Q.run[r].left = 0;
     }
-    for (int k = 0; k < 2; ++k) SHD_TRY(Q.curs[k].ensure((size_t)(kEqMaxRuns + 1) * n_hosts * 4));
+    for (int k = 0; k < 2; ++k) SHD_TRY(Q.curs[k].ensure((size_t)kEqSlots * n_hosts * 4));
+    Q.lend = -1;
     SHD_TRY(Q.bcut.ensure((size_t)n_hosts * 4));
     SHD_TRY(Q.pop_cnt.ensure((size_t)(n_hosts + 1) * 4));
     SHD_TRY(Q.keep_cnt.ensure((size_t)(n_hosts + 1) * 4));
@@ -514,6 +534,40 @@ shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_total) {
     Q.n_popped = 0;
     Q.batches = 0;
     Q.ready = true;
+    return SHD_OK;
+}
+
+shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64_t window_end,
+                              shd_equeue_out* out);
+
+// the pending runs alone (an adopted batch is one of them by now)
+static shd_status advance_runs(shd_ctx* ctx, uint64_t window_end, shd_equeue_out* out) {
+    return shd_equeue_advance(ctx, nullptr, window_end, out);
+}
+
+shd_status shd_equeue_batch_buffers(shd_ctx* ctx, uint64_t max_events, shd_relay_out* out) {
+    if (!ctx || !out) return SHD_ERR_INVALID;
+    EqState& Q = ctx->eq;
+    if (!Q.ready) return SHD_ERR_STATE;
+    SHD_HIP(hipSetDevice(ctx->device));
+    Q.lend = -1;
+    const int t = eq_free_slot(Q);
+    if (t < 0) return SHD_ERR_STATE;
+    EqRunBuf& R = Q.run[t];
+    const size_t m = std::max<uint64_t>(max_events, 1);
+    SHD_TRY(R.off.ensure((size_t)(Q.n_hosts + 1) * 4));
+    SHD_TRY(R.deliver.ensure(m * 8));
+    SHD_TRY(R.src.ensure(m * 4));
+    SHD_TRY(R.seq.ensure(m * 8));
+    SHD_TRY(R.pkt.ensure(m * 4));
+    Q.lend = t;
+    out->ev_off = R.off.as<uint32_t>();
+    out->ev_deliver = R.deliver.as<uint64_t>();
+    out->ev_src = R.src.as<uint32_t>();
+    out->ev_seq = R.seq.as<uint64_t>();
+    out->ev_pkt = R.pkt.as<uint32_t>();
+    out->n_dst = Q.n_hosts;
+    out->n_events = 0;
     return SHD_OK;
 }
 
@@ -536,9 +590,33 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     const uint64_t n_b = has_b ? d_batch->n_events : 0;   // this context's events (a sharded round: received)
     const uint64_t n_in = Q.n_pending + n_b;
     if (n_in >= 0xFFFFFFFFull) return SHD_ERR_INVALID;   // 32-bit positions
+    // adoption: a batch written into the slot shd_equeue_batch_buffers handed out becomes a stored
+    // run as it is -- its cursor starts at its offsets, nothing of it is copied
+    bool adopt = false;
+    if (has_b && Q.lend >= 0) {
+        EqRunBuf& L = Q.run[Q.lend];
+        adopt = d_batch->ev_off == L.off.p && d_batch->ev_deliver == L.deliver.p && d_batch->ev_src == L.src.p &&
+                d_batch->ev_seq == L.seq.p && d_batch->ev_pkt == L.pkt.p;
+        if (adopt && (n_b * 8 > L.deliver.bytes || n_b * 4 > L.pkt.bytes)) return SHD_ERR_INVALID;
+        if (!adopt) Q.lend = -1;   // the lent slot went unused: free again
+    }
     int live = 0;
-    for (int r = 0; r <= kEqMaxRuns; ++r) live += Q.run[r].live ? 1 : 0;
-    if (has_b && n_b && live >= kEqMaxRuns) SHD_TRY(eq_compact(ctx));   // room for the batch's run
+    for (int r = 0; r < kEqSlots; ++r) live += Q.run[r].live ? 1 : 0;
+    if (has_b && n_b && live >= kEqMaxRuns) SHD_TRY(eq_compact(ctx, false));   // room for the batch's run
+    if (adopt) {
+        const int t = Q.lend;
+        EqRunBuf& R = Q.run[t];
+        SHD_HIP(hipMemcpyAsync(eq_cursor(Q, Q.ccur, t), R.off.p, (size_t)H * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        R.has_pkt = true;
+        R.batch = Q.batches;
+        R.n = R.left = n_b;
+        R.live = n_b > 0;
+        Q.lend = -1;
+        ++Q.batches;
+        Q.n_pending += n_b;
+        ctx->rnd.batch_min_deliver = ~0ull;
+        return advance_runs(ctx, window_end, out);
+    }
     // the popped events: at most everything (headroom: the pending set creeps up at first)
     if (Q.ps.bytes < std::max<uint64_t>(n_in, 1) * 4) {
         const uint64_t cap = std::max<uint64_t>(n_in, 1) * 3 / 2 + 1;
@@ -627,9 +705,9 @@ shd_status shd_equeue_pending(shd_ctx* ctx, uint32_t* off, uint64_t* deliver, ui
     const uint64_t n = Q.n_pending;
     if (n_pending) *n_pending = n;
     if (!off && !(n && (deliver || src || seq || tag))) return SHD_OK;
-    SHD_TRY(eq_compact(ctx));
+    SHD_TRY(eq_compact(ctx, true));
     int live = -1;
-    for (int r = 0; r <= kEqMaxRuns; ++r)
+    for (int r = 0; r < kEqSlots; ++r)
         if (Q.run[r].live) live = r;
     if (off) {
         if (live >= 0) SHD_HIP(hipMemcpyAsync(off, Q.run[live].off.p, (size_t)(Q.n_hosts + 1) * 4, hipMemcpyDeviceToHost, s));

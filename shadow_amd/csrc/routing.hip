@@ -189,7 +189,7 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
                                             uint32_t* bits, const uint2* rng, const uint32_t* __restrict__ abeg,
                                             const uint32_t* __restrict__ aend, const uint4* __restrict__ arcs,
                                             uint32_t* fx, bool& ovf, bool& dirty, uint8_t* bkt, float inv_delta,
-                                            uint32_t scratch, uint32_t& mnext) {
+                                            uint32_t scratch, uint32_t& mnext, const uint32_t* offl = nullptr) {
     uint32_t* pre = fx;          // [65]
     uint32_t* beg = fx + 65;     // [64]
     uint32_t* nl = fx + 129;     // [64] latency of the node's label
@@ -200,7 +200,7 @@ __device__ __forceinline__ void expand_flat(const uint32_t* q, uint32_t qn, uint
         uint64_t ku = kKeyInf;
         if (lane < cn) {
             const uint32_t u = q[c0 + lane];
-            const uint2 r = rng ? rng[u] : make_uint2(abeg[u], aend[u]);
+            const uint2 r = rng ? rng[u] : offl ? make_uint2(offl[u], offl[u + 1]) : make_uint2(abeg[u], aend[u]);
             b = r.x;
             deg = r.y - b;
             ku = ld_lab<GLAB>(&lab[u]);
@@ -407,7 +407,7 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
 
 // One source row: init, sweeps until nothing improves, emit the used columns.
 // FASTG (global labels): flat expansion + bucket bytes + one-barrier delta sweeps only (C4)
-template <int BLOCK, int G, int R, bool CACHE, bool GLAB, int PADR = 0, bool FASTG = false>
+template <int BLOCK, int G, int R, bool CACHE, bool GLAB, int PADR = 0, bool FASTG = false, bool FLATL = false>
 __device__ __forceinline__ void sssp_row(
     uint64_t* lab, uint32_t* bits, uint32_t* ctl, uint32_t* wq, uint2* rng,
     const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
@@ -534,6 +534,9 @@ __device__ __forceinline__ void sssp_row(
                                                           ovf, dirty, bkt, inv_delta, mnext);
                     }
                 }
+            } else if constexpr (FLATL) {   // LDS labels, edge-parallel (sparse graphs with hubs)
+                expand_flat<false>(q, qn, lane, lab, bits, CACHE ? rng : nullptr, abeg, aend, arcs,
+                                   flat + wave * kFlatWords, ovf, dirty, nullptr, inv_delta, V + lane, mnext, offl);
             } else {
                 for (uint32_t t = 0; t < qn; t += NG) {
                     const uint32_t qi = t + grp;
@@ -719,7 +722,7 @@ __device__ __forceinline__ void sssp_row(
 
 // Kernel 1: one workgroup per source row, labels (8 B/node) and the arc ranges in LDS.
 // PADR = 8: padded arc lists (prune_rows), relax_node_pad with 8 arcs per lane per step.
-template <int BLOCK, int G, int R, bool CACHE, int PADR>
+template <int BLOCK, int G, int R, bool CACHE, int PADR, bool FLATL = false>
 __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
     const uint4* __restrict__ arcs, uint32_t V, const uint32_t* __restrict__ used,
@@ -728,9 +731,11 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     float* __restrict__ out_loss, uint32_t* __restrict__ flags,
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
-    uint32_t seed_stride, uint32_t* __restrict__ nh_out, uint32_t lat_guard, uint32_t use_offl) {
+    uint32_t seed_stride, uint32_t* __restrict__ nh_out, uint32_t lat_guard, uint32_t use_offl,
+    uint32_t flat_off) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr uint32_t NW = BLOCK / 64;
+    uint32_t* flat = FLATL ? reinterpret_cast<uint32_t*>(smem + flat_off) : nullptr;   // expand_flat scratch
     uint64_t* lab = reinterpret_cast<uint64_t*>(smem);   // V labels + 64 per-lane scratch labels
     const uint32_t W = (V + 31) >> 5;
     uint32_t* bits = reinterpret_cast<uint32_t*>(lab + V + 64);
@@ -744,10 +749,10 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     // next hops' pred[V] then follows them
     uint32_t* offl = !CACHE && use_offl ? reinterpret_cast<uint32_t*>(smem + rng_off) : nullptr;
     uint32_t* pred = offl ? offl + V + 1 : reinterpret_cast<uint32_t*>(smem + rng_off);
-    sssp_row<BLOCK, G, R, CACHE, false, PADR>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
+    sssp_row<BLOCK, G, R, CACHE, false, PADR, false, FLATL>(lab, bits, ctl, wq, rng, abeg, aend, arcs, V, used, n_used,
                                               row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
                                               diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
-                                              delta, stats, seed_lat, seed_stride, nullptr, nullptr, nh_out,
+                                              delta, stats, seed_lat, seed_stride, nullptr, flat, nh_out,
                                               pred, lat_guard, nullptr, nullptr, offl);
 }
 
@@ -1567,16 +1572,22 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
                                   (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
                                   (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(),
                                   (const float*)ctx->g_diag_loss.as<float>(), d_lat, d_loss, flags, unreach, delta,
-                                  stats, seed, seed_stride, ctx->nh_out, lat_guard, use_offl);
+                                  stats, seed, seed_stride, ctx->nh_out, lat_guard, use_offl, 0u);
             return;
         }
     }
-    hipExtLaunchKernelGGL(sssp_lds_group<BLOCK, G, R, CACHE, 0>, dim3(re - rb), dim3(BLOCK), (uint32_t)lds,
+    // edge-parallel expansion (expand_flat) for sparse graphs whose hubs would idle a node
+    // group's wave (SHD_SSSP_LFLAT=1), when its per-wave scratch fits beside the rest
+    const size_t flat_off = (lds + 15) & ~(size_t)15, flat_bytes = (size_t)(BLOCK / 64) * kFlatWords * 4;
+    const bool flatl = !A.padded && !seed && delta != kLat32Inf && env_u32("SHD_SSSP_LFLAT", 0) == 1 &&
+                       flat_off + flat_bytes <= ctx->max_lds;
+    auto kern = flatl ? sssp_lds_group<BLOCK, G, R, CACHE, 0, true> : sssp_lds_group<BLOCK, G, R, CACHE, 0, false>;
+    hipExtLaunchKernelGGL(kern, dim3(re - rb), dim3(BLOCK), (uint32_t)(flatl ? flat_off + flat_bytes : lds),
                           ctx->stream, e0, e1, 0u, A.beg, A.end, A.arcs, P.V,
                           (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
                           (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(), (const float*)ctx->g_diag_loss.as<float>(),
                           d_lat, d_loss, flags, unreach, delta, stats, seed, seed_stride, ctx->nh_out, 0u,
-                          use_offl);
+                          use_offl, (uint32_t)flat_off);
 }
 
 static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {

@@ -50,6 +50,15 @@ class EventQueues:
         self.n_local = self.hi - self.lo
         N.check(engine.lib.shd_equeue_setup(engine.ctx, self.n_hosts), "shd_equeue_setup")
 
+    def batch_buffers(self, max_events: int) -> N.RelayOut:
+        """Engine-owned device arrays for the next relay output (``shd_equeue_batch_buffers``):
+        pass them as that round's output and then to ``advance_device``, which adopts the batch
+        without copying it.  The caller sets ``status`` before the relay call."""
+        out = N.RelayOut()
+        N.check(self.eng.lib.shd_equeue_batch_buffers(self.eng.ctx, int(max_events), C.byref(out)),
+                "shd_equeue_batch_buffers")
+        return out
+
     def advance_device(self, d_batch: N.RelayOut | None, window_end: int) -> N.EqueueOut:
         out = N.EqueueOut()
         N.check(self.eng.lib.shd_equeue_advance(self.eng.ctx, C.byref(d_batch) if d_batch is not None else None,

@@ -121,6 +121,17 @@ class Relay:
                 "shd_relay_round_device")
         return out
 
+    def round_device_into(self, d_off, d_time, d_dst, d_pay, round_end: int, sim_end: int, bootstrap_end: int,
+                          out: N.RelayOut) -> N.RelayOut:
+        """``shd_relay_round_device`` into a prepared output (e.g. ``EventQueues.batch_buffers``
+        with ``status`` set): the events land where the queues adopt them."""
+        n = int(d_time.numel())
+        b = N.Batch(n, N.ptr(d_off).value, N.ptr(d_time).value, N.ptr(d_dst).value, N.ptr(d_pay).value, None)
+        rd = N.Round(round_end, sim_end, bootstrap_end)
+        N.check(self.eng.lib.shd_relay_round_device(self.eng.ctx, C.byref(b), C.byref(rd), C.byref(out)),
+                "shd_relay_round_device")
+        return out
+
     def host_state(self):
         rng = np.zeros((self.n_hosts, 4), np.uint64)
         nid = np.zeros(self.n_hosts, np.uint64)

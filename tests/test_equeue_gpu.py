@@ -135,6 +135,57 @@ def _cmp_popped(p, op):
     assert np.array_equal(p.tag, op["tag"])
 
 
+@pytest.mark.parametrize("adopt", [True, False])
+def test_adopted_batches_vs_c_queues(engine, adopt):
+    """The relay writes each round straight into the slot shd_equeue_batch_buffers hands out and
+    the advance adopts it as a stored run (no copy) -- or, adopt=False, into the caller's own
+    device arrays (copied).  5 ms windows over 1-300 ms paths for 14 rounds: the run limit forces
+    partial compactions (the runs holding the fewest pending events) from round 8 on.  Every
+    popped event, the pending count and the next time against the C EventQueues; then pending()
+    against the heaps' contents."""
+    import torch
+    from shadow_amd import synth
+    from shadow_amd.equeue import EventQueues
+    from shadow_amd.relay import Relay
+    H, P, NN = 2000, 60_000, 60
+    el = synth.complete_graph(NN, 31)
+    used = np.arange(NN, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(NN, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    host_node = synth.c5_host_nodes(H, NN)
+    rng0 = synth.host_rng_states(H, 1)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    q = EventQueues(engine, H)
+    oq = corc.EventQueues(H)
+    orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+    bufs = rl.device_buffers(P)
+    dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()  # noqa: E731
+    start, win = 10**9, 5 * 10**6
+    for rnd in range(14):
+        b = synth.packet_batch(H, P, start, start + win, seed=300 + rnd)
+        d = [dev(b.src_off, np.int32), dev(b.send_time, np.int64), dev(b.dst_host, np.int32), dev(b.payload, np.int32)]
+        torch.cuda.synchronize()
+        if adopt:
+            out = q.batch_buffers(P)
+            out.status = N_ptr(bufs["status"])
+            rl.round_device_into(*d, start + win, start + 10**12, 0, out)
+        else:
+            out = rl.round_device(*d, start + win, start + 10**12, 0, bufs)
+        corc.relay_round_eq(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, orng, onid,
+                            start + win, start + 10**12, 0, queues=oq, batch_no=rnd)
+        p = q.popped(q.advance_device(out, start + 2 * win))
+        _cmp_popped(p, oq.pop(start + 2 * win))
+        start += win
+    off, dl, sr, sq, tg = q.pending()
+    op = oq.pending()
+    for k, v in (("off", off), ("deliver", dl), ("src", sr), ("seq", sq), ("tag", tg)):
+        assert np.array_equal(v, op[k]), k
+
+
+def N_ptr(t):
+    return t.data_ptr()
+
+
 def test_c5_scale_rounds_vs_c_queues(engine):
     """BASELINE config 5 at full size: 100k hosts x 10M packets per round on the C2 table (1-300
     ms paths), 1 ms windows for 4 rounds -- the queues then hold ~40M pending events in up to 5
