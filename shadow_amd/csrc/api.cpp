@@ -1,5 +1,7 @@
 // C ABI entry points (include/shd_accel.h): context lifetime, routing build front ends,
 // resident-table lookups.  The relay entry points live in relay.hip.
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <new>
 #include <vector>
@@ -33,6 +35,31 @@ static void drop_resident_table(shd_ctx* ctx) {
     ctx->t_full = false;
     if (ctx->relay.ready && !ctx->relay.own_table) ctx->relay.ready = false;
 }
+
+namespace shd {
+// Wait for the stream by polling a pinned host word that a marker copy, enqueued behind the
+// work, sets to 1: the copy lands when every earlier operation on the stream has completed
+// (streams run in order), and the host sees it within a few hundred ns, while
+// hipStreamSynchronize's wake-up costs several us on every synchronous call (the C2 build
+// is ~0.1 ms).  A wait longer than 20 ms (long kernels, or a fault that stops the queue) falls
+// back to hipStreamSynchronize, which also reports a failed kernel.
+shd_status wait_stream(shd_ctx* ctx, hipStream_t s) {
+    if (!ctx->spin_wait) {
+        SHD_HIP(hipStreamSynchronize(s));
+        return SHD_OK;
+    }
+    volatile unsigned long long* done = ctx->h_pin + kPinMarker;
+    *done = 0;
+    SHD_HIP(hipMemcpyAsync(const_cast<unsigned long long*>(done), ctx->g_one.p, 8, hipMemcpyDeviceToHost, s));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1; *done != 1; ++i) {
+        __builtin_ia32_pause();
+        if ((i & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+    }
+    if (*done != 1) SHD_HIP(hipStreamSynchronize(s));
+    return SHD_OK;
+}
+}  // namespace shd
 
 extern "C" {
 
@@ -84,11 +111,21 @@ shd_ctx* shd_open(int device_ordinal, shd_status* st) {
         return fail(SHD_ERR_HIP);
     }
     ctx->own_stream = true;
-    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pin), 64 * sizeof(unsigned long long),
+    if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pin), shd::kPinWords * sizeof(unsigned long long),
                       hipHostMallocDefault) != hipSuccess) {
         ctx->h_pin = nullptr;
         shd_close(ctx);
         return fail(SHD_ERR_HIP);
+    }
+    {   // the device word the polled waits copy back (shd::wait_stream)
+        const unsigned long long one = 1;
+        if (ctx->g_one.ensure(8) != SHD_OK ||
+            hipMemcpy(ctx->g_one.p, &one, 8, hipMemcpyHostToDevice) != hipSuccess) {
+            shd_close(ctx);
+            return fail(SHD_ERR_HIP);
+        }
+        const char* v = std::getenv("SHD_SPIN_WAIT");
+        ctx->spin_wait = !(v && *v == '0');
     }
     // timing-only events: no system-scope fence (cache writeback + invalidate) when recorded --
     // with it each event cost ~5 us of queue gap beside C2's ~80 us kernel

@@ -164,6 +164,10 @@ struct PreparedGraph {
 
 struct shd_ctx;
 namespace shd {
+constexpr int kPinWords = 72;       // h_pin words; [64] is wait_stream's marker
+constexpr int kPinMarker = 64;
+// Wait until everything enqueued on stream s has finished (see api.cpp)
+shd_status wait_stream(shd_ctx* ctx, hipStream_t s);
 // a committed relay round's (all-rank) reductions: the runahead update (runahead.rs:60-115) and
 // the earliest deliver time of the relay output that the queues have not merged yet (rounds.cpp)
 void round_note(shd_ctx* ctx, uint64_t min_deliver, uint64_t min_latency);
@@ -178,7 +182,9 @@ struct shd_ctx {
     hipEvent_t ev[8] = {};
     hipStream_t side = nullptr;        // second stream: work that overlaps the main stream's
     hipEvent_t sev[2] = {};            // fork / join events (no timing)
-    unsigned long long* h_pin = nullptr;   // 64 pinned host words: flag / reduction read-backs
+    unsigned long long* h_pin = nullptr;   // shd::kPinWords pinned host words: flag / reduction read-backs
+    shd::DevBuf g_one;                     // a device word holding 1 (shd::wait_stream's marker)
+    bool spin_wait = true;                 // SHD_SPIN_WAIT=0: hipStreamSynchronize instead
     int n_cu = 0;
     size_t max_lds = 0;
 

@@ -429,8 +429,7 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
     SHD_HIP(hipGetLastError());
     eq_totals<<<1, 1024, 0, s>>>(H, nb, out_off, nrun ? nrun->off.as<uint32_t>() : nullptr, part, words);
     SHD_HIP(hipMemcpyAsync(ctx->h_pin + kEqPinWord, words, kEqWords * 8, hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
-    return SHD_OK;
+    return wait_stream(ctx, s);
 }
 
 static uint32_t* eq_cursor(EqState& Q, int buf, int slot) {

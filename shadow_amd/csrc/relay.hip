@@ -1919,7 +1919,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
                                            o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt);
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipMemcpyAsync(ctx->h_pin + 8, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
+    SHD_TRY(wait_stream(ctx, s));
     std::memcpy(R.red_host, ctx->h_pin + 8, sizeof(R.red_host));
     return SHD_OK;
 }
@@ -2007,7 +2007,7 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
                                              stop && *stop ? (uint32_t)std::atoi(stop) : 0u);
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipMemcpyAsync(ctx->h_pin + 8, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    SHD_HIP(hipStreamSynchronize(s));
+    SHD_TRY(wait_stream(ctx, s));
     std::memcpy(R.red_host, ctx->h_pin + 8, sizeof(R.red_host));
     return SHD_OK;
 }

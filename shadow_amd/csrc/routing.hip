@@ -405,6 +405,16 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
     }
 }
 
+#ifdef SHD_SSSP_PROF
+// tuning builds only (tools/sssp_prof.py): shader clocks per phase of the padded-list kernel,
+// summed over waves: init, bitmap scan, relaxation (flush), sweep end (reduce + barrier), output
+__device__ unsigned long long g_sssp_prof[8];
+#define SS_MARK(slot) do { if (PADR != 0 || FASTG) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    ss_acc[slot] += t_ - ss_t; ss_t = t_; } } while (0)
+#else
+#define SS_MARK(slot) do { } while (0)
+#endif
+
 // One source row: init, sweeps until nothing improves, emit the used columns.
 // FASTG (global labels): flat expansion + bucket bytes + one-barrier delta sweeps only (C4)
 template <int BLOCK, int G, int R, bool CACHE, bool GLAB, int PADR = 0, bool FASTG = false, bool FLATL = false>
@@ -428,6 +438,9 @@ __device__ __forceinline__ void sssp_row(
     const uint32_t grp = lane / G, gl = lane % G;
     uint32_t* q = wq + wave * kQStride;
     const uint32_t src = used[row];
+#ifdef SHD_SSSP_PROF
+    uint64_t ss_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ss_t = __builtin_amdgcn_s_memtime();
+#endif
     // PADR kernels run only delta-stepping with one-barrier sweeps and no seed (launch_group)
     const bool use_delta = PADR != 0 || FASTG || delta != kLat32Inf;
     // bucket bytes count steps of delta / kBktSub (global labels); the LDS kernels do not use them
@@ -480,6 +493,7 @@ __device__ __forceinline__ void sssp_row(
         if (fused) ctl[1] = ctl[2] = ctl[3] = kLat32Inf;
     }
     if (fused) __syncthreads();
+    SS_MARK(0);
     bool ovf = false;
     uint32_t expanded = 0, sweeps = 0;
     uint32_t slot = 0;   // fused: this sweep's accumulator, ctl[1 + slot]
@@ -515,6 +529,7 @@ __device__ __forceinline__ void sssp_row(
         uint32_t qn = 0;  // wave-uniform queue length
         // expand the queued nodes: NG nodes per step, G lanes each (or edge-parallel, global labels)
         auto flush = [&]() {
+            SS_MARK(1);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -551,6 +566,7 @@ __device__ __forceinline__ void sssp_row(
             }
             qn = 0;
             __builtin_amdgcn_wave_barrier();
+            SS_MARK(2);
         };
         // scan form: padded-list kernels (dense graphs, V <= kPruneMaxV) only the small-bitmap
         // one, global-label kernels (large V) only the lane-per-word one, so each kernel carries
@@ -632,10 +648,12 @@ __device__ __forceinline__ void sssp_row(
         }
         }
         ++sweeps;
+        SS_MARK(1);
         if (fused) {
             for (int o = 32; o > 0; o >>= 1) mnext = min(mnext, (uint32_t)__shfl_xor((int)mnext, o));
             if (lane == 0 && mnext != kLat32Inf) atomicMin(&ctl[1 + slot], mnext);
             __syncthreads();
+            SS_MARK(3);
             slot = slot == 2 ? 0 : slot + 1;
         } else if (!use_delta) {
             if (dirty) ctl[0] = 1;
@@ -718,6 +736,15 @@ __device__ __forceinline__ void sssp_row(
         __builtin_nontemporal_store(l, &out_lat[orow + j]);
         __builtin_nontemporal_store(p, &out_loss[orow + j]);
     }
+#ifdef SHD_SSSP_PROF
+    SS_MARK(4);
+    if ((PADR != 0 || FASTG) && lane == 0) {
+        for (int k = 0; k < 5; ++k) atomicAdd(&g_sssp_prof[k], (unsigned long long)ss_acc[k]);
+        atomicAdd(&g_sssp_prof[5], (unsigned long long)sweeps);
+        atomicAdd(&g_sssp_prof[6], (unsigned long long)expanded);
+        atomicAdd(&g_sssp_prof[7], 1ull);
+    }
+#endif
 }
 
 // Kernel 1: one workgroup per source row, labels (8 B/node) and the arc ranges in LDS.
@@ -1345,8 +1372,7 @@ static shd_status upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
 // one pinned read-back of the build flags (overflow word, first unreachable pair) and one sync
 static shd_status read_flags(shd_ctx* ctx) {
     SHD_HIP(hipMemcpyAsync(ctx->h_pin, ctx->g_flags.p, 24, hipMemcpyDeviceToHost, ctx->stream));
-    SHD_HIP(hipStreamSynchronize(ctx->stream));
-    return SHD_OK;
+    return wait_stream(ctx, ctx->stream);
 }
 static bool flag_ovf(const shd_ctx* ctx) { return (uint32_t)ctx->h_pin[0] != 0; }
 
@@ -2060,3 +2086,14 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
 }
 
 }  // namespace shd
+
+#ifdef SHD_SSSP_PROF
+extern "C" int shd_debug_sssp_prof(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(shd::g_sssp_prof), sizeof(unsigned long long) * 8) != hipSuccess) return 1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(shd::g_sssp_prof), z, sizeof(z)) != hipSuccess) return 1;
+    }
+    return 0;
+}
+#endif
