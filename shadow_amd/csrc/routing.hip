@@ -309,7 +309,7 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
                                              const uint32_t* __restrict__ aend, const uint2* __restrict__ arcs8,
                                              const float* __restrict__ aq, uint32_t* fx, bool& ovf, bool& dirty,
                                              uint8_t* bkt, float inv_delta, uint32_t& mnext, uint64_t* llab,
-                                             uint32_t kl) {
+                                             uint32_t kl, uint32_t* wmin) {
     uint32_t* pre = fx;          // [65]
     uint32_t* beg = fx + 65;     // [64]
     uint32_t* nl = fx + 129;     // [64] latency of the node's label
@@ -344,6 +344,8 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
             uint32_t lu[kFlatR], k[kFlatR], cl[kFlatR];
             float qu[kFlatR];
             bool ok[kFlatR], sure[kFlatR];
+            // (every round issues all kFlatR slots: skipping a short last round's empty slots
+            // behind wave-uniform branches measured slower, C4 rows 0-4095 17.2 -> 18.2 ms)
 #pragma unroll
             for (int r = 0; r < kFlatR; ++r) {
                 const uint32_t t = t0 + r * 64 + lane;
@@ -397,6 +399,8 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
                         bkt[a[r].x] = bk;
                         mnext = min(mnext, (uint32_t)(bk >> kBktShift));
                         atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
+                        // after the bit (sssp_row's word scan relies on this order)
+                        if (wmin) atomicMin(&wmin[a[r].x >> 5], (uint32_t)(bk >> kBktShift));
                     }
                 }
             }
@@ -429,7 +433,7 @@ __device__ __forceinline__ void sssp_row(
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
     uint32_t seed_stride, uint8_t* bkt, uint32_t* flat, uint32_t* nh_out, uint32_t* pred,
     uint32_t lat_guard, const uint2* __restrict__ arcs8 = nullptr, const float* __restrict__ aq = nullptr,
-    uint32_t* offl = nullptr, uint64_t* llab = nullptr, uint32_t kl = 0) {
+    uint32_t* offl = nullptr, uint64_t* llab = nullptr, uint32_t kl = 0, uint32_t* wmin = nullptr) {
     // bkt (global labels + delta-stepping): per node, the bucket of the latency that last
     // activated it, in LDS, so choosing a sweep's nodes reads no global label
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
@@ -470,6 +474,8 @@ __device__ __forceinline__ void sssp_row(
         else if (offl) offl[v] = abeg[v];
     }
     for (uint32_t w = tid; w < W; w += BLOCK) bits[w] = 0;
+    if (wmin)   // per bitmap word, a lower bound of its active nodes' bucket keys (none: +inf)
+        for (uint32_t w = tid; w < W; w += BLOCK) wmin[w] = w == (src >> 5) ? 0u : kLat32Inf;
     if (bkt)   // unreached: the top bucket (the relax filter never skips against it)
         for (uint32_t w = tid; w < (V + 3) / 4; w += BLOCK) reinterpret_cast<uint32_t*>(bkt)[w] = 0xFFFFFFFFu;
     if (offl && tid == 0) offl[V] = aend[V - 1];   // CSR: aend == abeg + 1
@@ -537,7 +543,7 @@ __device__ __forceinline__ void sssp_row(
             if constexpr (GLAB) {
                 if constexpr (FASTG) {
                     expand_flat8(q, qn, lane, lab, bits, abeg, aend, arcs8, aq, flat + wave * kFlatWords, ovf, dirty,
-                                 bkt, inv_delta, mnext, llab, kl);
+                                 bkt, inv_delta, mnext, llab, kl, wmin);
                 } else if (flat) {
                     expand_flat<GLAB>(q, qn, lane, lab, bits, nullptr, abeg, aend, arcs, flat + wave * kFlatWords,
                                       ovf, dirty, bkt, inv_delta, V + lane, mnext);
@@ -612,18 +618,37 @@ __device__ __forceinline__ void sssp_row(
             const bool more = k0 * NW + wave < W;   // wave-uniform: the wave has words in this batch
             const uint32_t widx = (k0 + lane) * NW + wave;
             uint32_t rem = 0;           // this lane's selected nodes not yet queued
-            if (more && widx < W) {
+            // Per-word minimum (wmin, global labels): a word whose active nodes all lie above
+            // the threshold is skipped on one LDS read instead of one bucket-byte read per active
+            // node -- most active nodes of a sparse graph wait many sweeps for their bucket.
+            // The scanning lane owns the word: it resets wmin, then reads the bits and puts the
+            // keys of those it leaves back; a relaxation sets the bit first and lowers wmin
+            // after, so every set bit is either seen by that read or lowers wmin afterwards.
+            bool scan_word = more && widx < W;
+            if (scan_word && wmin) {
+                const uint32_t m = __hip_atomic_load(&wmin[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (m > thr) {
+                    mnext = min(mnext, m);
+                    scan_word = false;
+                } else {
+                    atomicExch(&wmin[widx], kLat32Inf);
+                }
+            }
+            if (scan_word) {
                 const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (word) {
                     uint32_t selm = word;
                     if (use_delta) {
                         selm = 0;
+                        uint32_t rest = kLat32Inf;
                         for (uint32_t mm = word; mm; mm &= mm - 1) {
                             const uint32_t b = __builtin_ctz(mm);
                             const uint32_t key = act_key(widx * 32 + b);
                             if (key <= thr) selm |= 1u << b;
-                            else mnext = min(mnext, key);
+                            else rest = min(rest, key);
                         }
+                        mnext = min(mnext, rest);
+                        if (wmin && rest != kLat32Inf) atomicMin(&wmin[widx], rest);
                     }
                     if (selm) atomicAnd(&bits[widx], ~selm);
                     rem = selm;
@@ -713,28 +738,46 @@ __device__ __forceinline__ void sssp_row(
             __builtin_nontemporal_store(nh, &nh_out[orow + j]);
         }
     }
-    for (uint32_t j = tid; j < n_used; j += BLOCK) {
-        uint64_t l;
-        float p;
-        if (j == row) {
-            l = diag_lat[j];
-            p = diag_loss[j];
-        } else {
-            const uint32_t uj = used[j];
-            const uint64_t k = uj < kl ? llab[uj] : ld_lab<GLAB>(&lab[uj]);
-            if (k == kKeyInf) {
+#ifndef SHD_OUT_SINGLE   // (tuning A/B: one column per iteration)
+    constexpr uint32_t kOut = 4;   // columns per thread per iteration: their loads in flight together
+#else
+    constexpr uint32_t kOut = 1;
+#endif
+    for (uint32_t j0 = tid; j0 < n_used; j0 += kOut * BLOCK) {
+        uint32_t uj[kOut];
+        uint64_t k[kOut];
+#pragma unroll
+        for (uint32_t i = 0; i < kOut; ++i) {
+            const uint32_t j = j0 + i * BLOCK;
+            uj[i] = j < n_used ? used[j] : 0u;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kOut; ++i) {
+            const uint32_t j = j0 + i * BLOCK;
+            k[i] = j < n_used && j != row ? (uj[i] < kl ? llab[uj[i]] : ld_lab<GLAB>(&lab[uj[i]])) : 0ull;
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kOut; ++i) {
+            const uint32_t j = j0 + i * BLOCK;
+            if (j >= n_used) break;
+            uint64_t l;
+            float p;
+            if (j == row) {
+                l = diag_lat[j];
+                p = diag_loss[j];
+            } else if (k[i] == kKeyInf) {
                 atomicMin(unreach, (unsigned long long)((uint64_t)row * n_used + j));
                 l = ~0ull;
                 p = 0.0f;
             } else {
-                l = key_lat(k);
-                p = key_loss(k);
+                l = key_lat(k[i]);
+                p = key_loss(k[i]);
             }
+            // the table is written once and never read here: non-temporal stores keep it from
+            // evicting the label rows (C4: 600 KB of table per source row) from L2 / Infinity Cache
+            __builtin_nontemporal_store(l, &out_lat[orow + j]);
+            __builtin_nontemporal_store(p, &out_loss[orow + j]);
         }
-        // the table is written once and never read here: non-temporal stores keep it from
-        // evicting the label rows (C4: 600 KB of table per source row) from L2 / Infinity Cache
-        __builtin_nontemporal_store(l, &out_lat[orow + j]);
-        __builtin_nontemporal_store(p, &out_loss[orow + j]);
     }
 #ifdef SHD_SSSP_PROF
     SS_MARK(4);
@@ -808,10 +851,13 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     uint8_t* bkt = use_bkt ? reinterpret_cast<uint8_t*>(wq + (BLOCK / 64) * (kQStride + (use_flat ? kFlatWords : 0)))
                            : nullptr;
     uint64_t* lab = glab + (size_t)blockIdx.x * V;
-    // kl > 0 (FASTG, no next hops): the labels of nodes [0, kl) in LDS after the bucket bytes
+    // FASTG with use_flat bit 1: the per-word minimum keys (W words) after the bucket bytes
+    uint32_t* wmin = FASTG && use_bkt && (use_flat & 2u) ? reinterpret_cast<uint32_t*>(bkt + ((V + 3) / 4) * 4) : nullptr;
+    // kl > 0 (FASTG, no next hops): the labels of nodes [0, kl) in LDS after the bucket bytes (and wmin)
     uint64_t* llab = nullptr;
     if (FASTG && kl) {
-        const size_t at = ((size_t)((bkt + ((V + 3) / 4) * 4) - smem) + 7) & ~(size_t)7;
+        const unsigned char* end = wmin ? reinterpret_cast<unsigned char*>(wmin + W) : bkt + ((V + 3) / 4) * 4;
+        const size_t at = ((size_t)(end - smem) + 7) & ~(size_t)7;
         llab = reinterpret_cast<uint64_t*>(smem + at);
     }
     // row_ctr (zeroed before the launch): after its first row a slot takes the next unclaimed row,
@@ -823,7 +869,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_global_group(
                                            diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
                                            delta, stats, nullptr, 0, bkt, flat, nh_out,
                                            gpred ? gpred + (size_t)blockIdx.x * V : nullptr, 0u, arcs8, aq, nullptr,
-                                           llab, FASTG ? kl : 0u);
+                                           llab, FASTG ? kl : 0u, wmin);
         __syncthreads();   // the next row re-initialises labels and bitmap
         if (row_ctr) {
             if (threadIdx.x == 0) s_next = row_begin + gridDim.x + atomicAdd(row_ctr, 1u);
@@ -1745,6 +1791,12 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     const size_t lds_bkt = lds + ((size_t)P.V + 3) / 4 * 4;
     const uint32_t use_bkt = delta != kLat32Inf && lds_bkt <= ctx->max_lds && env_u32("SHD_SSSP_NO_BKT", 0) != 1;
     if (use_bkt) lds = lds_bkt;
+    // the flat + bucket-byte kernel (FASTG) keeps a per-word minimum key beside the bitmap
+    uint32_t flat_arg = use_flat;
+    if (use_bkt && use_flat && delta != kLat32Inf && env_u32("SHD_SSSP_WMIN", 1) != 0 && lds + (size_t)W * 4 <= ctx->max_lds) {
+        lds += (size_t)W * 4;
+        flat_arg |= 2u;
+    }
     const uint32_t per_cu = std::max<uint32_t>(1, env_u32("SHD_SSSP_SLOTS", 2));
     // labels of the first kl nodes (locality order: highest degree first) in the LDS left over by
     // per_cu slots per CU: their relaxations take LDS atomics instead of memory-side ones
@@ -1761,9 +1813,9 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
     const uint32_t G = env_u32("SHD_SSSP_G", deg >= 64 ? 16 : deg >= 24 ? 8 : 4);
     switch (G) {
-        case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
-        case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
-        default: launch_global<BLOCK, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, use_flat, kl); break;
+        case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, flat_arg, kl); break;
+        case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, flat_arg, kl); break;
+        default: launch_global<BLOCK, 4>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, flat_arg, kl); break;
     }
     SHD_HIP(hipGetLastError());
     (void)ovf;   // the caller reads the overflow flag with read_flags()
