@@ -312,6 +312,8 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
     const uint32_t n_chunks = !replicate && C.size > 1 && cs < per ? (uint32_t)((per + cs - 1) / cs) : 1u;
     shd_error e{SHD_OK, 0, 0};
     shd_status st = SHD_OK;
+    const char* sv = std::getenv("SHD_SHARD_RESERVE_SLOTS");
+    const uint32_t reserve = sv && *sv ? (uint32_t)std::strtoul(sv, nullptr, 10) : 32u;
     auto rows_of = [&](int q, uint32_t k) -> uint32_t {   // rank q's rows in chunk k
         uint32_t a = 0, z = 0;
         shard_range(n, C.size, q, &a, &z);
@@ -322,7 +324,12 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
         const uint32_t mine = n_chunks == 1 ? re - rb : rows_of(C.rank, k);
         const uint32_t a = rb + (n_chunks == 1 ? 0u : k * cs);
         const size_t at = replicate ? 0 : ((size_t)C.rank * per + (size_t)(a - rb)) * n;
+        // from the second chunk on, the previous chunk's exchange runs beside this build: leave
+        // some CUs a free slot for RCCL's workgroups (SHD_SHARD_RESERVE_SLOTS, default 32 of
+        // the global-label kernel's 2 per CU)
+        ctx->slot_reserve = k > 0 ? reserve : 0u;
         if (mine && st == SHD_OK) st = routing_run_impl(ctx, algo, a, a + mine, d_lat_full + at, d_loss_full + at, &e);
+        ctx->slot_reserve = 0;
         if (n_chunks == 1) break;
         // the build of this chunk has completed (routing_run_impl ends with a stream sync)
         std::vector<const void*> sp(4 * (size_t)C.size);

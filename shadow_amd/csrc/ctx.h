@@ -207,6 +207,10 @@ struct shd_ctx {
         g_dense, g_prune_dst, g_prune_cnt, g_labels, g_aux, g_arc16, g_arc8, g_aq, g_fw, g_glab, g_pred,
         g_offr, g_usedr, g_arc8r, g_aqr;   // locality-ordered copies (global-label kernel)
     uint32_t* nh_out = nullptr;   // next-hop rows of the running build (shd_routing_run_next_hops)
+    // global-label slots left unlaunched while a sharded build's previous chunk is still being
+    // exchanged on the side stream: the persistent kernel fills every CU's LDS, so RCCL's
+    // send/recv workgroups would otherwise wait for it to finish (shd_routing_run_sharded)
+    uint32_t slot_reserve = 0;
 
     std::unique_ptr<shd::Comm> comm;   // multi-GPU communicator (shd_comm_init*), or none
     shd::DevBuf comm_scratch;

@@ -1807,7 +1807,9 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
         if (room > lds + 64) kl = std::min<uint32_t>(std::min<uint32_t>(P.V, P.lds_labels), (uint32_t)((room - lds - 16) / 8)) & ~63u;
         if (kl) lds = ((lds + 7) & ~(size_t)7) + (size_t)kl * 8;
     }
-    const uint32_t grid = std::min<uint32_t>(re - rb, (uint32_t)ctx->n_cu * per_cu);
+    const uint32_t slots = (uint32_t)ctx->n_cu * per_cu;
+    const uint32_t reserve = std::max(ctx->slot_reserve, env_u32("SHD_SSSP_RESERVE", 0));   // env: tools/overlap_probe.py
+    const uint32_t grid = std::min<uint32_t>(re - rb, slots - std::min(reserve, slots / 2));
     SHD_TRY(ctx->g_glab.ensure((size_t)grid * P.V * 8));
     if (ctx->nh_out) SHD_TRY(ctx->g_pred.ensure((size_t)grid * P.V * 4));
     const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
