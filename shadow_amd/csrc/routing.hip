@@ -579,9 +579,51 @@ __device__ __forceinline__ void sssp_row(
         // one loop (fewer registers)
         // (plain chaotic sweeps, no delta, keep the word-per-step form: C3 SSSP 11.2 ms against
         // 17.4 with lane-per-word, whose frontier there is dense)
-        constexpr int kScan = PADR != 0 ? 1 : GLAB ? 2 : 0;   // 1 small, 2 lane, 0 by W / delta
+#ifndef SHD_SCAN_WORDSTEP   // (tuning A/B: padded-list kernels back on the word-per-step scan)
+        constexpr int kScan = PADR != 0 ? 3 : GLAB ? 2 : 0;   // 3 nibbles, 2 lane, 0 by W / delta
+#else
+        constexpr int kScan = PADR != 0 ? 1 : GLAB ? 2 : 0;
+#endif
         const bool lane_scan = kScan == 2 || (kScan == 0 && use_delta && W > NW * 16);
-        if (!lane_scan) {
+        if constexpr (kScan == 3) {
+            // small bitmap, bits in parallel (padded lists, C2: 32 words over 4 waves): a wave
+            // takes 8 of its words at once, each lane 4 bits of one, so the key reads of all 8
+            // words are in flight together -- one LDS round trip per 256 bits instead of one per
+            // word step (the word-per-step form used half the lanes, one word at a time)
+            for (uint32_t k0 = 0;; k0 += 8) {
+                const bool more = k0 * NW + wave < W;   // wave-uniform
+                const uint32_t widx = (k0 + (lane >> 3)) * NW + wave, nb = (lane & 7) * 4;
+                uint32_t sel4 = 0;
+                if (more && widx < W) {
+                    const uint32_t word = __hip_atomic_load(&bits[widx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    const uint32_t nib = (word >> nb) & 0xFu;
+                    uint32_t key[4];
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i)
+                        key[i] = (nib >> i) & 1u ? act_key(widx * 32 + nb + i) : kLat32Inf;
+#pragma unroll
+                    for (uint32_t i = 0; i < 4; ++i) {
+                        if (key[i] <= thr) sel4 |= 1u << i;
+                        else mnext = min(mnext, key[i]);
+                    }
+                    // words are owned by one wave; other waves only set bits: clearing is exact
+                    if (sel4) atomicAnd(&bits[widx], ~(sel4 << nb));
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < 4; ++i) {
+                    const bool has = (sel4 >> i) & 1u;
+                    const uint64_t bal = __ballot(has);
+                    if (bal == 0) continue;   // wave-uniform
+                    if (has) q[qn + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = widx * 32 + nb + i;
+                    qn += (uint32_t)__popcll(bal);
+                    if (qn >= kQCap) flush();
+                }
+                if (!more) {
+                    if (qn > 0) flush();
+                    break;
+                }
+            }
+        } else if (!lane_scan) {
             // small bitmap (C2: 32 words over 4 waves): a word per wave step, lane per bit
             for (uint32_t widx = wave;; widx += NW) {
                 const bool more = widx < W;
