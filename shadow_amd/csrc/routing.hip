@@ -2119,8 +2119,10 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
                   P.arcs};
         if (prune) {
             SHD_TRY(run_prune(ctx, &A));
-            // the kept-arc count steers the lane-group width; it is known after the first build
-            A.n_arcs = P.pruned_arcs ? P.pruned_arcs : (uint64_t)P.V * 64;
+            // the kept-arc count steers the lane-group width: counted once per prepared graph,
+            // before its first SSSP launch, so every build (the first too) runs the same kernel
+            if (P.pruned_arcs == 0) SHD_TRY(count_kept(ctx, A));
+            A.n_arcs = P.pruned_arcs;
         }
         bool ovf = false;
         // delta-stepping bucket width (env override for tuning).  SHD_ALGO_DELTA: the mean arc
@@ -2146,7 +2148,6 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         ms_main = main_ms(ctx);
         ctx->info.ms_total = ms;
         ctx->info.ms_main = ms_main;
-        if (prune && P.pruned_arcs == 0) SHD_TRY(count_kept(ctx, A));  // once per prepared graph
         ctx->info.arcs_kept = prune ? P.pruned_arcs : P.arcs;
         if (!ovf) return check_unreach(ctx, err);
         SHD_TRY(reset_flags(ctx));  // some path latency >= 2^32-1 ns: redo with u64 labels

@@ -109,6 +109,36 @@ def test_c2_full_bit_exact(engine, c2_case, algo):
     assert engine.smallest_latency_ns() == int(lat.min())
 
 
+@pytest.mark.parametrize("group", ["", "8", "4"])
+def test_c2_repeated_runs_bit_exact(engine, c2_case, group, monkeypatch):
+    """Prepare once, run several builds: from the second on the engine knows the pruned arc count,
+    so AUTO picks the padded-list kernel (sssp_lds_group<..., 8>) -- the C2 headline kernel, which
+    a single shd_routing_build never reaches (its first run sizes the lane groups on the unpruned
+    degree).  Every build against the C restatement; also with the lane-group width forced."""
+    import ctypes as C
+
+    import torch
+
+    from shadow_amd import _native as N
+    if group:
+        monkeypatch.setenv("SHD_SSSP_G", group)
+    el, used, lat, loss = c2_case
+    g = engine_graph_from_edges(el)._cgraph()
+    err = N.Error()
+    N.check(engine.lib.shd_routing_prepare(engine.ctx, C.byref(g), N.ptr(used), len(used), N.ROUTE_SHORTEST,
+                                           C.byref(err)), "prepare", err)
+    n = len(used)
+    dl = torch.empty((n, n), dtype=torch.int64, device="cuda")
+    dp = torch.empty((n, n), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(3):
+        N.check(engine.lib.shd_routing_run(engine.ctx, N.ALGO_AUTO, 0, n, N.ptr(dl), N.ptr(dp), C.byref(err)),
+                "shd_routing_run", err)
+        assert engine.last_info()["algo_used"] == N.ALGO_PRUNED
+        assert np.array_equal(dl.cpu().numpy().view(np.uint64), lat)
+        assert np.array_equal(dp.cpu().numpy().view(np.uint32), loss.view(np.uint32))
+
+
 def test_c3_rows_bit_exact(engine):
     """BASELINE config 3 (10k-node BA graph): a row slice against the C restatement."""
     from shadow_amd import synth
