@@ -413,7 +413,7 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
 // tuning builds only (tools/sssp_prof.py): shader clocks per phase of the padded-list kernel,
 // summed over waves: init, bitmap scan, relaxation (flush), sweep end (reduce + barrier), output
 __device__ unsigned long long g_sssp_prof[8];
-#define SS_MARK(slot) do { if (PADR != 0 || FASTG) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+#define SS_MARK(slot) do { if (true) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
     ss_acc[slot] += t_ - ss_t; ss_t = t_; } } while (0)
 #else
 #define SS_MARK(slot) do { } while (0)
@@ -579,17 +579,20 @@ __device__ __forceinline__ void sssp_row(
         // one loop (fewer registers)
         // (plain chaotic sweeps, no delta, keep the word-per-step form: C3 SSSP 11.2 ms against
         // 17.4 with lane-per-word, whose frontier there is dense)
-#ifndef SHD_SCAN_WORDSTEP   // (tuning A/B: padded-list kernels back on the word-per-step scan)
-        constexpr int kScan = PADR != 0 ? 3 : GLAB ? 2 : 0;   // 3 nibbles, 2 lane, 0 by W / delta
+#ifndef SHD_SCAN_WORDSTEP   // (tuning A/B: the LDS kernels back on the word-per-step / lane-per-word scans)
+        constexpr int kScan = GLAB ? 2 : 3;   // 3 nibbles (LDS labels), 2 lane per word (global labels)
 #else
         constexpr int kScan = PADR != 0 ? 1 : GLAB ? 2 : 0;
 #endif
         const bool lane_scan = kScan == 2 || (kScan == 0 && use_delta && W > NW * 16);
-        if constexpr (kScan == 3) {
-            // small bitmap, bits in parallel (padded lists, C2: 32 words over 4 waves): a wave
+        // (plain chaotic sweeps on an unpruned graph keep the word-per-step form: C2 SSSP 2.65 ms
+        // against 2.95 with nibbles; the seeded loss pass of the blocked engine takes nibbles)
+        if (kScan == 3 && (use_delta || seed)) {
+            // bits in parallel (LDS labels; C2: 32 words over 4 waves, C3: 313 over 16): a wave
             // takes 8 of its words at once, each lane 4 bits of one, so the key reads of all 8
             // words are in flight together -- one LDS round trip per 256 bits instead of one per
-            // word step (the word-per-step form used half the lanes, one word at a time)
+            // word step (the word-per-step form used half the lanes, one word at a time; the
+            // lane-per-word form walked a word's bits one dependent read after another)
             for (uint32_t k0 = 0;; k0 += 8) {
                 const bool more = k0 * NW + wave < W;   // wave-uniform
                 const uint32_t widx = (k0 + (lane >> 3)) * NW + wave, nb = (lane & 7) * 4;
@@ -600,9 +603,10 @@ __device__ __forceinline__ void sssp_row(
                     uint32_t key[4];
 #pragma unroll
                     for (uint32_t i = 0; i < 4; ++i)
-                        key[i] = (nib >> i) & 1u ? act_key(widx * 32 + nb + i) : kLat32Inf;
+                        key[i] = (nib >> i) & 1u ? (use_delta ? act_key(widx * 32 + nb + i) : 0u) : kLat32Inf;
 #pragma unroll
                     for (uint32_t i = 0; i < 4; ++i) {
+                        if (!((nib >> i) & 1u)) continue;   // (thr is +inf in plain chaotic sweeps)
                         if (key[i] <= thr) sel4 |= 1u << i;
                         else mnext = min(mnext, key[i]);
                     }
@@ -823,7 +827,7 @@ __device__ __forceinline__ void sssp_row(
     }
 #ifdef SHD_SSSP_PROF
     SS_MARK(4);
-    if ((PADR != 0 || FASTG) && lane == 0) {
+    if (lane == 0) {
         for (int k = 0; k < 5; ++k) atomicAdd(&g_sssp_prof[k], (unsigned long long)ss_acc[k]);
         atomicAdd(&g_sssp_prof[5], (unsigned long long)sweeps);
         atomicAdd(&g_sssp_prof[6], (unsigned long long)expanded);
