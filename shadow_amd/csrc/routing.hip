@@ -1156,13 +1156,19 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
         }
     }
     __syncthreads();
-    // rows land contiguously (in any row order) so the kept arcs stay dense in L2; each list is
-    // padded to kArcPad slots with no-op arcs for relax_node_pad (scratch label V + i, lat 0,
-    // q 0: candidate (lu, 1.0f) against a scratch label holding 0)
+    // each list is padded to kArcPad slots with no-op arcs for relax_node_pad (scratch label
+    // V + i, lat 0, q 0: candidate (lu, 1.0f) against a scratch label holding 0).  Row u's list
+    // starts at u * roundup(V, kArcPad): the 1000 workgroups of C2 finish together, and one
+    // shared cursor (rows packed in arrival order) serialised their atomics at the end of the
+    // kernel; the slots a sweep touches are the same lines either way.
     const uint32_t n = cnt[0], np = (n + kArcPad - 1) / kArcPad * kArcPad;
+#ifdef SHD_PRUNE_CURSOR   // (tuning A/B: rows packed by one atomic cursor)
     if (tid == 0) cnt[1] = atomicAdd(cursor, np);
     __syncthreads();
     const uint32_t at = cnt[1];
+#else
+    const uint32_t at = u * ((V + kArcPad - 1) / kArcPad * kArcPad);
+#endif
     for (uint32_t i = tid; i < np; i += BLOCK)
         parcs[at + i] = i < n ? kept[i] : make_uint4(V + (i & 63u), 0u, 0u, 0u);
     if (tid == 0) {
