@@ -918,6 +918,35 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     min_l = wave_min_u64(min_l);
     for (int o = 32; o > 0; o >>= 1) ns_total += __shfl_xor(ns_total, o);
     const bool any_wide = __ballot(wide) != 0, any_disorder = __ballot(disorder) != 0;
+#ifndef SHD_RED_PER_WAVE   // (tuning A/B: one set of global atomics per wave)
+    // the workgroup's 16 waves combine in LDS first: one atomic per word per workgroup instead of
+    // per wave -- the grid's waves all end together, and 4096 atomics on the same few words
+    // serialise at the memory side (~12 ns each)
+    __shared__ unsigned long long s_red[3][kS6Threads / 64];
+    __shared__ uint32_t s_flag[kS6Threads / 64];
+    if (lane == 0) {
+        s_red[0][w] = min_d;
+        s_red[1][w] = min_l;
+        s_red[2][w] = ns_total;
+        s_flag[w] = (any_wide ? 1u : 0u) | (any_disorder ? 2u : 0u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        unsigned long long md = ~0ull, ml = ~0ull, ns = 0;
+        uint32_t fl = 0;
+        for (uint32_t k = 0; k < kS6Threads / 64; ++k) {
+            md = s_red[0][k] < md ? s_red[0][k] : md;
+            ml = s_red[1][k] < ml ? s_red[1][k] : ml;
+            ns += s_red[2][k];
+            fl |= s_flag[k];
+        }
+        if (md != ~0ull) atomicMin(&a.red[0], md);
+        if (ml != ~0ull) atomicMin(&a.red[1], ml);
+        if (ns) atomicAdd(&a.red[2], ns);
+        if (fl & 1u) atomicOr(&a.red[4], 1ull);
+        if (fl & 2u) atomicOr(&a.red[5], 1ull);
+    }
+#else
     if (lane == 0) {
         if (min_d != ~0ull) atomicMin(&a.red[0], (unsigned long long)min_d);
         if (min_l != ~0ull) atomicMin(&a.red[1], (unsigned long long)min_l);
@@ -925,6 +954,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
         if (any_wide) atomicOr(&a.red[4], 1ull);
         if (any_disorder) atomicOr(&a.red[5], 1ull);
     }
+#endif
 }
 
 // the bit-packed host -> node map for relay_stamp_v6 (built at setup)
