@@ -582,6 +582,7 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=16, timed=8, cpu=False):
     qo = N.EqueueOut()
     start0 = start = rl["start"]
     t_relay = t_adv = 0.0
+    adv_each = []   # per timed round: a round that compacts the stored runs takes longer
     pops = pend = bytes_merge = n_sent_t = 0
     b = rl["batch"]
     d = [_dev(b.src_off, np.int32), _dev(b.send_time, np.int64), _dev(b.dst_host, np.int32),
@@ -604,6 +605,7 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=16, timed=8, cpu=False):
         if k >= rounds - timed:
             t_relay += t1 - t0
             t_adv += t2 - t1
+            adv_each.append(round((t2 - t1) * 1e3, 4))
             pops += qo.n_popped
             pend += qo.n_pending
             n_sent_t += out.n_sent
@@ -624,7 +626,7 @@ def equeue_leg(eng, rl, lat_table, loss_table, rounds=16, timed=8, cpu=False):
     ach = algo / (ms * 1e-3) / 1e9
     res = {"workload": "C5 rounds: relay + shd_equeue_advance (merge into the pending destination queues, pop "
                        "the next 1 ms window)", "rounds": rounds, "timed_rounds": timed,
-           "relay_ms_per_round": t_relay / timed * 1e3, "advance_ms_per_round": t_adv / timed * 1e3,
+           "relay_ms_per_round": t_relay / timed * 1e3, "advance_ms_per_round": t_adv / timed * 1e3, "advance_ms_each": adv_each,
            "ms_per_round": ms, "value": P / (ms * 1e-3), "unit": "packets relayed + merged/s",
            "popped_per_round": pops / timed, "pending_mean": pend / timed,
            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
