@@ -966,15 +966,17 @@ __global__ __launch_bounds__(64) void flags_init(uint32_t* __restrict__ f) {
 }
 
 // One workgroup per row u: the row's arc keys (parallel arcs folded by a lexicographic LDS
-// atomicMin) built in LDS and written once as the key row Wk and the latency row Wl -- one
-// pass instead of init + global-atomic scatter + a latency-extract pass (C2: 16 -> 7 us).
+// atomicMin) built in LDS and written once as the latency row Wl and the loss row Wp -- one
+// pass instead of init + global-atomic scatter + a latency-extract pass (C2: 16 -> 7 us); the
+// prune reads its own row's latencies from Wl and the loss only of the arcs it keeps, so the
+// 8-byte key row is not written (round 3).
 // (A u16 latency row rounded up -- sound for the prune, half the gathered bytes -- measured
 // slower: prune_rows 32 -> 57 us, the decode outweighing the bytes.)
 __global__ __launch_bounds__(256) void dense_build(const uint32_t* __restrict__ off,
                                                    const uint32_t* __restrict__ adst,
                                                    const uint32_t* __restrict__ alat,
                                                    const float* __restrict__ aloss, uint32_t V,
-                                                   uint64_t* __restrict__ Wk, uint32_t* __restrict__ Wl,
+                                                   float* __restrict__ Wp, uint32_t* __restrict__ Wl,
                                                    uint32_t* __restrict__ cursor, uint32_t* __restrict__ flags) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t* rowk = reinterpret_cast<uint64_t*>(smem);
@@ -989,14 +991,14 @@ __global__ __launch_bounds__(256) void dense_build(const uint32_t* __restrict__ 
     const size_t base = (size_t)u * V;
     for (uint32_t v = tid; v < V; v += 256) {
         const uint64_t k = rowk[v];
-        Wk[base + v] = k;
+        Wp[base + v] = key_loss(k);
         Wl[base + v] = key_lat(k);
     }
 }
 
 template <int BLOCK, int K>
 __global__ __launch_bounds__(BLOCK) void prune_rows(
-    const uint32_t* __restrict__ Wl, const uint64_t* __restrict__ Wk, uint32_t V,
+    const uint32_t* __restrict__ Wl, const float* __restrict__ Wp, uint32_t V,
     uint32_t* __restrict__ pbeg, uint32_t* __restrict__ pend, uint4* __restrict__ parcs,
     uint32_t* __restrict__ cursor) {
     // Detour nodes x: ~K of u's lowest-latency neighbours, chosen by a 256-bin latency histogram
@@ -1014,7 +1016,7 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
     uint16_t* binv = reinterpret_cast<uint16_t*>(row + V);   // bin per node (0xFFFF: no arc)
     const uint32_t u = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const size_t base = (size_t)u * V;
-    for (uint32_t v = tid; v < V; v += BLOCK) row[v] = key_lat(Wk[base + v]);
+    for (uint32_t v = tid; v < V; v += BLOCK) row[v] = Wl[base + v];
     for (uint32_t i = tid; i < 256; i += BLOCK) hist[i] = 0;
     if (tid < 8) cnt[tid] = 0;
     uint32_t mx = 0;
@@ -1151,8 +1153,7 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
             if (w[i] == kLat32Inf || w[i] > z[i]) continue;
             const uint32_t v = v0 + i * BLOCK;
             const uint32_t slot = atomicAdd(&cnt[0], 1u);
-            const uint64_t key = Wk[base + v];
-            kept[slot] = make_uint4(v, w[i], __float_as_uint(one_minus(key_loss(key))), 0u);
+            kept[slot] = make_uint4(v, w[i], __float_as_uint(one_minus(Wp[base + v])), 0u);
         }
     }
     __syncthreads();
@@ -1938,22 +1939,22 @@ static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
     SHD_TRY(ctx->g_labels.ensure(nn * 4));
     SHD_TRY(ctx->g_prune_dst.ensure((nn + (uint64_t)V * kArcPad) * 16));   // + list padding
     SHD_TRY(ctx->g_prune_cnt.ensure((size_t)V * 8 + 16));
-    uint64_t* Wk = ctx->g_dense.as<uint64_t>();
+    float* Wp = ctx->g_dense.as<float>();   // the lexicographic-min arc's loss per pair (its latency: Wl)
     uint32_t* Wl = ctx->g_labels.as<uint32_t>();
     uint32_t* pbeg = ctx->g_prune_cnt.as<uint32_t>();
     uint32_t* pend = pbeg + V;
     uint32_t* cursor = pend + V;
     uint4* pa = ctx->g_prune_dst.as<uint4>();
     dense_build<<<V, 256, (size_t)V * 8, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
-                                              ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wk, Wl, cursor,
+                                              ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wp, Wl, cursor,
                                               ctx->g_flags.as<uint32_t>());
     const char* pk = std::getenv("SHD_PRUNE_K");   // tuning: detour nodes per row (same output tables)
     const uint32_t Kr = pk && *pk ? (uint32_t)std::atoi(pk) : kPruneK;
     const uint32_t K = Kr >= 128 ? 128u : Kr >= 64 ? 64u : 32u;
     const size_t plds = (size_t)V * 22 + (8 + 256 + 2 * (size_t)K) * 4;
-    if (K >= 128) prune_rows<256, 128><<<V, 256, plds, s>>>(Wl, Wk, V, pbeg, pend, pa, cursor);
-    else if (K >= 64) prune_rows<256, 64><<<V, 256, plds, s>>>(Wl, Wk, V, pbeg, pend, pa, cursor);
-    else prune_rows<256, 32><<<V, 256, plds, s>>>(Wl, Wk, V, pbeg, pend, pa, cursor);
+    if (K >= 128) prune_rows<256, 128><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor);
+    else if (K >= 64) prune_rows<256, 64><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor);
+    else prune_rows<256, 32><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor);
     SHD_HIP(hipGetLastError());
     *out = ArcView{pbeg, pend, ctx->g_prune_dst.as<uint4>(), 0, true};
     return SHD_OK;
