@@ -109,6 +109,15 @@ void shd_close(shd_ctx* ctx);
 /* Stream for all device work of this context (a hipStream_t passed as void*; NULL => the
  * context's own stream).  Lets a caller order the engine behind its own stream. */
 shd_status shd_set_stream(shd_ctx* ctx, void* hip_stream);
+/* Tuning and testing knobs of this context (no reference counterpart).  No knob changes a result:
+ * they pick grids, kernel variants or an equivalent fallback pipeline.  Every knob starts from the
+ * environment variable SHD_<name>, read ONCE by shd_open, so the process environment cannot change
+ * a context's grids between two calls; shd_set_knob overrides one for this context (value < 0: back
+ * to the built-in default), shd_get_knob reads it (-1: the built-in default applies).  `name` is
+ * spelled with or without the SHD_ prefix (e.g. "SSSP_SLOTS"); an unknown name is SHD_ERR_INVALID.
+ * Relay pipeline knobs (RELAY_FORCE_*, RELAY_NO_LDS_MAP) apply from the next shd_relay_setup. */
+shd_status shd_set_knob(shd_ctx* ctx, const char* name, int64_t value);
+shd_status shd_get_knob(const shd_ctx* ctx, const char* name, int64_t* value);
 
 /* ---------------------------------------------------------------- routing build */
 /*

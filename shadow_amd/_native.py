@@ -37,6 +37,7 @@ EXPORTED = [
     "shd_routing_run_next_hops", "shd_assign_ips", "shd_gml_load",
     "shd_runahead_setup", "shd_runahead_get", "shd_round_window", "shd_window_compute", "shd_copy_to_host",
     "shd_routing_lookup_batch", "shd_routing_mirror", "shd_equeue_batch_buffers",
+    "shd_set_knob", "shd_get_knob",
 ]
 COMM_ID_BYTES = 128
 
@@ -184,6 +185,8 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_routing_lookup_batch": (I32, [P, U64, P, P, P, P]),
         "shd_routing_mirror": (I32, [P, I32]),
         "shd_equeue_batch_buffers": (I32, [P, U64, P]),
+        "shd_set_knob": (I32, [P, C.c_char_p, C.c_int64]),
+        "shd_get_knob": (I32, [P, C.c_char_p, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

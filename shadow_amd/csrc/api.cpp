@@ -102,10 +102,9 @@ shd_ctx* shd_open(int device_ordinal, shd_status* st) {
     ctx->device = device_ordinal;
     ctx->n_cu = prop.multiProcessorCount;
     ctx->max_lds = prop.sharedMemPerBlock;
-    {
-        const char* v = std::getenv("SHD_SSSP_STATS");
-        ctx->stats_on = v && *v == '1';
-    }
+    // every knob is read from the environment here, once (knobs.h); shd_set_knob changes them later
+    ctx->knobs.from_env();
+    ctx->stats_on = ctx->knobs.on(K_SSSP_STATS);
     if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return fail(SHD_ERR_HIP);
@@ -124,8 +123,7 @@ shd_ctx* shd_open(int device_ordinal, shd_status* st) {
             shd_close(ctx);
             return fail(SHD_ERR_HIP);
         }
-        const char* v = std::getenv("SHD_SPIN_WAIT");
-        ctx->spin_wait = !(v && *v == '0');
+        ctx->spin_wait = ctx->knobs.get(K_SPIN_WAIT, 1) != 0;
     }
     // timing-only events: no system-scope fence (cache writeback + invalidate) when recorded --
     // with it each event cost ~5 us of queue gap beside C2's ~80 us kernel
@@ -274,9 +272,8 @@ shd_status shd_routing_build(shd_ctx* ctx, const shd_graph* g, const uint32_t* u
 // (C4 at 8 ranks: 3.75 GB per rank in ~15 chunks), at least 4 chunks once a rank's share passes
 // 256 MB; SHD_SHARD_CHUNK_ROWS overrides (tests use it to exercise the chunked path on small
 // graphs).
-static uint64_t env_chunk_rows(uint64_t per, uint64_t row_bytes, int ranks) {
-    const char* v = std::getenv("SHD_SHARD_CHUNK_ROWS");
-    if (v && *v) return std::max<uint64_t>(1, std::strtoull(v, nullptr, 10));
+static uint64_t chunk_rows(const shd_ctx* ctx, uint64_t per, uint64_t row_bytes, int ranks) {
+    if (ctx->knobs.set(K_SHARD_CHUNK_ROWS)) return std::max<uint64_t>(1, ctx->knobs.get64(K_SHARD_CHUNK_ROWS, 1));
     if (ranks <= 1 || per * row_bytes <= (256ull << 20)) return per;
     const uint64_t by_size = std::max<uint64_t>(1, (256ull << 20) / std::max<uint64_t>(row_bytes, 1));
     return std::min<uint64_t>(by_size, (per + 3) / 4);
@@ -303,17 +300,15 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
     // (~10 MB over xGMI plus the all-gather's latency) costs more than the rows it would save.
     // Every rank prepared the same graph and gets the same table; the status agreement below
     // still runs, so a failure on one rank (allocation) fails every rank.
-    const char* rv = std::getenv("SHD_SHARD_REPLICATE_MB");
-    const uint64_t rep_bytes = (rv && *rv ? std::strtoull(rv, nullptr, 10) : 64ull) << 20;
+    const uint64_t rep_bytes = ctx->knobs.get64(K_SHARD_REPLICATE_MB, 64) << 20;
     const bool replicate = C.size > 1 && (uint64_t)n * row_bytes <= rep_bytes;
     if (replicate) { rb = 0; re = n; }
-    const uint64_t want = env_chunk_rows(per, row_bytes, C.size);
+    const uint64_t want = chunk_rows(ctx, per, row_bytes, C.size);
     const uint32_t cs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(per, want));
     const uint32_t n_chunks = !replicate && C.size > 1 && cs < per ? (uint32_t)((per + cs - 1) / cs) : 1u;
     shd_error e{SHD_OK, 0, 0};
     shd_status st = SHD_OK;
-    const char* sv = std::getenv("SHD_SHARD_RESERVE_SLOTS");
-    const uint32_t reserve = sv && *sv ? (uint32_t)std::strtoul(sv, nullptr, 10) : 32u;
+    const uint32_t reserve = ctx->knobs.get(K_SHARD_RESERVE_SLOTS, 32);
     auto rows_of = [&](int q, uint32_t k) -> uint32_t {   // rank q's rows in chunk k
         uint32_t a = 0, z = 0;
         shard_range(n, C.size, q, &a, &z);
@@ -375,6 +370,24 @@ shd_status shd_routing_run_sharded(shd_ctx* ctx, uint32_t algo, uint64_t* d_lat_
         SHD_TRY(C.all_gather(d_loss_full + (size_t)C.rank * per * n, d_loss_full, per * n * 4, s));
         SHD_HIP(hipStreamSynchronize(s));
     }
+    return SHD_OK;
+}
+
+shd_status shd_set_knob(shd_ctx* ctx, const char* name, int64_t value) {
+    if (!ctx) return SHD_ERR_INVALID;
+    const int k = Knobs::find(name);
+    if (k < 0) return SHD_ERR_INVALID;
+    ctx->knobs.v[k] = value < 0 ? -1 : value;
+    ctx->stats_on = ctx->knobs.on(K_SSSP_STATS);
+    ctx->spin_wait = ctx->knobs.get(K_SPIN_WAIT, 1) != 0;
+    return SHD_OK;
+}
+
+shd_status shd_get_knob(const shd_ctx* ctx, const char* name, int64_t* value) {
+    if (!ctx || !value) return SHD_ERR_INVALID;
+    const int k = Knobs::find(name);
+    if (k < 0) return SHD_ERR_INVALID;
+    *value = ctx->knobs.v[k];
     return SHD_OK;
 }
 

@@ -5,6 +5,7 @@
 
 #include "comm.h"
 #include "common.h"
+#include "knobs.h"
 
 namespace shd {
 
@@ -68,6 +69,7 @@ struct EqRunBuf {   // one stored run of the event queues: a CSR of per-host sor
 struct EqState {   // destination event queues (equeue.hip): a list of sorted runs (one per batch)
     EqRunBuf run[kEqSlots];         // slots
     int lend = -1;                  // the slot handed out by shd_equeue_batch_buffers (not live yet)
+    uint64_t lend_cap = 0;          // events the lent slot holds
     DevBuf curs[2];                 // [kEqSlots][n_hosts] u32 cursors (first unpopped), double-buffered
     DevBuf bcut;                    // [n_hosts] the batch's first kept event per host
     DevBuf pd, ps, pq, pt;          // the last call's popped events
@@ -139,6 +141,7 @@ struct PreparedGraph {
     bool ready = false;
     uint32_t mode = 0, V = 0, n_used = 0;
     bool directed = false, narrow_arcs = false;
+    bool dense_rows = false;  // the arc CSR is the complete graph's dense matrix (routing.hip csr_is_dense)
     uint64_t arcs = 0, max_arc_lat = 0, pruned_arcs = 0, tight_arcs = 0;
     uint32_t mean_arc_lat = 1, min_arc_lat = 1;
     bool reordered = false;   // g_offr / g_usedr / g_arc8r / g_aqr hold the locality order
@@ -185,6 +188,7 @@ struct shd_ctx {
     unsigned long long* h_pin = nullptr;   // shd::kPinWords pinned host words: flag / reduction read-backs
     shd::DevBuf g_one;                     // a device word holding 1 (shd::wait_stream's marker)
     bool spin_wait = true;                 // SHD_SPIN_WAIT=0: hipStreamSynchronize instead
+    shd::Knobs knobs;                      // tuning / testing knobs (knobs.h), from the env at shd_open
     int n_cu = 0;
     size_t max_lds = 0;
 

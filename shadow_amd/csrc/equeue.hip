@@ -409,11 +409,8 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
     const uint32_t H = Q.n_hosts;
     unsigned long long* words = Q.next.as<unsigned long long>();
     unsigned long long* part = words + kEqWords;
-    static const uint32_t grid_max = [] {
-        const char* v = std::getenv("SHD_EQ_COUNT_BLOCKS");
-        const unsigned long x = v ? std::strtoul(v, nullptr, 10) : 0ul;
-        return x >= 1 && x <= kEqCountBlocksMax ? (uint32_t)x : kEqCountBlocks;
-    }();
+    const uint32_t gx = ctx->knobs.get(K_EQ_COUNT_BLOCKS, 0);
+    const uint32_t grid_max = gx >= 1 && gx <= kEqCountBlocksMax ? gx : kEqCountBlocks;
     const uint32_t nb = std::min<uint32_t>(grid_max, div_up(((uint64_t)H + 1) * kEqLanes, 256));
     SHD_TRY(Q.ranges.ensure((size_t)H * kEqSrcMax * 8));
     eqr_count<<<nb, 256, 0, s>>>(H, S, window_end, Q.pop_cnt.as<uint32_t>(), Q.keep_cnt.as<uint32_t>(), part,
@@ -532,6 +529,7 @@ shd_status shd_equeue_setup(shd_ctx* ctx, uint32_t n_total) {
     Q.n_pending = 0;
     Q.n_popped = 0;
     Q.batches = 0;
+    ctx->rnd.batch_min_deliver = ~0ull;   // new queues: no relay output is pending for them
     Q.ready = true;
     return SHD_OK;
 }
@@ -560,6 +558,7 @@ shd_status shd_equeue_batch_buffers(shd_ctx* ctx, uint64_t max_events, shd_relay
     SHD_TRY(R.seq.ensure(m * 8));
     SHD_TRY(R.pkt.ensure(m * 4));
     Q.lend = t;
+    Q.lend_cap = m;   // the relay refuses a round of more events than this into the slot
     out->ev_off = R.off.as<uint32_t>();
     out->ev_deliver = R.deliver.as<uint64_t>();
     out->ev_src = R.src.as<uint32_t>();
@@ -644,8 +643,14 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     const uint64_t n_pop = wd[1], n_keep = wd[2];
     uint64_t left = 0;
     for (uint32_t k = 0; k < S.n; ++k) left += wd[4 + k];
-    if (n_pop + left != n_in || (has_b && wd[4 + S.b] != n_keep))
-        return SHD_ERR_INVALID;   // batch ev_off / n_events disagree
+    if (n_pop + left != n_in || (has_b && wd[4 + S.b] != n_keep)) {   // batch ev_off / n_events disagree
+        std::fprintf(stderr, "shd_equeue_advance: counts disagree: popped %llu + left %llu != in %llu "
+                     "(pending %llu, batch %llu, runs %u, batch kept %llu vs %llu)\n",
+                     (unsigned long long)n_pop, (unsigned long long)left, (unsigned long long)n_in,
+                     (unsigned long long)Q.n_pending, (unsigned long long)n_b, n_runs,
+                     has_b ? (unsigned long long)wd[4 + S.b] : 0ull, (unsigned long long)n_keep);
+        return SHD_ERR_INVALID;
+    }
     // commit: cursors moved to the cut buffer; drained runs dropped; the batch's remainder is a run
     for (uint32_t k = 0; k < n_runs; ++k) {
         EqRunBuf& R = Q.run[slots[k]];

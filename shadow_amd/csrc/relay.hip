@@ -1974,10 +1974,9 @@ static bool relay_v7_ok(shd_ctx* ctx, uint64_t n) {
 // Hosts per stamp group: about S sends per group (SHD_RELAY_GROUP_SENDS, 0 = fixed kS5Hosts),
 // so a group is one full chunk of the stamp, and a group count that is a multiple of the stamp's
 // G workgroups, so no pass of the persistent grid runs with most workgroups idle.
-static uint32_t v7_group_size(uint32_t n_src, uint32_t G, uint64_t n) {
-    const char* v = std::getenv("SHD_RELAY_GROUP_SENDS");
+static uint32_t v7_group_size(const shd_ctx* ctx, uint32_t n_src, uint32_t G, uint64_t n) {
     // default: one chunk's worth (C5: 40 hosts, ~4000 sends; stamp 310 -> 283 us; 36 hosts: 290)
-    const uint64_t S = v && *v ? std::strtoull(v, nullptr, 10) : (uint64_t)kS6Cap;
+    const uint64_t S = ctx->knobs.get64(K_RELAY_GROUP_SENDS, (uint64_t)kS6Cap);
     if (!S || !n || !n_src || !G) return kS5Hosts;
     const double per_host = (double)n / n_src;
     const uint32_t want = (uint32_t)std::min<double>(kS5Hosts, std::max<double>(8.0, (double)S / per_host));
@@ -2000,7 +1999,7 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     SHD_TRY(R.bin_base.ensure((size_t)(2 * n_bins + 1) * 4));
     SHD_TRY(R.bin_lb.ensure((size_t)(n_bins + 1) * 8));
     RelayArgs3 a = relay_args3(ctx, b, rd, o);
-    a.gs = v7_group_size(R.n_src, G, n);
+    a.gs = v7_group_size(ctx, R.n_src, G, n);
     uint32_t* tot = R.bin_base.as<uint32_t>() + n_bins + 1;
     a.bin_base = R.bin_base.as<uint32_t>();
     a.n_bins = n_bins;
@@ -2017,8 +2016,8 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     }
     // the histogram's first block also resets the round's reductions (red_init's job: one
     // launch less; only the scans and the stamp read them, all after the histogram)
-    const char* hv = std::getenv("SHD_HIST_SCALAR");   // tuning A/B: the flattened-position form
-    if (((uintptr_t)b->dst_host & 15) == 0 && n < (1ull << 31) && !(hv && *hv == '1'))
+    // (SHD_HIST_SCALAR=1, tuning A/B: the flattened-position form)
+    if (((uintptr_t)b->dst_host & 15) == 0 && n < (1ull << 31) && !ctx->knobs.on(K_HIST_SCALAR))
         relay_bin_hist4<<<G * kHistSplit, kHist4Threads, (size_t)n_bins * 4, s>>>(a, G, (uint32_t)n,
                                                                              R.bin_cnt.as<uint32_t>());
     else
@@ -2031,10 +2030,10 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
         a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     V7Out vo{o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt,
              a.abs_seq ? nullptr : R.next_id.as<uint64_t>(), rd->round_end};
-    const char* stop = std::getenv("SHD_B7_STOP");   // tuning only: partial K4 (wrong output)
+    const uint32_t stop = ctx->knobs.get(K_B7_STOP, 0);   // tuning only: partial K4 (wrong output)
     bin_sort_v7<<<n_bins, kB7Threads, 0, s>>>(H, n_bins, R.bin_base.as<uint32_t>(), R.rec.as<uint4>(),
                                              R.bin_lb.as<unsigned long long>(), o->ev_off, vo, a.red,
-                                             stop && *stop ? (uint32_t)std::atoi(stop) : 0u);
+                                             stop);
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipMemcpyAsync(ctx->h_pin + 8, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     SHD_TRY(wait_stream(ctx, s));
@@ -2467,19 +2466,14 @@ shd_status shd_relay_setup(shd_ctx* ctx, uint32_t n_hosts, const uint32_t* host_
             SHD_HIP(hipStreamSynchronize(s));
         }
     }
-    {
-        const char* v = std::getenv("SHD_RELAY_FORCE_V1");
-        R.force_v1 = v && *v == '1';
-        const char* v3 = std::getenv("SHD_RELAY_FORCE_V3");   // testing: radix pipeline instead of v7
-        R.force_v3 = v3 && *v3 == '1';
-    }
+    R.force_v1 = ctx->knobs.on(K_RELAY_FORCE_V1);
+    R.force_v3 = ctx->knobs.on(K_RELAY_FORCE_V3);   // testing: radix pipeline instead of v7
     {   // bit-packed host -> node map for the LDS-resident stamp, when it fits
         uint32_t bits = 1;
         while (bits < 32 && (n_nodes - 1) >> bits) ++bits;
         const uint64_t words = ((uint64_t)n_hosts * bits + 31) / 32 + 1;
-        const char* v = std::getenv("SHD_RELAY_NO_LDS_MAP");   // testing: force the gather path
-        R.hn_bits = 0;
-        if (words * 4 + kS6FixedLds <= ctx->max_lds && !(v && *v == '1')) {
+        R.hn_bits = 0;   // (SHD_RELAY_NO_LDS_MAP=1, testing: force the gather path)
+        if (words * 4 + kS6FixedLds <= ctx->max_lds && !ctx->knobs.on(K_RELAY_NO_LDS_MAP)) {
             SHD_TRY(R.hn_packed.ensure(words * 4));
             pack_host_node<<<div_up(words, 256), 256, 0, s>>>(R.host_node.as<uint32_t>(), n_hosts, bits,
                                                               (uint32_t)words, R.hn_packed.as<uint32_t>());
@@ -2502,6 +2496,12 @@ shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const 
         return SHD_ERR_INVALID;
     if (!d_out->status || !d_out->ev_off || !d_out->ev_deliver || !d_out->ev_src ||
         !d_out->ev_seq || !d_out->ev_pkt)
+        return SHD_ERR_INVALID;
+    // an output slot lent by shd_equeue_batch_buffers holds lend_cap events: a round that could
+    // send more would write past it, so it is refused before any kernel runs
+    const EqState& Q = ctx->eq;
+    if (Q.ready && Q.lend >= 0 && d_out->ev_deliver == Q.run[Q.lend].deliver.p &&
+        d_batch->n_packets > Q.lend_cap)
         return SHD_ERR_INVALID;
     SHD_HIP(hipSetDevice(ctx->device));
     return relay_device(ctx, d_batch, round, d_out);

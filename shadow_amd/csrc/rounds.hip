@@ -80,6 +80,7 @@ shd_status shd_runahead_setup(shd_ctx* ctx, int32_t dynamic, uint64_t min_possib
     W.min_possible = mp;
     W.cfg = min_runahead_config_ns;
     W.min_used = ~0ull;
+    W.batch_min_deliver = ~0ull;   // a new run: no relay output is pending
     W.ready = true;
     return SHD_OK;
 }
@@ -125,6 +126,11 @@ shd_status shd_round_window(shd_ctx* ctx, uint64_t cpu_next_event_time, uint64_t
             if ((shd_status)all[2 * q] != SHD_OK) return (shd_status)all[2 * q];
         for (int q = 0; q < C.size; ++q) m = std::min(m, all[2 * q + 1]);
     }
+    // Without the device queues the caller took the relay output into its own queues, whose
+    // heads it reports in cpu_next_event_time from now on: the output's earliest deliver time
+    // counts for this one window (manager.rs:455-464 folds a round's minimum into the next window
+    // once), then it is consumed.  With the queues it stays until shd_equeue_advance merges it.
+    if (!ctx->eq.ready) W.batch_min_deliver = ~0ull;
     SHD_TRY(st);
     window_of(m, runahead_of(W), end_time, window_start, window_end, running);
     return SHD_OK;

@@ -399,8 +399,11 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
                         bkt[a[r].x] = bk;
                         mnext = min(mnext, (uint32_t)(bk >> kBktShift));
                         atomicOr(&bits[a[r].x >> 5], 1u << (a[r].x & 31));
-                        // after the bit (sssp_row's word scan relies on this order)
-                        if (wmin) atomicMin(&wmin[a[r].x >> 5], (uint32_t)(bk >> kBktShift));
+                        // after the bit (sssp_row's word scan relies on this order): a release,
+                        // so neither the compiler nor the LDS queue lets the minimum go first
+                        if (wmin)
+                            __hip_atomic_fetch_min(&wmin[a[r].x >> 5], (uint32_t)(bk >> kBktShift), __ATOMIC_RELEASE,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
             }
@@ -676,8 +679,8 @@ __device__ __forceinline__ void sssp_row(
                 if (m > thr) {
                     mnext = min(mnext, m);
                     scan_word = false;
-                } else {
-                    atomicExch(&wmin[widx], kLat32Inf);
+                } else {   // an acquire: the bits below are read after the reset, never before
+                    (void)__hip_atomic_exchange(&wmin[widx], kLat32Inf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
             if (scan_word) {
@@ -996,11 +999,22 @@ __global__ __launch_bounds__(256) void dense_build(const uint32_t* __restrict__ 
     }
 }
 
-template <int BLOCK, int K>
+// DCSR (complete graphs without parallel arcs, PreparedGraph::dense_rows): the arc CSR is the
+// dense matrix itself -- node x's arcs are every other node in index order, so the latency of
+// (x, v) is Wl[x (V - 1) + v - (v > x)] and (x, x) has none -- and the prune reads it directly:
+// no dense_build pass, no V x V matrices (the CSR's latency and loss arrays are Wl and Wp).
+// Block 0 then also resets the build flags (dense_build's job otherwise).
+template <bool DCSR>
+__device__ __forceinline__ uint32_t dense_lat(const uint32_t* __restrict__ Wl, uint32_t V, uint32_t x, uint32_t v) {
+    if constexpr (DCSR) return v == x ? kLat32Inf : Wl[(size_t)x * (V - 1) + v - (v > x ? 1u : 0u)];
+    else return Wl[(size_t)x * V + v];
+}
+
+template <int BLOCK, int K, bool DCSR = false>
 __global__ __launch_bounds__(BLOCK) void prune_rows(
     const uint32_t* __restrict__ Wl, const float* __restrict__ Wp, uint32_t V,
     uint32_t* __restrict__ pbeg, uint32_t* __restrict__ pend, uint4* __restrict__ parcs,
-    uint32_t* __restrict__ cursor) {
+    uint32_t* __restrict__ cursor, uint32_t* __restrict__ flags) {
     // Detour nodes x: ~K of u's lowest-latency neighbours, chosen by a 256-bin latency histogram
     // (every node in the bins below the K-th smallest latency's bin, then nodes of that bin in
     // index order up to K).  Any set of detour nodes is sound -- it only decides how many arcs
@@ -1015,8 +1029,8 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
     uint32_t* row = sela + K;                          // u's exact arc latencies
     uint16_t* binv = reinterpret_cast<uint16_t*>(row + V);   // bin per node (0xFFFF: no arc)
     const uint32_t u = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const size_t base = (size_t)u * V;
-    for (uint32_t v = tid; v < V; v += BLOCK) row[v] = Wl[base + v];
+    if (DCSR && u == 0 && tid < 16) flags[tid] = (tid == 4 || tid == 5) ? 0xFFFFFFFFu : 0u;   // as flags_init
+    for (uint32_t v = tid; v < V; v += BLOCK) row[v] = dense_lat<DCSR>(Wl, V, u, v);
     for (uint32_t i = tid; i < 256; i += BLOCK) hist[i] = 0;
     if (tid < 8) cnt[tid] = 0;
     uint32_t mx = 0;
@@ -1126,19 +1140,26 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
 #pragma unroll
             for (int i = 0; i < VB; ++i) any |= w[i] != kLat32Inf && w[i] <= z[i];
             if (!any) break;
-            uint32_t as[KB], bv[VB][KB];
+            uint32_t as[KB], bv[VB][KB], xs[KB];
             size_t xb[KB];
 #pragma unroll
             for (int j = 0; j < KB; ++j) {
                 as[j] = sela[j0 + j];
-                xb[j] = (size_t)selx[j0 + j] * V;
+                xs[j] = selx[j0 + j];
+                xb[j] = (size_t)xs[j] * (DCSR ? V - 1 : V);
             }
 #pragma unroll
             for (int i = 0; i < VB; ++i) {
+                const uint32_t v = v0 + i * BLOCK;
                 const bool live = w[i] != kLat32Inf && w[i] <= z[i];
 #pragma unroll
-                for (int j = 0; j < KB; ++j)
-                    bv[i][j] = live && as[j] != kLat32Inf ? Wl[xb[j] + v0 + i * BLOCK] : kLat32Inf;
+                for (int j = 0; j < KB; ++j) {
+                    if constexpr (DCSR)   // (x, x) has no arc; past the diagonal the row is shifted by one
+                        bv[i][j] = live && as[j] != kLat32Inf && v != xs[j] ? Wl[xb[j] + v - (v > xs[j] ? 1u : 0u)]
+                                                                            : kLat32Inf;
+                    else
+                        bv[i][j] = live && as[j] != kLat32Inf ? Wl[xb[j] + v] : kLat32Inf;
+                }
             }
 #pragma unroll
             for (int i = 0; i < VB; ++i)
@@ -1153,7 +1174,8 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
             if (w[i] == kLat32Inf || w[i] > z[i]) continue;
             const uint32_t v = v0 + i * BLOCK;
             const uint32_t slot = atomicAdd(&cnt[0], 1u);
-            kept[slot] = make_uint4(v, w[i], __float_as_uint(one_minus(Wp[base + v])), 0u);
+            const size_t at = DCSR ? (size_t)u * (V - 1) + v - (v > u ? 1u : 0u) : (size_t)u * V + v;
+            kept[slot] = make_uint4(v, w[i], __float_as_uint(one_minus(Wp[at])), 0u);
         }
     }
     __syncthreads();
@@ -1459,6 +1481,43 @@ static void build_csr(const shd_graph* g, bool reverse, HostGraph& H) {
             put(b, a);
         }
     }
+    // each node's arcs in destination order (stable: parallel arcs keep GML order).  The kernels
+    // do not depend on the order; a complete graph's CSR then IS its dense matrix without the
+    // diagonal, which the prune reads directly (dense_rows)
+    std::vector<uint32_t> idx;
+    for (uint32_t u = 0; u < V; ++u) {
+        const uint32_t b0 = H.off[u], b1 = H.off[u + 1];
+        bool sorted = true;
+        for (uint32_t k = b0 + 1; k < b1 && sorted; ++k) sorted = H.dst[k - 1] <= H.dst[k];
+        if (sorted) continue;
+        idx.resize(b1 - b0);
+        for (uint32_t k = 0; k < b1 - b0; ++k) idx[k] = b0 + k;
+        std::stable_sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) { return H.dst[x] < H.dst[y]; });
+        std::vector<uint32_t> d2(b1 - b0);
+        std::vector<uint64_t> l2(b1 - b0);
+        std::vector<float> p2(b1 - b0);
+        for (uint32_t k = 0; k < b1 - b0; ++k) {
+            d2[k] = H.dst[idx[k]];
+            l2[k] = H.lat[idx[k]];
+            p2[k] = H.loss[idx[k]];
+        }
+        std::copy(d2.begin(), d2.end(), H.dst.begin() + b0);
+        std::copy(l2.begin(), l2.end(), H.lat.begin() + b0);
+        std::copy(p2.begin(), p2.end(), H.loss.begin() + b0);
+    }
+}
+
+// every node's arc list is exactly the other V - 1 nodes in index order (a complete graph with no
+// parallel arcs): the CSR is the dense latency / loss matrix without its diagonal
+static bool csr_is_dense(const HostGraph& H) {
+    const uint32_t V = H.V;
+    if (V < 2 || H.dst.size() != (size_t)V * (V - 1)) return false;
+    for (uint32_t u = 0; u < V; ++u) {
+        if (H.off[u] != (size_t)u * (V - 1)) return false;
+        for (uint32_t k = 0; k + 1 < V; ++k)
+            if (H.dst[H.off[u] + k] != k + (k >= u ? 1u : 0u)) return false;
+    }
+    return true;
 }
 
 template <class T>
@@ -1591,6 +1650,7 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
         SHD_TRY(upload(ctx->g_diag_loss, H.diag_loss, s));
         build_csr(g, /*reverse=*/false, H);
         P.arcs = H.dst.size();
+        P.dense_rows = csr_is_dense(H);
         P.max_arc_lat = H.max_arc_lat;
         P.narrow_arcs = H.max_arc_lat < kLat32Inf;
         P.mean_arc_lat = H.dst.empty() ? 1u
@@ -1661,11 +1721,6 @@ static shd_status run_direct(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* d
     return SHD_OK;
 }
 
-static uint32_t env_u32(const char* name, uint32_t dflt) {
-    const char* v = std::getenv(name);
-    return v && *v ? (uint32_t)std::strtoul(v, nullptr, 10) : dflt;
-}
-
 struct ArcView {
     const uint32_t *beg, *end;
     const uint4* arcs;
@@ -1683,7 +1738,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
     const uint64_t guard = (uint64_t)kLat32Inf - 1 - P.max_arc_lat;
     const uint32_t lat_guard =
         A.padded && delta != kLat32Inf && !seed && P.max_arc_lat < kLat32Inf - 1 &&
-                env_u32("SHD_SSSP_NO_PAD", 0) != 1
+                ctx->knobs.get(K_SSSP_NO_PAD, 0) != 1
             ? (uint32_t)std::max<uint64_t>(guard, 1)
             : 0u;
     uint32_t* flags = ctx->g_flags.as<uint32_t>();
@@ -1704,7 +1759,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
     // edge-parallel expansion (expand_flat) for sparse graphs whose hubs would idle a node
     // group's wave (SHD_SSSP_LFLAT=1), when its per-wave scratch fits beside the rest
     const size_t flat_off = (lds + 15) & ~(size_t)15, flat_bytes = (size_t)(BLOCK / 64) * kFlatWords * 4;
-    const bool flatl = !A.padded && !seed && delta != kLat32Inf && env_u32("SHD_SSSP_LFLAT", 0) == 1 &&
+    const bool flatl = !A.padded && !seed && delta != kLat32Inf && ctx->knobs.get(K_SSSP_LFLAT, 0) == 1 &&
                        flat_off + flat_bytes <= ctx->max_lds;
     auto kern = flatl ? sssp_lds_group<BLOCK, G, R, CACHE, 0, true> : sssp_lds_group<BLOCK, G, R, CACHE, 0, false>;
     hipExtLaunchKernelGGL(kern, dim3(re - rb), dim3(BLOCK), (uint32_t)(flatl ? flat_off + flat_bytes : lds),
@@ -1732,7 +1787,7 @@ static void launch_by_degree(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32
     // (C3, 10k nodes: every relaxation's arc range from LDS instead of two dependent loads)
     uint32_t use_offl = 0;
     if (!CACHE && A.end == A.beg + 1 && lds + (size_t)(V + 1) * 4 + 8 <= ctx->max_lds &&
-        env_u32("SHD_SSSP_NO_OFFL", 0) != 1) {
+        ctx->knobs.get(K_SSSP_NO_OFFL, 0) != 1) {
         lds = ((lds + 7) & ~(size_t)7) + (size_t)(V + 1) * 4;
         use_offl = 1;
     }
@@ -1754,7 +1809,7 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
     // G lanes x R arcs (R = 4 below G = 32) per node; measured best on C2 (pruned, ~48 arcs
     // per node) at G = 8 and on C3 (BA, ~6 arcs per node) at G = 4
     uint32_t G = deg >= 64 ? 16 : deg >= 24 ? 8 : 4;
-    G = env_u32("SHD_SSSP_G", G);          // tuning overrides (results are identical)
+    G = ctx->knobs.get(K_SSSP_G, G);          // tuning overrides (results are identical)
     // Workgroup shape: once a source's labels need most of the LDS, one 1024-thread workgroup
     // per CU (the LDS arc-range cache is dropped when it no longer fits).  Otherwise rows per CU
     // decide: with one row or fewer per CU the row's sweeps are the critical path and 16 waves
@@ -1764,7 +1819,7 @@ static shd_status run_sssp(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t
     const uint32_t rows_per_cu = div_up(re - rb, (uint32_t)ctx->n_cu);
     uint32_t block = sssp_lds_bytes(P.V, 256, true) > half ? 1024
                      : rows_per_cu <= 1 ? 1024 : rows_per_cu <= 2 ? 512 : 256;
-    block = env_u32("SHD_SSSP_BLOCK", block);
+    block = ctx->knobs.get(K_SSSP_BLOCK, block);
     if (block != 256 && block != 512 && block != 1024) block = 256;
     // (edge-parallel expand_flat, as in the global-label kernel, measured slower here: the
     // kernel is issue-bound and the owner search costs more than the dead group slots; C2
@@ -1807,7 +1862,7 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
     const bool fast = use_bkt && use_flat && delta != kLat32Inf;
     auto kern = fast ? sssp_global_group<BLOCK, G, R, true> : sssp_global_group<BLOCK, G, R, false>;
     // the locality-ordered copy (prepare_reordered) when it exists and no next hops are asked for
-    const bool ro = fast && P.reordered && !ctx->nh_out && env_u32("SHD_SSSP_NO_REORDER", 0) != 1;
+    const bool ro = fast && P.reordered && !ctx->nh_out && ctx->knobs.get(K_SSSP_NO_REORDER, 0) != 1;
     const uint32_t* beg = ro ? ctx->g_offr.as<uint32_t>() : A.beg;
     const uint32_t* end = ro ? ctx->g_offr.as<uint32_t>() + 1 : A.end;
     const uint32_t* usedp = ro ? ctx->g_usedr.as<uint32_t>() : ctx->g_used.as<uint32_t>();
@@ -1815,7 +1870,7 @@ static void launch_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t 
     const float* aqp = ro ? ctx->g_aqr.as<float>() : ctx->g_aq.as<float>();
     // dynamic row claiming (SHD_SSSP_DYN=0: fixed round-robin rows, for A/B)
     uint32_t* row_ctr = nullptr;
-    if (env_u32("SHD_SSSP_DYN", 1) != 0) {
+    if (ctx->knobs.get(K_SSSP_DYN, 1) != 0) {
         row_ctr = reinterpret_cast<uint32_t*>(ctx->g_flags.as<char>() + 48);
         (void)hipMemsetAsync(row_ctr, 0, 4, ctx->stream);
     }
@@ -1838,35 +1893,35 @@ static shd_status run_sssp_global(shd_ctx* ctx, const ArcView& A, uint32_t rb, u
     const uint32_t W = (P.V + 31) / 32;
     // bitmap + control + per-wave queues (+ delta-stepping: one bucket byte per node, when it
     // fits beside the bitmap; else the sweeps read the active nodes' global labels)
-    const uint32_t use_flat = env_u32("SHD_SSSP_FLAT", 1) != 0;   // edge-parallel expansion
+    const uint32_t use_flat = ctx->knobs.get(K_SSSP_FLAT, 1) != 0;   // edge-parallel expansion
     size_t lds = (size_t)W * 4 + 16 + (BLOCK / 64) * (kQStride + (use_flat ? kFlatWords : 0)) * 4;
     if (lds > ctx->max_lds) return SHD_ERR_INVALID;   // bitmap of > ~1.2M nodes
     const size_t lds_bkt = lds + ((size_t)P.V + 3) / 4 * 4;
-    const uint32_t use_bkt = delta != kLat32Inf && lds_bkt <= ctx->max_lds && env_u32("SHD_SSSP_NO_BKT", 0) != 1;
+    const uint32_t use_bkt = delta != kLat32Inf && lds_bkt <= ctx->max_lds && ctx->knobs.get(K_SSSP_NO_BKT, 0) != 1;
     if (use_bkt) lds = lds_bkt;
     // the flat + bucket-byte kernel (FASTG) keeps a per-word minimum key beside the bitmap
     uint32_t flat_arg = use_flat;
-    if (use_bkt && use_flat && delta != kLat32Inf && env_u32("SHD_SSSP_WMIN", 1) != 0 && lds + (size_t)W * 4 <= ctx->max_lds) {
+    if (use_bkt && use_flat && delta != kLat32Inf && ctx->knobs.get(K_SSSP_WMIN, 1) != 0 && lds + (size_t)W * 4 <= ctx->max_lds) {
         lds += (size_t)W * 4;
         flat_arg |= 2u;
     }
-    const uint32_t per_cu = std::max<uint32_t>(1, env_u32("SHD_SSSP_SLOTS", 2));
+    const uint32_t per_cu = std::max<uint32_t>(1, ctx->knobs.get(K_SSSP_SLOTS, 2));
     // labels of the first kl nodes (locality order: highest degree first) in the LDS left over by
     // per_cu slots per CU: their relaxations take LDS atomics instead of memory-side ones
     uint32_t kl = 0;
     if (use_bkt && use_flat && delta != kLat32Inf && P.reordered && !ctx->nh_out &&
-        env_u32("SHD_SSSP_NO_LDS_LABELS", 0) != 1) {
+        ctx->knobs.get(K_SSSP_NO_LDS_LABELS, 0) != 1) {
         const size_t room = ctx->max_lds / per_cu;
         if (room > lds + 64) kl = std::min<uint32_t>(std::min<uint32_t>(P.V, P.lds_labels), (uint32_t)((room - lds - 16) / 8)) & ~63u;
         if (kl) lds = ((lds + 7) & ~(size_t)7) + (size_t)kl * 8;
     }
     const uint32_t slots = (uint32_t)ctx->n_cu * per_cu;
-    const uint32_t reserve = std::max(ctx->slot_reserve, env_u32("SHD_SSSP_RESERVE", 0));   // env: tools/overlap_probe.py
+    const uint32_t reserve = std::max(ctx->slot_reserve, ctx->knobs.get(K_SSSP_RESERVE, 0));   // env: tools/overlap_probe.py
     const uint32_t grid = std::min<uint32_t>(re - rb, slots - std::min(reserve, slots / 2));
     SHD_TRY(ctx->g_glab.ensure((size_t)grid * P.V * 8));
     if (ctx->nh_out) SHD_TRY(ctx->g_pred.ensure((size_t)grid * P.V * 4));
     const double deg = (double)A.n_arcs / std::max<uint32_t>(P.V, 1);
-    const uint32_t G = env_u32("SHD_SSSP_G", deg >= 64 ? 16 : deg >= 24 ? 8 : 4);
+    const uint32_t G = ctx->knobs.get(K_SSSP_G, deg >= 64 ? 16 : deg >= 24 ? 8 : 4);
     switch (G) {
         case 16: launch_global<BLOCK, 16>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, flat_arg, kl); break;
         case 8: launch_global<BLOCK, 8>(ctx, A, rb, re, grid, lds, d_lat, d_loss, delta, use_bkt, flat_arg, kl); break;
@@ -1896,7 +1951,7 @@ static shd_status run_blocked(shd_ctx* ctx, uint32_t rb, uint32_t re, uint64_t* 
     PreparedGraph& P = ctx->prep;
     hipStream_t s = ctx->stream;
     const uint32_t V = P.V;
-    const uint32_t T = env_u32("SHD_FW_TILE", V > 2048 ? 128 : 64) == 128 ? 128 : 64;
+    const uint32_t T = ctx->knobs.get(K_FW_TILE, V > 2048 ? 128 : 64) == 128 ? 128 : 64;
     const uint32_t Vp = (V + T - 1) / T * T;
     SHD_TRY(ctx->g_fw.ensure((size_t)Vp * Vp * 4));
     SHD_TRY(ctx->g_prune_dst.ensure(std::max<uint64_t>(P.arcs, 1) * 16));
@@ -1935,26 +1990,35 @@ static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
     hipStream_t s = ctx->stream;
     const uint32_t V = P.V;
     const uint64_t nn = (uint64_t)V * V;
-    SHD_TRY(ctx->g_dense.ensure(nn * 8));
-    SHD_TRY(ctx->g_labels.ensure(nn * 4));
     SHD_TRY(ctx->g_prune_dst.ensure((nn + (uint64_t)V * kArcPad) * 16));   // + list padding
     SHD_TRY(ctx->g_prune_cnt.ensure((size_t)V * 8 + 16));
-    float* Wp = ctx->g_dense.as<float>();   // the lexicographic-min arc's loss per pair (its latency: Wl)
-    uint32_t* Wl = ctx->g_labels.as<uint32_t>();
     uint32_t* pbeg = ctx->g_prune_cnt.as<uint32_t>();
     uint32_t* pend = pbeg + V;
     uint32_t* cursor = pend + V;
     uint4* pa = ctx->g_prune_dst.as<uint4>();
-    dense_build<<<V, 256, (size_t)V * 8, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
-                                              ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wp, Wl, cursor,
-                                              ctx->g_flags.as<uint32_t>());
-    const char* pk = std::getenv("SHD_PRUNE_K");   // tuning: detour nodes per row (same output tables)
-    const uint32_t Kr = pk && *pk ? (uint32_t)std::atoi(pk) : kPruneK;
+    uint32_t* flags = ctx->g_flags.as<uint32_t>();
+    const uint32_t Kr = ctx->knobs.get(K_PRUNE_K, kPruneK);   // tuning: detour nodes per row (same output tables)
     const uint32_t K = Kr >= 128 ? 128u : Kr >= 64 ? 64u : 32u;
     const size_t plds = (size_t)V * 22 + (8 + 256 + 2 * (size_t)K) * 4;
-    if (K >= 128) prune_rows<256, 128><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor);
-    else if (K >= 64) prune_rows<256, 64><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor);
-    else prune_rows<256, 32><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor);
+    if (P.dense_rows && !ctx->knobs.on(K_PRUNE_DENSE_BUILD)) {
+        // the CSR is the dense matrix (complete graph, arcs in index order): prune straight from it
+        const uint32_t* Wl = ctx->g_lat.as<uint32_t>();
+        const float* Wp = ctx->g_aux.as<float>();
+        if (K >= 128) prune_rows<256, 128, true><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+        else if (K >= 64) prune_rows<256, 64, true><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+        else prune_rows<256, 32, true><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+    } else {
+        SHD_TRY(ctx->g_dense.ensure(nn * 8));
+        SHD_TRY(ctx->g_labels.ensure(nn * 4));
+        float* Wp = ctx->g_dense.as<float>();   // the lexicographic-min arc's loss per pair (its latency: Wl)
+        uint32_t* Wl = ctx->g_labels.as<uint32_t>();
+        dense_build<<<V, 256, (size_t)V * 8, s>>>(ctx->g_off.as<uint32_t>(), ctx->g_dst.as<uint32_t>(),
+                                                  ctx->g_lat.as<uint32_t>(), ctx->g_aux.as<float>(), V, Wp, Wl, cursor,
+                                                  flags);
+        if (K >= 128) prune_rows<256, 128><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+        else if (K >= 64) prune_rows<256, 64><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+        else prune_rows<256, 32><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+    }
     SHD_HIP(hipGetLastError());
     *out = ArcView{pbeg, pend, ctx->g_prune_dst.as<uint4>(), 0, true};
     return SHD_OK;
@@ -1972,15 +2036,14 @@ static shd_status count_kept(shd_ctx* ctx, const ArcView& A) {
     return SHD_OK;
 }
 
-static uint32_t env_u32(const char* name, uint32_t dflt);
 static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache);
 
 static shd_status prepare_reordered(shd_ctx* ctx, const HostGraph& H, const uint32_t* used, uint32_t n_used) {
     PreparedGraph& P = ctx->prep;
     P.reordered = false;
     const uint32_t V = P.V;
-    if (V == 0 || (sssp_lds_bytes(V, 1024, false) <= ctx->max_lds && env_u32("SHD_SSSP_REORDER", 0) != 1) ||
-        env_u32("SHD_SSSP_NO_REORDER", 0) == 1)
+    if (V == 0 || (sssp_lds_bytes(V, 1024, false) <= ctx->max_lds && ctx->knobs.get(K_SSSP_REORDER, 0) != 1) ||
+        ctx->knobs.get(K_SSSP_NO_REORDER, 0) == 1)
         return SHD_OK;   // the LDS kernels take this graph
     hipStream_t s = ctx->stream;
     std::vector<uint32_t> deg(V), roots(V), ord, pi(V, 0xFFFFFFFFu);
@@ -1990,7 +2053,7 @@ static shd_status prepare_reordered(shd_ctx* ctx, const HostGraph& H, const uint
     }
     std::stable_sort(roots.begin(), roots.end(), [&](uint32_t a, uint32_t b) { return deg[a] > deg[b]; });
     ord.reserve(V);
-    const uint32_t mode = env_u32("SHD_REORDER_MODE", 0);   // tuning: 1 = degree order only
+    const uint32_t mode = ctx->knobs.get(K_REORDER_MODE, 0);   // tuning: 1 = degree order only
     // the K highest-degree nodes first: the global kernel keeps their labels in LDS (the LDS a
     // slot has left at 2 slots per CU, as run_sssp_global sizes it)
     {
@@ -2085,13 +2148,13 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
     // labels + bitmap + queues (+ next hops: pred[V]) must fit the LDS for the LDS-label kernels
     const size_t lds = sssp_lds_bytes(P.V, 1024, false) + (ctx->nh_out ? (size_t)P.V * 4 + 8 : 0);
     const bool blocked = algo == SHD_ALGO_BLOCKED && P.narrow_arcs && lds <= ctx->max_lds && P.V <= kBlockedMaxV;
-    const bool lds_path = !blocked && P.narrow_arcs && lds <= ctx->max_lds && env_u32("SHD_SSSP_GLOBAL", 0) != 1;
+    const bool lds_path = !blocked && P.narrow_arcs && lds <= ctx->max_lds && ctx->knobs.get(K_SSSP_GLOBAL, 0) != 1;
     const bool dense = P.V <= kPruneMaxV && P.arcs * 8 >= (uint64_t)P.V * P.V;
     const bool prune = lds_path && P.mode != SHD_ROUTE_DIRECT &&
                        (algo == SHD_ALGO_PRUNED || ((algo == SHD_ALGO_AUTO || algo == SHD_ALGO_DELTA) && dense)) &&
                        P.V <= kPruneMaxV;
     SHD_TRY(ctx->g_flags.ensure(64));
-    if (!prune) SHD_TRY(reset_flags(ctx));   // the prune path's dense_build resets them
+    if (!prune) SHD_TRY(reset_flags(ctx));   // the prune path's dense_build (or prune_rows) resets them
     // wall time of the call (host clock): timing events between the build's kernels cost a
     // few microseconds of queue bubble each, so only the main kernel is bracketed by events
     const auto t_call = std::chrono::steady_clock::now();
@@ -2145,10 +2208,10 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         // AUTO on a sparse graph: buckets of the mean arc latency (C3: 9.9 ms against 11.6 for
         // plain sweeps; 5 ms buckets 11.4, 2 ms 15.8)
         uint32_t delta = kLat32Inf;
-        if (algo == SHD_ALGO_DELTA || (algo == SHD_ALGO_AUTO && !prune && env_u32("SHD_SSSP_NO_DELTA", 0) != 1))
-            delta = env_u32("SHD_SSSP_DELTA", P.mean_arc_lat);
-        else if (algo == SHD_ALGO_AUTO && prune && env_u32("SHD_SSSP_NO_DELTA", 0) != 1)
-            delta = env_u32("SHD_SSSP_DELTA", std::max(P.min_arc_lat, P.mean_arc_lat / 256));
+        if (algo == SHD_ALGO_DELTA || (algo == SHD_ALGO_AUTO && !prune && ctx->knobs.get(K_SSSP_NO_DELTA, 0) != 1))
+            delta = ctx->knobs.get(K_SSSP_DELTA, P.mean_arc_lat);
+        else if (algo == SHD_ALGO_AUTO && prune && ctx->knobs.get(K_SSSP_NO_DELTA, 0) != 1)
+            delta = ctx->knobs.get(K_SSSP_DELTA, std::max(P.min_arc_lat, P.mean_arc_lat / 256));
         SHD_TRY(run_sssp(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
         ctx->info.algo_used = algo == SHD_ALGO_DELTA ? SHD_ALGO_DELTA
                               : prune ? SHD_ALGO_PRUNED : delta != kLat32Inf ? SHD_ALGO_DELTA : SHD_ALGO_SSSP;
@@ -2163,7 +2226,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         if (!ovf) return check_unreach(ctx, err);
         SHD_TRY(reset_flags(ctx));  // some path latency >= 2^32-1 ns: redo with u64 labels
     }
-    if (P.narrow_arcs && (lds > ctx->max_lds || env_u32("SHD_SSSP_GLOBAL", 0) == 1)) {
+    if (P.narrow_arcs && (lds > ctx->max_lds || ctx->knobs.get(K_SSSP_GLOBAL, 0) == 1)) {
         // labels exceed the LDS: global-label kernel (C4)
         bool ovf = false;
         // bucket width: 0.4 x mean_arc_lat, never below the smallest arc.  (mean_arc_lat is the
@@ -2175,7 +2238,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         // 228.8, 7 ms 231.0, 10 ms 241.2 / 242.0
         uint32_t delta = kLat32Inf;
         if (algo == SHD_ALGO_DELTA)
-            delta = env_u32("SHD_SSSP_DELTA", std::max(P.min_arc_lat, (uint32_t)(P.mean_arc_lat * 2ull / 5)));
+            delta = ctx->knobs.get(K_SSSP_DELTA, std::max(P.min_arc_lat, (uint32_t)(P.mean_arc_lat * 2ull / 5)));
         ArcView A{ctx->g_off.as<uint32_t>(), ctx->g_off.as<uint32_t>() + 1, ctx->g_arc16.as<uint4>(),
                   P.arcs};
         SHD_TRY(run_sssp_global(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));

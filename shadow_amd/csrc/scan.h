@@ -3,8 +3,8 @@
 //
 // scan_excl2: exclusive scans of one or two u32 arrays in ONE launch: a tile of 8192 entries per
 // 1024-thread workgroup (8 per thread, two 16-byte loads), a block scan, then a decoupled
-// look-back over the earlier tiles' published sums (tiles wait only on lower workgroup indices,
-// dispatched before them).  Each tile's state word is epoch << 34 | flag << 32 | value (flag 1:
+// look-back over the earlier tiles' published sums (a workgroup's tile comes from a ticket
+// counter, so a tile waits only on tiles whose workgroups already run).  Each tile's state word is epoch << 34 | flag << 32 | value (flag 1:
 // the tile's own sum, 2: the inclusive prefix); the epoch changes every launch, so the states are
 // never cleared between launches.
 //
@@ -27,6 +27,20 @@ __device__ __forceinline__ void scan_load8(const uint32_t* in, uint64_t at, uint
     } else {
 #pragma unroll
         for (uint32_t i = 0; i < kScanV; ++i) v[i] = in && at + i < n ? in[at + i] : 0u;
+    }
+}
+
+// A workgroup's tile index: the next ticket of this launch, not blockIdx.x -- a tile then only
+// waits on tiles whose workgroups are already running, whatever order the dispatcher uses.  The
+// ticket word holds epoch << 32 | tickets taken; the first taker of a new epoch restarts it at 1.
+__device__ __forceinline__ uint32_t scan_ticket(unsigned long long* t, uint32_t epoch) {
+    unsigned long long v = __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        const unsigned long long want =
+            (uint32_t)(v >> 32) == epoch ? v + 1 : ((unsigned long long)epoch << 32) | 1ull;
+        const unsigned long long prev = atomicCAS(t, v, want);
+        if (prev == v) return (uint32_t)want - 1u;
+        v = prev;
     }
 }
 
@@ -57,7 +71,13 @@ static __global__ __launch_bounds__(1024) void scan_excl2_kernel(uint64_t n, con
                                                                  uint32_t epoch) {
     __shared__ uint32_t s_w[16][2];
     __shared__ uint32_t s_pref[2];
-    const uint32_t tile = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    __shared__ uint32_t s_tile;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // state[0]: the launch's ticket word; tile t's states at state[2 + 2t]
+    if (tid == 0) s_tile = scan_ticket(state, epoch);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    state += 2;
     const uint64_t at = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanV;
     // 16-byte vector accesses when every array allows them (a caller's ev_off may be offset)
     const bool vec = ((reinterpret_cast<uintptr_t>(a_in) | reinterpret_cast<uintptr_t>(a_out) |
@@ -143,8 +163,8 @@ static shd_status scan_excl2(ScanScratch& S, const uint32_t* a_in, uint32_t* a_o
                              uint32_t* b_out, uint64_t n, hipStream_t s) {
     if (n == 0) return SHD_OK;
     const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
-    if (tiles * 16 > S.state.bytes) {   // grown: fresh states (epoch 0 is never a live epoch)
-        SHD_TRY(S.state.ensure(tiles * 16));
+    if (tiles * 16 + 16 > S.state.bytes) {   // grown: fresh states (epoch 0 is never a live epoch)
+        SHD_TRY(S.state.ensure(tiles * 16 + 16));   // + the ticket word
         SHD_HIP(hipMemsetAsync(S.state.p, 0, S.state.bytes, s));
         S.epoch = 0;
     }

@@ -55,6 +55,17 @@ class Engine:
         N.check(self.lib.shd_set_stream(self.ctx, C.c_void_p(stream_handle) if stream_handle else None),
                 "shd_set_stream")
 
+    def set_knob(self, name: str, value: int | None):
+        """Tuning / testing knob of this context (knobs.h; None or < 0: the built-in default).
+        Knobs start from the SHD_<name> environment variables, read once when the engine opens."""
+        v = -1 if value is None else int(value)
+        N.check(self.lib.shd_set_knob(self.ctx, name.encode(), v), f"shd_set_knob({name})")
+
+    def get_knob(self, name: str) -> int | None:
+        v = C.c_int64(0)
+        N.check(self.lib.shd_get_knob(self.ctx, name.encode(), C.byref(v)), f"shd_get_knob({name})")
+        return None if v.value < 0 else v.value
+
     def last_info(self) -> dict:
         info = N.RoutingInfo()
         N.check(self.lib.shd_routing_last_info(self.ctx, C.byref(info)), "shd_routing_last_info")

@@ -18,3 +18,22 @@ def engine():
     eng = Engine(0)
     yield eng
     eng.close()
+
+
+@pytest.fixture
+def knob(engine):
+    """knob(name, value): set a tuning / testing knob of the session engine (shd_set_knob) for
+    this test; every knob it touched is put back afterwards."""
+    saved = {}
+
+    def set_(name, value, eng=None):
+        e = eng or engine
+        key = (id(e), name)
+        if key not in saved:
+            saved[key] = (e, name, e.get_knob(name))
+        e.set_knob(name, value)
+
+    yield set_
+    for e, name, v in saved.values():
+        if e.ctx:
+            e.set_knob(name, v)

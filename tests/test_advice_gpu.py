@@ -28,10 +28,10 @@ def _want_counts(NN, host_node, b, status):
 
 
 @pytest.mark.parametrize("pipe", [7, 3])
-def test_failed_round_does_not_count(engine, pipe, monkeypatch):
+def test_failed_round_does_not_count(engine, pipe, knob):
     from shadow_amd._native import ShdError
     from shadow_amd.relay import Relay
-    monkeypatch.setenv("SHD_RELAY_FORCE_V3", "1" if pipe == 3 else "0")
+    knob("RELAY_FORCE_V3", 1 if pipe == 3 else 0)
     H, NN = 2000, 40
     _, lat, loss, host_node, rng0, b = _setup(H, NN, 100_000, 21)
     rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
@@ -101,3 +101,80 @@ def test_zero_latency_edge_rejected(engine):
     g = NetworkGraph([0, 1], [0, 1, 0], [0, 1, 1], [5, 5, 0], [0.0, 0.0, 0.0], False)
     with pytest.raises(ShdError, match="INVALID"):
         g.compute_shortest_paths([0, 1], engine)
+
+
+def test_round_window_without_device_queues():
+    """A caller that keeps the relay's events in its own queues (no shd_equeue_setup) and reports
+    their heads as its next event time: shd_round_window must count each relay output's earliest
+    deliver time for the window right after that round only, so the window keeps moving forward
+    (controller.rs:86-111, manager.rs:455-464) -- round after round against the restatement, with
+    the dynamic runahead (runahead.rs:43-115) fed by every round's min latency.  A fresh engine:
+    the session engine may hold device queues from other tests."""
+    from oracle.relay import EventQueues, RunaheadState, next_window
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    from shadow_amd.rounds import Runahead, next_window as eng_window
+    from shadow_amd.routing import Engine
+    H, NN, P = 3000, 40, 60_000
+    _, lat, loss, host_node, rng0, _ = _setup(H, NN, 1000, 41)
+    U64 = 2**64 - 1
+    with Engine(0) as eng:
+        rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=eng)
+        min_possible = int(lat.min())
+        Runahead(eng, True, min_possible)
+        ora = RunaheadState(True, min_possible)
+        q = EventQueues(H)
+        end_time = 10**9 + 500 * 10**6
+        ws, we = 10**9, 10**9 + ora.get()
+        starts = []
+        for rnd in range(6):
+            for h in range(H):   # every host executes its events below the window end
+                q.pop_until(h, we)
+            b = synth.packet_batch(H, P, ws, we, seed=300 + rnd)
+            r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, we, end_time, 0)
+            if r.min_latency != U64:
+                ora.update_lowest_used_latency(r.min_latency)
+            for d in range(H):
+                for t, s, sq, p in r.events_for(d):
+                    q.push(d, t, s, sq, (rnd << 32) | p)
+            heads = [q.next_event_time(h) for h in range(H)]
+            heads = [x for x in heads if x is not None]
+            cpu_next = min(heads) if heads else None
+            want = next_window(min(cpu_next if cpu_next is not None else U64, r.min_deliver), ora.get(), end_time)
+            got = eng_window(eng, cpu_next, end_time)
+            assert got == want, (rnd, got, want)
+            ws, we = want
+            starts.append(ws)
+        assert starts == sorted(starts) and starts[-1] > starts[0]
+
+
+def test_lent_batch_slot_refuses_larger_rounds(engine):
+    """shd_equeue_batch_buffers lends a slot of max_events events: a relay round of more packets
+    into that slot is refused before any kernel runs (it could write past the slot), and the same
+    round into a slot large enough goes through and is adopted."""
+    import torch
+    from shadow_amd import synth
+    from shadow_amd._native import ShdError
+    from shadow_amd.equeue import EventQueues
+    from shadow_amd.relay import Relay
+    H, NN, P = 1000, 30, 20_000
+    _, lat, loss, host_node, rng0, b = _setup(H, NN, P, 43)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    q = EventQueues(engine, H)
+    dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()  # noqa: E731
+    d = [dev(b.src_off, np.int32), dev(b.send_time, np.int64), dev(b.dst_host, np.int32), dev(b.payload, np.int32)]
+    st = torch.empty(P, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    small = q.batch_buffers(P // 2)
+    small.status = st.data_ptr()
+    with pytest.raises(ShdError, match="INVALID"):
+        rl.round_device_into(*d, 10**9 + 10**6, 10**12, 0, small)
+    big = q.batch_buffers(P)
+    big.status = st.data_ptr()
+    out = rl.round_device_into(*d, 10**9 + 10**6, 10**12, 0, big)
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss,
+                         rng0.copy(), np.zeros(H, np.uint64), 10**9 + 10**6, 10**12, 0)
+    assert out.n_sent == int((o["status"] == 2).sum())
+    p = q.popped(q.advance_device(out, 2**63))
+    assert np.array_equal(p.deliver, o["events"]["deliver"])
+    assert np.array_equal(p.seq, o["events"]["seq"])

@@ -135,16 +135,12 @@ def test_local_two_ranks_failure_is_global(engine):
 
 
 @pytest.mark.parametrize("chunk_rows", [None, 7, 64, "replicate"])
-def test_local_two_ranks_routing_sharded(engine, monkeypatch, chunk_rows):
+def test_local_two_ranks_routing_sharded(engine, chunk_rows):
     """Row shards + the table exchange: one all-gather, or row chunks exchanged while the next
     chunk is built (SHD_SHARD_CHUNK_ROWS forces the chunked path on a small graph; 7 leaves a
     short last chunk, 64 a rank whose last chunk is shorter than its peer's); "replicate" is the
     small-table default, every rank building the whole table (SHD_SHARD_REPLICATE_MB=0 turns it
     off for the exchange cases)."""
-    if chunk_rows != "replicate":
-        monkeypatch.setenv("SHD_SHARD_REPLICATE_MB", "0")
-    if chunk_rows not in (None, "replicate"):
-        monkeypatch.setenv("SHD_SHARD_CHUNK_ROWS", str(chunk_rows))
     import torch
     from shadow_amd import dist as D
     from shadow_amd import synth
@@ -158,6 +154,11 @@ def test_local_two_ranks_routing_sharded(engine, monkeypatch, chunk_rows):
     code, lat, loss, _ = corc.routing(n, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
     engines = [Engine(0), Engine(0)]
     try:
+        for e in engines:
+            if chunk_rows != "replicate":
+                e.set_knob("SHARD_REPLICATE_MB", 0)
+            if chunk_rows not in (None, "replicate"):
+                e.set_knob("SHARD_CHUNK_ROWS", chunk_rows)
         D.comm_init_local(engines)
         g = engine_graph_from_edges(el)
         per = (n + 1) // 2

@@ -48,12 +48,12 @@ def _c5_like(n_hosts, n_nodes, n_packets, seed, start=10**9, runahead=10**6):
 
 @pytest.mark.parametrize("pipe", [7, 3, 1])
 @pytest.mark.parametrize("chance_mode", [False, True])
-def test_multi_round_vs_c_oracle(engine, chance_mode, pipe, monkeypatch):
+def test_multi_round_vs_c_oracle(engine, chance_mode, pipe, knob):
     """Three consecutive rounds on 20k hosts / 1M packets: streams and ids carry across rounds
     (bin-placement pipeline, radix-sort pipeline and the 64-bit fallback pipeline)."""
     from shadow_amd.relay import Relay
-    monkeypatch.setenv("SHD_RELAY_FORCE_V1", "1" if pipe == 1 else "0")
-    monkeypatch.setenv("SHD_RELAY_FORCE_V3", "1" if pipe == 3 else "0")
+    knob("RELAY_FORCE_V1", 1 if pipe == 1 else 0)
+    knob("RELAY_FORCE_V3", 1 if pipe == 3 else 0)
     H, NN = 20_000, 200
     lat, loss, host_node, rng0, _ = _c5_like(H, NN, 1000, 11)
     nid0 = np.zeros(H, np.uint64)
@@ -193,13 +193,13 @@ def test_wide_latency_table_and_failed_round_keeps_state(engine):
 
 @pytest.mark.parametrize("lds_map", [True, False])
 @pytest.mark.parametrize("n_hosts", [300, 2000, 5000])
-def test_bucket_size_classes(engine, n_hosts, lds_map, monkeypatch):
+def test_bucket_size_classes(engine, n_hosts, lds_map, knob):
     """Destination runs of every size class of the per-run sort (<= 64, <= 128, <= 256 events
     per destination, and longer runs on the merge path) against the C restatement; both stamp
     kernels (host -> node map resident in LDS, or gathered from global memory)."""
     from shadow_amd import synth
     from shadow_amd.relay import Relay
-    monkeypatch.setenv("SHD_RELAY_NO_LDS_MAP", "0" if lds_map else "1")
+    knob("RELAY_NO_LDS_MAP", 0 if lds_map else 1)
     NN = 50
     lat, loss, host_node, rng0, b = _c5_like(n_hosts, NN, 400_000, 13)
     nid0 = np.arange(n_hosts, dtype=np.uint64) * np.uint64(7)

@@ -110,7 +110,7 @@ def test_c2_full_bit_exact(engine, c2_case, algo):
 
 
 @pytest.mark.parametrize("group", ["", "8", "4"])
-def test_c2_repeated_runs_bit_exact(engine, c2_case, group, monkeypatch):
+def test_c2_repeated_runs_bit_exact(engine, c2_case, group, knob):
     """Prepare once, run several builds: from the second on the engine knows the pruned arc count,
     so AUTO picks the padded-list kernel (sssp_lds_group<..., 8>) -- the C2 headline kernel, which
     a single shd_routing_build never reaches (its first run sizes the lane groups on the unpruned
@@ -121,7 +121,7 @@ def test_c2_repeated_runs_bit_exact(engine, c2_case, group, monkeypatch):
 
     from shadow_amd import _native as N
     if group:
-        monkeypatch.setenv("SHD_SSSP_G", group)
+        knob("SSSP_G", int(group))
     el, used, lat, loss = c2_case
     g = engine_graph_from_edges(el)._cgraph()
     err = N.Error()
@@ -208,11 +208,11 @@ def test_blocked_closure_padding_and_directed(engine):
         used = rng.permutation(n).astype(np.uint32)
         code, lat, loss, _ = corc.routing(n, s, d, l, p, directed, used)
         assert code == "OK"
-        os.environ["SHD_FW_TILE"] = tile
+        engine.set_knob("FW_TILE", int(tile))
         try:
             t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=4)
         finally:
-            del os.environ["SHD_FW_TILE"]
+            engine.set_knob("FW_TILE", None)
         _assert_table(t, lat, loss.view(np.uint32))
         info = engine.last_info()
         assert info["algo_used"] == 4 and info["ms_minplus"] > 0
@@ -250,16 +250,16 @@ def _tie_heavy_ba(n, m, seed, directed):
 
 @pytest.mark.parametrize("directed", [False, True])
 @pytest.mark.parametrize("slots", ["2", "1"])
-def test_global_label_kernel_claimed_rows(engine, directed, slots, monkeypatch):
+def test_global_label_kernel_claimed_rows(engine, directed, slots, knob):
     """Every row of a 3,000-node tie-heavy graph on the persistent global-label kernel, built as
     C4 is (locality order + LDS labels for the hubs, SHD_SSSP_REORDER=1).  The grid holds
     slots x n_cu (256 CUs: 512 or 256) slots, so rows past it -- most of the table -- are taken
     from the row counter (sssp_global_group's dynamic claiming), and every one of them is compared
     against the C restatement (graph/mod.rs:185-230)."""
     from shadow_amd.routing import NetworkGraph
-    monkeypatch.setenv("SHD_SSSP_GLOBAL", "1")
-    monkeypatch.setenv("SHD_SSSP_REORDER", "1")
-    monkeypatch.setenv("SHD_SSSP_SLOTS", slots)
+    knob("SSSP_GLOBAL", 1)
+    knob("SSSP_REORDER", 1)
+    knob("SSSP_SLOTS", int(slots))
     n = 3000
     ids, s, d, l, p, directed = _tie_heavy_ba(n, 3, 31 + int(slots), directed)
     used = np.arange(n, dtype=np.uint32)
@@ -272,12 +272,32 @@ def test_global_label_kernel_claimed_rows(engine, directed, slots, monkeypatch):
         _assert_table(t, lat, loss.view(np.uint32))
 
 
-def test_global_label_kernel_claimed_rows_sub_range(engine, monkeypatch):
+@pytest.mark.parametrize("reserve", [32, 255])
+def test_global_label_kernel_claimed_rows_reserved_slots(engine, knob, reserve):
+    """The grid every C4 build at N >= 2 runs from its second chunk on (shd_routing_run_sharded
+    leaves SHD_SHARD_RESERVE_SLOTS = 32 slots unlaunched while the previous chunk is exchanged):
+    2 x n_cu - reserve slots (capped at half), so the row counter hands out more rows per slot.
+    Every row of a 3,000-node tie-heavy graph against the C restatement."""
+    from shadow_amd.routing import NetworkGraph
+    knob("SSSP_GLOBAL", 1)
+    knob("SSSP_REORDER", 1)
+    knob("SSSP_RESERVE", reserve)
+    n = 3000
+    ids, s, d, l, p, directed = _tie_heavy_ba(n, 3, 57, False)
+    used = np.random.default_rng(11).permutation(n).astype(np.uint32)
+    code, lat, loss, _ = corc.routing(n, s, d, l, p, directed, used)
+    assert code == "OK"
+    t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=3)
+    assert engine.last_info()["algo_used"] == 3
+    _assert_table(t, lat, loss.view(np.uint32))
+
+
+def test_global_label_kernel_claimed_rows_sub_range(engine, knob):
     """A row range that does not start at 0 (a rank's shard): claimed rows are offset by
     row_begin + grid, so rows [1000, 2900) of a 3,000-node graph, every one compared."""
     from shadow_amd.routing import NetworkGraph
-    monkeypatch.setenv("SHD_SSSP_GLOBAL", "1")
-    monkeypatch.setenv("SHD_SSSP_REORDER", "1")
+    knob("SSSP_GLOBAL", 1)
+    knob("SSSP_REORDER", 1)
     n = 3000
     ids, s, d, l, p, directed = _tie_heavy_ba(n, 2, 77, False)
     used = np.random.default_rng(3).permutation(n).astype(np.uint32)
@@ -289,9 +309,9 @@ def test_global_label_kernel_claimed_rows_sub_range(engine, monkeypatch):
 
 
 @pytest.mark.parametrize("seed", range(4))
-def test_global_label_kernel_forced(engine, seed, monkeypatch):
+def test_global_label_kernel_forced(engine, seed, knob):
     """The global-label kernel on small tie-heavy graphs (forced with SHD_SSSP_GLOBAL=1)."""
-    monkeypatch.setenv("SHD_SSSP_GLOBAL", "1")
+    knob("SSSP_GLOBAL", 1)
     rng = np.random.default_rng(2000 + seed)
     n = int(rng.integers(2, 300))
     ids, s, d, l, p, directed = random_graph(rng, n, float(rng.uniform(0.005, 0.3)), bool(seed % 2),

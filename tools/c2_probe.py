@@ -23,7 +23,7 @@ for spec in sys.argv[1:]:           # "algo[:ENV=val,ENV=val]"
     algo, _, envs = spec.partition(":")
     for kv in filter(None, envs.split(",")):
         k, v = kv.split("=")
-        os.environ[k] = v
+        eng.set_knob(k, int(v))   # knobs are per context (read from the env only at shd_open)
     ms = []
     for rep in range(8 if GRAPH == "c2" else 3):
         run_rows(eng, int(algo), 0, n, lat, loss)
@@ -34,4 +34,4 @@ for spec in sys.argv[1:]:           # "algo[:ENV=val,ENV=val]"
     print(f"{spec:40s} main_us={np.median(ms) * 1e3:7.1f} total_us={i['ms_total'] * 1e3:7.1f} kept={i['arcs_kept']} "
           f"same={h == ref}", flush=True)
     for kv in filter(None, envs.split(",")):
-        os.environ.pop(kv.split("=")[0])
+        eng.set_knob(kv.split("=")[0], None)
