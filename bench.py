@@ -513,8 +513,85 @@ def relay_check_and_e2e(eng, rl, lat_table, loss_table, reps=3):
         N.check(eng.lib.shd_relay_round(eng.ctx, C.byref(batch), C.byref(rnd), C.byref(out)), "shd_relay_round")
     ms = (time.perf_counter() - t0) / reps * 1e3
     moved = (H + 1) * 4 + P * (8 + 4 + 4) + P + (H + 1) * 4 + ns * 24
-    return ok, {"ms_per_round": ms, "packets_per_s": P / (ms * 1e-3), "pcie_bytes": moved,
-                "what": "shd_relay_round with pinned host buffers: staged batch H2D, round, statuses + events D2H"}
+    res = {"ms_per_round": ms, "packets_per_s": P / (ms * 1e-3), "pcie_bytes": moved,
+           "what": "shd_relay_round with pinned host buffers: staged batch H2D, round, statuses + events D2H"}
+    # the same call with the CPU-drawn f64 chance (INTEGRATION.md's drop-in before shd_relay_flush)
+    h_ch = pin(np.random.default_rng(5).random(P), np.float64)
+    batch_c = N.Batch(P, hp(h_off), hp(h_time), hp(h_dst), hp(h_pay), hp(h_ch))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        N.check(eng.lib.shd_relay_round(eng.ctx, C.byref(batch_c), C.byref(rnd), C.byref(out)), "shd_relay_round")
+    msc = (time.perf_counter() - t0) / reps * 1e3
+    res["with_chance"] = {"ms_per_round": msc, "packets_per_s": P / (msc * 1e-3), "pcie_bytes": moved + P * 8}
+    fl, ok_fl = flush_e2e(eng, rl, lat_table, loss_table, setup, reps)
+    res["flush"] = fl
+    return ok and ok_fl, res
+
+
+def flush_e2e(eng, rl, lat_table, loss_table, setup, reps=3, n_threads=16):
+    """The drop-in round barrier (shd_relay_flush): the round's sends as 16 worker threads' pinned
+    staging buffers (per thread: runs of its hosts, 12-byte sends with the CPU's top-32-bit draws),
+    grouped on the device; 2-bit statuses and 16-byte events back into pinned memory.  The first
+    round (from the setup state) is checked against the C restatement in CPU-chance mode (the same
+    u64 draws as f64 chances); then `reps` rounds are timed."""
+    from oracle import corc
+    from shadow_amd import _native as N
+    from shadow_amd import synth
+    from shadow_amd.relay import PinnedStages
+    b, H, P = rl["batch"], rl["H"], rl["P"]
+    rd = rl["rd"]
+    time_base = int(b.send_time.min())
+    st = synth.stage_round(b, n_threads, time_base, seed=11)
+    ps = PinnedStages.pinned(eng.lib, st.run_host, st.run_count, st.sends)
+    st2 = torch_pinned_u8((P + 3) // 4)
+    ev_off = torch_pinned_u8((H + 1) * 4)
+    evs = torch_pinned_u8(P * 16)
+    sb = torch_pinned_u8(H * 8)
+    out = N.FlushOut(st2.data_ptr(), ev_off.data_ptr(), evs.data_ptr(), sb.data_ptr(), 0, 0, 0)
+    rnd = N.Round(*rd)
+
+    def flush():
+        N.check(eng.lib.shd_relay_flush(eng.ctx, ps.array, len(ps.stages), time_base, C.byref(rnd), C.byref(out)),
+                "shd_relay_flush")
+    try:
+        setup()
+        t0 = time.perf_counter()
+        flush()
+        first_ms = (time.perf_counter() - t0) * 1e3
+        ns = out.n_sent
+        chance = (st.draw64 >> np.uint64(11)).astype(np.float64) * 2.0**-53
+        o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, rl["host_node"], lat_table, loss_table,
+                             rl["rng0"].copy(), np.zeros(H, np.uint64), *rd, chance=chance, threads=corc.max_threads())
+        ev = o["events"]
+        inv = np.empty(P, np.int64)
+        inv[st.stage_of_send] = np.arange(P)
+        e = evs.numpy()[: ns * 16].view(np.uint32).reshape(-1, 4)
+        seq_base = sb.numpy()[: H * 8].view(np.uint64)
+        status = ((st2.numpy()[:, None] >> (np.arange(4, dtype=np.uint8) * 2)) & 3).reshape(-1)[:P]
+        ok = (np.array_equal(status, o["status"][st.stage_of_send])
+              and np.array_equal(ev_off.numpy()[: (H + 1) * 4].view(np.uint32), ev["off"])
+              and np.array_equal(e[:, 0].astype(np.uint64) + np.uint64(rd[0]), ev["deliver"])
+              and np.array_equal(e[:, 1], ev["src"])
+              and np.array_equal(e[:, 2].astype(np.uint64) + seq_base[e[:, 1]], ev["seq"])
+              and np.array_equal(e[:, 3].astype(np.int64), inv[ev["pkt"].astype(np.int64)])
+              and (out.min_deliver, out.min_latency, ns) == (o["min_deliver"], o["min_latency"], o["n_sent"]))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            flush()
+        ms = (time.perf_counter() - t0) / reps * 1e3
+        moved = P * 12 + sum(len(x) for x in st.run_host) * 8 + (P + 3) // 4 + (H + 1) * 4 + out.n_sent * 16 + H * 8
+        return ({"ms_per_round": ms, "packets_per_s": P / (ms * 1e-3), "pcie_bytes": moved, "first_call_ms": first_ms,
+                 "stages": n_threads, "bit_exact_vs_cpu_chance": bool(ok),
+                 "what": "shd_relay_flush: 16 worker threads' pinned staging buffers (runs + 12-byte sends with the "
+                         "CPU's top-32-bit draws) grouped on the device, round, 2-bit statuses + 16-byte events D2H"},
+                ok)
+    finally:
+        ps.free()
+
+
+def torch_pinned_u8(n):
+    import torch
+    return torch.empty(max(int(n), 1), dtype=torch.uint8).pin_memory()
 
 
 def cpu_baseline_routing(el, budget_s=8.0):

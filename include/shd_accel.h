@@ -274,6 +274,69 @@ shd_status shd_relay_round(shd_ctx* ctx, const shd_batch* batch, const shd_round
 shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const shd_round* round,
                                   shd_relay_out* d_out);
 
+/* ---------------------------------------------------------------- drop-in flush of staged sends */
+/*
+ * The round barrier of the drop-in (manager.rs:455-464) without any CPU reorder: the worker threads'
+ * staging buffers go to the device as they are.  Each host runs on one worker thread per round
+ * (scheduler/thread_per_core.rs:188-206), so its sends form ONE run (host, count) of consecutive
+ * records in ONE stage (= one thread's buffer), in send order; stages and runs may come in any
+ * order.  A staged send is 12 bytes (worker.rs:328-413 reads nothing else):
+ *   time_off  now - time_base (ns; the round's window start is a natural time_base)
+ *   dst       destination HostId (resolve_ip_to_host_id, worker.rs:350-355), | SHD_SEND_PAYLOAD
+ *             when packet_getPayloadSize > 0 (the drop rule spares empty packets, :370)
+ *   draw_hi   the source host's next_u64() >> 32 taken at send time -- in place of gen::<f64>()
+ *             (:365), which consumes the same one next_u64, so the CPU stream advances as in the
+ *             reference; the top 32 bits decide chance >= reliability exactly
+ * The completed check (:334-341) stays on the CPU: staged sends have now < sim_end.
+ * Outputs (host buffers; pinned -- shd_host_alloc -- for the link's full rate; any may be NULL):
+ *   status2   2-bit SHD_PKT_* per send in stage order (stage 0's sends, then stage 1's, ...):
+ *             send i in bits 2(i%4), 2(i%4)+1 of byte i/4; ceil(n/4) bytes
+ *   ev_off    [n_hosts + 1]; events[ev_off[h], ev_off[h+1]) are host h's, in EventQueue order
+ *   events    n_sent shd_event16 records
+ *   seq_base  [n_hosts]: each host's first packet event id of this round (event id = seq_base[src]
+ *             + seq_off)
+ * Device RNG streams are not used (the draws are the CPU's); event ids, counters and the runahead
+ * update as in shd_relay_round.  SHD_ERR_NO_HOST: a run's host or a destination is not a relay
+ * host; SHD_ERR_INVALID: a host with two runs, or runs that do not cover a stage's records.
+ */
+#define SHD_SEND_PAYLOAD 0x80000000u
+typedef struct shd_send12 {
+    uint32_t time_off;
+    uint32_t dst;
+    uint32_t draw_hi;
+} shd_send12;
+
+typedef struct shd_stage {
+    uint32_t n_runs;
+    const uint32_t* run_host;    /* [n_runs] source HostId of each run */
+    const uint32_t* run_count;   /* [n_runs] its sends, consecutive in `sends` */
+    uint64_t n_sends;
+    const shd_send12* sends;     /* [n_sends] */
+} shd_stage;
+
+typedef struct shd_event16 {
+    uint32_t deliver_off;   /* deliver time - round_end */
+    uint32_t src_host;
+    uint32_t seq_off;       /* src_host_event_id - seq_base[src_host] */
+    uint32_t send;          /* the send's index in stage order */
+} shd_event16;
+
+typedef struct shd_flush_out {
+    uint8_t* status2;
+    uint32_t* ev_off;
+    shd_event16* events;
+    uint64_t* seq_base;
+    uint64_t min_deliver;   /* as shd_relay_out */
+    uint64_t min_latency;
+    uint64_t n_sent;
+} shd_flush_out;
+
+shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_stages, uint64_t time_base,
+                           const shd_round* round, shd_flush_out* out);
+/* Pinned host memory for staging buffers and outputs (hipHostMalloc); NULL on failure. */
+void* shd_host_alloc(size_t bytes);
+void shd_host_free(void* p);
+
 /* ---------------------------------------------------------------- multi-GPU */
 /*
  * The reference is one process whose manager thread runs every round to a barrier

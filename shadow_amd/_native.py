@@ -37,7 +37,7 @@ EXPORTED = [
     "shd_routing_run_next_hops", "shd_assign_ips", "shd_gml_load",
     "shd_runahead_setup", "shd_runahead_get", "shd_round_window", "shd_window_compute", "shd_copy_to_host",
     "shd_routing_lookup_batch", "shd_routing_mirror", "shd_equeue_batch_buffers",
-    "shd_set_knob", "shd_get_knob",
+    "shd_set_knob", "shd_get_knob", "shd_relay_flush", "shd_host_alloc", "shd_host_free",
 ]
 COMM_ID_BYTES = 128
 
@@ -82,6 +82,19 @@ class RelayOut(C.Structure):
                 ("ev_src", C.c_void_p), ("ev_seq", C.c_void_p), ("ev_pkt", C.c_void_p),
                 ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64),
                 ("n_dst", C.c_uint32), ("n_events", C.c_uint32)]
+
+
+class Stage(C.Structure):
+    _fields_ = [("n_runs", C.c_uint32), ("run_host", C.c_void_p), ("run_count", C.c_void_p),
+                ("n_sends", C.c_uint64), ("sends", C.c_void_p)]
+
+
+class FlushOut(C.Structure):
+    _fields_ = [("status2", C.c_void_p), ("ev_off", C.c_void_p), ("events", C.c_void_p), ("seq_base", C.c_void_p),
+                ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64)]
+
+
+SEND_PAYLOAD = 0x80000000
 
 
 class EqueueOut(C.Structure):
@@ -186,6 +199,9 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_routing_mirror": (I32, [P, I32]),
         "shd_equeue_batch_buffers": (I32, [P, U64, P]),
         "shd_set_knob": (I32, [P, C.c_char_p, C.c_int64]),
+        "shd_relay_flush": (I32, [P, P, U32, U64, P, P]),
+        "shd_host_alloc": (P, [C.c_size_t]),
+        "shd_host_free": (None, [P]),
         "shd_get_knob": (I32, [P, C.c_char_p, P]),
     }
     for name, (res, args) in sig.items():

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = [os.path.join(HERE, "csrc", f) for f in ("routing.hip", "blocked.hip", "relay.hip", "api.cpp", "gml.cpp",
                                                 "codel.hip", "tbucket.hip", "comm.cpp", "equeue.hip",
-                                                "hosts.cpp", "rounds.hip")]
+                                                "hosts.cpp", "rounds.hip", "flush.hip")]
 OUT = os.path.join(HERE, "libshd_accel.so")
 OBJ = os.path.join(HERE, "build", "obj")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",

@@ -135,6 +135,11 @@ struct RelayState {
     // received, and the merged events of this rank's destinations (engine-owned outputs)
     DevBuf x_rec, x_words, x_off, x_roff, x_rrec, m_off, m_deliver, m_src, m_seq, m_pkt;
     uint64_t x_cap = 0;   // events x_rrec and m_* hold (grown with a growth agreement, never between collectives)
+    // shd_relay_flush (flush.hip): the round's draws came from the CPU (top 32 bits in `draws`), the
+    // staged runs and records as uploaded, the send permutation (grouped <-> stage order) and the
+    // packed outputs
+    bool cpu_draws = false;
+    DevBuf fl_runh, fl_runc, fl_runo, fl_hrun, fl_hcnt, fl_send, fl_perm, fl_inv, fl_st2, fl_ev16;
 };
 
 struct PreparedGraph {

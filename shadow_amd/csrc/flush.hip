@@ -1,0 +1,246 @@
+// shd_relay_flush: the drop-in form of the relay round -- the worker threads' staging buffers as
+// they stand at the round barrier, grouped by source host on the device, with the CPU-drawn loss
+// draws, and compact outputs for the trip back over PCIe.
+//
+// Reference: Worker::send_packet (src/main/core/worker.rs:328-413) runs on every worker thread;
+// each host runs on one thread per round (scheduler/thread_per_core.rs:188-206), so a host's sends
+// are ONE contiguous run in ONE thread's buffer, in send order.  The round's sends reach the device
+// as those buffers (stage = thread), each a list of runs (host, count) and 12-byte send records:
+//   time_off = now - time_base, dst | SHD_SEND_PAYLOAD (payload_size > 0 is all the drop rule reads,
+//   worker.rs:370), draw_hi = the source host's next_u64() >> 32 at send time.  gen::<f64>() is
+//   (next_u64 >> 11) * 2^-53 and consumes exactly one next_u64, so the CPU stream advances as in
+//   the reference; the top 32 bits decide `chance >= reliability` exactly for every reliability
+//   1f32 - loss (relay.hip draw_drops).
+// The device turns the runs into the grouped layout the pipelines take (src_off, one contiguous
+// range per host in host order), runs the round with those draws (the device streams are left
+// untouched), and writes back per send a 2-bit status in stage order, and per event a 16-byte
+// record {deliver - round_end, src host, event id - the host's first id of the round, send index
+// in stage order} grouped by destination in EventQueue order (event.rs:84-155).
+#include <algorithm>
+#include <cstring>
+
+#include "ctx.h"
+#include "scan.h"
+
+namespace shd {
+
+// relay.hip: the round (pipelines + checks + commit) on a grouped device batch
+shd_status relay_flush_round(shd_ctx* ctx, const shd_batch* b, const shd_round* rd, shd_relay_out* o);
+
+struct Send12 {
+    uint32_t time_off, dst, draw_hi;
+};
+static_assert(sizeof(Send12) == sizeof(shd_send12), "12-byte staged send");
+
+// per run: its host's run index (+1); a second run of one host is an error (red[0]), as is a
+// host outside the relay (red[1])
+__global__ __launch_bounds__(256) void fl_runs(uint32_t n_runs, const uint32_t* __restrict__ run_host,
+                                               uint32_t n_hosts, uint32_t* __restrict__ hrun,
+                                               unsigned long long* __restrict__ red) {
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= n_runs) return;
+    const uint32_t h = run_host[r];
+    if (h >= n_hosts) {
+        atomicMin(&red[1], (unsigned long long)r);
+        return;
+    }
+    if (atomicExch(&hrun[h], r + 1) != 0) atomicMin(&red[0], (unsigned long long)h);
+}
+
+// per host: its send count (0 without a run); entry n_hosts is 0 so one scan gives src_off[0..H]
+__global__ __launch_bounds__(256) void fl_host_counts(uint32_t n_hosts, const uint32_t* __restrict__ hrun,
+                                                      const uint32_t* __restrict__ run_count,
+                                                      uint32_t* __restrict__ hcnt) {
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    if (h > n_hosts) return;
+    const uint32_t r = h < n_hosts ? hrun[h] : 0u;
+    hcnt[h] = r ? run_count[r - 1] : 0u;
+}
+
+// one wave per host: its run's records into the grouped arrays the pipelines read, the permutation
+// both ways (grouped position <-> send index in stage order)
+__global__ __launch_bounds__(256) void fl_gather(uint32_t n_hosts, const uint32_t* __restrict__ hrun,
+                                                 const uint32_t* __restrict__ run_off,
+                                                 const uint32_t* __restrict__ src_off, const Send12* __restrict__ in,
+                                                 uint64_t time_base, uint64_t* __restrict__ send_time,
+                                                 uint32_t* __restrict__ dst_host, uint32_t* __restrict__ payload,
+                                                 uint32_t* __restrict__ draws, uint32_t* __restrict__ perm,
+                                                 uint32_t* __restrict__ inv) {
+    const uint32_t h = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (h >= n_hosts) return;
+    const uint32_t r = hrun[h];
+    if (!r) return;
+    const uint32_t from = run_off[r - 1], to = src_off[h], cnt = src_off[h + 1] - to;
+    for (uint32_t k = lane; k < cnt; k += 64) {
+        const Send12 x = in[from + k];
+        const uint32_t p = to + k;
+        send_time[p] = time_base + x.time_off;
+        dst_host[p] = x.dst & ~SHD_SEND_PAYLOAD;
+        payload[p] = x.dst >> 31;
+        draws[p] = x.draw_hi;
+        perm[p] = from + k;
+        inv[from + k] = p;
+    }
+}
+
+// 2-bit statuses in stage order: byte j holds sends 4j .. 4j+3 (send 4j + k in bits 2k, 2k+1)
+__global__ __launch_bounds__(256) void fl_status2(uint64_t n, const uint32_t* __restrict__ inv,
+                                                  const uint8_t* __restrict__ st, uint8_t* __restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j * 4 >= n) return;
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        if (j * 4 + k < n) v |= (uint32_t)(st[inv[j * 4 + k]] & 3u) << (2 * k);
+    out[j] = (uint8_t)v;
+}
+
+// 16-byte event records (already grouped by destination in EventQueue order)
+__global__ __launch_bounds__(256) void fl_events16(uint64_t n, uint64_t round_end, const uint64_t* __restrict__ deliver,
+                                                   const uint32_t* __restrict__ src, const uint64_t* __restrict__ seq,
+                                                   const uint32_t* __restrict__ pkt, const uint64_t* __restrict__ seq_base,
+                                                   const uint32_t* __restrict__ perm, uint4* __restrict__ out) {
+    const uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t s = src[e];
+    out[e] = make_uint4((uint32_t)(deliver[e] - round_end), s, (uint32_t)(seq[e] - seq_base[s]), perm[pkt[e]]);
+}
+
+}  // namespace shd
+
+using namespace shd;
+
+extern "C" {
+
+void* shd_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void shd_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_stages, uint64_t time_base,
+                           const shd_round* round, shd_flush_out* out) {
+    if (!ctx || !round || !out || (n_stages && !stages)) return SHD_ERR_INVALID;
+    RelayState& R = ctx->relay;
+    if (!R.ready || R.sharded) return SHD_ERR_STATE;
+    // host-side shape checks (each stage's runs cover exactly its records)
+    uint64_t n = 0, n_runs = 0;
+    for (uint32_t k = 0; k < n_stages; ++k) {
+        const shd_stage& S = stages[k];
+        if (S.n_runs && (!S.run_host || !S.run_count)) return SHD_ERR_INVALID;
+        if (S.n_sends && !S.sends) return SHD_ERR_INVALID;
+        uint64_t c = 0;
+        for (uint32_t r = 0; r < S.n_runs; ++r) c += S.run_count[r];
+        if (c != S.n_sends) return SHD_ERR_INVALID;
+        n += S.n_sends;
+        n_runs += S.n_runs;
+    }
+    const uint32_t H = R.n_hosts;
+    if (n >= (1ull << 32) || n_runs >= (1ull << 32)) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const size_t nn = std::max<uint64_t>(n, 1), nr = std::max<uint64_t>(n_runs, 1);
+    SHD_TRY(R.fl_runh.ensure(nr * 4));
+    SHD_TRY(R.fl_runc.ensure(nr * 4));
+    SHD_TRY(R.fl_runo.ensure(nr * 4));
+    SHD_TRY(R.fl_hrun.ensure((size_t)(H + 1) * 4));
+    SHD_TRY(R.fl_hcnt.ensure((size_t)(H + 1) * 4));
+    SHD_TRY(R.fl_send.ensure(nn * 12));
+    SHD_TRY(R.fl_perm.ensure(nn * 4));
+    SHD_TRY(R.fl_inv.ensure(nn * 4));
+    SHD_TRY(R.fl_st2.ensure(nn / 4 + 1));
+    SHD_TRY(R.fl_ev16.ensure(nn * 16));
+    SHD_TRY(R.pk_off.ensure((size_t)(H + 1) * 4));
+    SHD_TRY(R.pk_time.ensure(nn * 8));
+    SHD_TRY(R.pk_dst.ensure(nn * 4));
+    SHD_TRY(R.pk_pay.ensure(nn * 4));
+    SHD_TRY(R.draws.ensure(nn * 4));
+    SHD_TRY(R.st.ensure(nn));
+    SHD_TRY(R.ev_off.ensure((size_t)(H + 1) * 4));
+    SHD_TRY(R.ev_deliver.ensure(nn * 8));
+    SHD_TRY(R.ev_src.ensure(nn * 4));
+    SHD_TRY(R.ev_seq.ensure(nn * 8));
+    SHD_TRY(R.ev_pkt.ensure(nn * 4));
+    SHD_TRY(R.red.ensure(64));
+    // 1. the staging buffers, stage after stage (pinned host memory -- shd_host_alloc -- moves at
+    //    the link's rate; pageable memory is staged by the runtime)
+    {
+        uint64_t at = 0, ar = 0;
+        for (uint32_t k = 0; k < n_stages; ++k) {
+            const shd_stage& S = stages[k];
+            if (S.n_runs) {
+                SHD_HIP(hipMemcpyAsync(R.fl_runh.as<uint32_t>() + ar, S.run_host, (size_t)S.n_runs * 4,
+                                       hipMemcpyHostToDevice, s));
+                SHD_HIP(hipMemcpyAsync(R.fl_runc.as<uint32_t>() + ar, S.run_count, (size_t)S.n_runs * 4,
+                                       hipMemcpyHostToDevice, s));
+            }
+            if (S.n_sends)
+                SHD_HIP(hipMemcpyAsync(R.fl_send.as<char>() + at * 12, S.sends, S.n_sends * 12, hipMemcpyHostToDevice, s));
+            at += S.n_sends;
+            ar += S.n_runs;
+        }
+    }
+    // 2. runs -> hosts, per-host counts, the grouped offsets, the gather
+    unsigned long long* red = R.red.as<unsigned long long>();
+    SHD_HIP(hipMemsetAsync(R.fl_hrun.p, 0, (size_t)(H + 1) * 4, s));
+    SHD_HIP(hipMemsetAsync(red, 0xFF, 16, s));
+    if (n_runs) {
+        fl_runs<<<div_up(n_runs, 256), 256, 0, s>>>((uint32_t)n_runs, R.fl_runh.as<uint32_t>(), H,
+                                                     R.fl_hrun.as<uint32_t>(), red);
+        SHD_TRY(scan_excl2(R.scan, R.fl_runc.as<uint32_t>(), R.fl_runo.as<uint32_t>(), nullptr, nullptr, n_runs, s));
+    }
+    fl_host_counts<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(H, R.fl_hrun.as<uint32_t>(), R.fl_runc.as<uint32_t>(),
+                                                                R.fl_hcnt.as<uint32_t>());
+    SHD_TRY(scan_excl2(R.scan, R.fl_hcnt.as<uint32_t>(), R.pk_off.as<uint32_t>(), nullptr, nullptr, (uint64_t)H + 1, s));
+    if (n)
+        fl_gather<<<div_up(H, 4), 256, 0, s>>>(H, R.fl_hrun.as<uint32_t>(), R.fl_runo.as<uint32_t>(),
+                                                R.pk_off.as<uint32_t>(), R.fl_send.as<Send12>(), time_base,
+                                                R.pk_time.as<uint64_t>(), R.pk_dst.as<uint32_t>(),
+                                                R.pk_pay.as<uint32_t>(), R.draws.as<uint32_t>(),
+                                                R.fl_perm.as<uint32_t>(), R.fl_inv.as<uint32_t>());
+    SHD_HIP(hipGetLastError());
+    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 32, red, 16, hipMemcpyDeviceToHost, s));   // h_pin words 32-33
+    SHD_TRY(wait_stream(ctx, s));
+    if (ctx->h_pin[33] != ~0ull) return SHD_ERR_NO_HOST;   // a run of a host the relay does not have
+    if (ctx->h_pin[32] != ~0ull) return SHD_ERR_INVALID;   // a host with two runs (two threads, or split)
+    // 3. the round on the grouped batch with the CPU's draws (the device streams stay as they are)
+    shd_batch db{n, R.pk_off.as<uint32_t>(), R.pk_time.as<uint64_t>(), R.pk_dst.as<uint32_t>(),
+                 R.pk_pay.as<uint32_t>(), nullptr};
+    shd_relay_out dout{};
+    dout.status = R.st.as<uint8_t>();
+    dout.ev_off = R.ev_off.as<uint32_t>();
+    dout.ev_deliver = R.ev_deliver.as<uint64_t>();
+    dout.ev_src = R.ev_src.as<uint32_t>();
+    dout.ev_seq = R.ev_seq.as<uint64_t>();
+    dout.ev_pkt = R.ev_pkt.as<uint32_t>();
+    R.cpu_draws = true;
+    const shd_status st = relay_flush_round(ctx, &db, round, &dout);
+    R.cpu_draws = false;
+    SHD_TRY(st);
+    // 4. compact outputs (the round committed: next_id2 holds every host's first id of the round)
+    const uint64_t ns = dout.n_sent;
+    const uint64_t* seq_base = R.next_id2.as<uint64_t>();
+    if (n) fl_status2<<<div_up((n + 3) / 4, 256), 256, 0, s>>>(n, R.fl_inv.as<uint32_t>(), R.st.as<uint8_t>(),
+                                                              R.fl_st2.as<uint8_t>());
+    if (ns)
+        fl_events16<<<div_up(ns, 256), 256, 0, s>>>(ns, round->round_end, R.ev_deliver.as<uint64_t>(),
+                                                    R.ev_src.as<uint32_t>(), R.ev_seq.as<uint64_t>(),
+                                                    R.ev_pkt.as<uint32_t>(), seq_base, R.fl_perm.as<uint32_t>(),
+                                                    R.fl_ev16.as<uint4>());
+    SHD_HIP(hipGetLastError());
+    if (out->status2 && n) SHD_HIP(hipMemcpyAsync(out->status2, R.fl_st2.p, (n + 3) / 4, hipMemcpyDeviceToHost, s));
+    if (out->ev_off) SHD_HIP(hipMemcpyAsync(out->ev_off, R.ev_off.p, (size_t)(H + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (out->events && ns) SHD_HIP(hipMemcpyAsync(out->events, R.fl_ev16.p, ns * 16, hipMemcpyDeviceToHost, s));
+    if (out->seq_base) SHD_HIP(hipMemcpyAsync(out->seq_base, seq_base, (size_t)H * 8, hipMemcpyDeviceToHost, s));
+    SHD_TRY(wait_stream(ctx, s));
+    out->min_deliver = dout.min_deliver;
+    out->min_latency = dout.min_latency;
+    out->n_sent = ns;
+    return SHD_OK;
+}
+
+}  // extern "C"

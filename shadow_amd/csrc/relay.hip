@@ -87,6 +87,7 @@ struct RelayArgs {
     const uint32_t* dst_host;
     const uint32_t* payload;
     const double* chance;
+    const uint32_t* draw_cpu;  // CPU-drawn top 32 bits of next_u64 per packet (shd_relay_flush), or null
     const uint32_t* host_node;
     const uint64_t* lat;
     const float* loss;
@@ -125,9 +126,15 @@ __global__ __launch_bounds__(256) void relay_stamp(RelayArgs a) {
                 }
                 const size_t pi = (size_t)sn * a.n_nodes + a.host_node[d];
                 const double reliability = (double)one_minus(a.loss[pi]);
-                const double chance = a.chance ? a.chance[i] : r.gen_f64();
+                bool ge;
+                if (a.draw_cpu) {   // the top 32 bits decide exactly for a table reliability (draw_drops)
+                    bool tie = false;
+                    ge = draw_drops(a.draw_cpu[i], reliability, tie);
+                } else {
+                    ge = (a.chance ? a.chance[i] : r.gen_f64()) >= reliability;
+                }
                 const bool boot = now < a.bootstrap_end;
-                if (!boot && chance >= reliability && a.payload[i] > 0) {
+                if (!boot && ge && a.payload[i] > 0) {
                     st = kStDropped;
                 } else {
                     const uint64_t delay = a.lat[pi];
@@ -320,6 +327,7 @@ struct RelayArgs3 {
     const uint32_t* dst_host;
     const uint32_t* payload;
     const double* chance;
+    uint32_t keep_rng;         // 1: the draws came from the CPU (shd_relay_flush): device streams untouched
     const uint32_t* host_node;
     const uint32_t* order;     // the n_src source host ids sorted by host_node (workgroup -> hosts)
     const uint2* path;         // {latency ns (u32), packet loss bits} per node pair
@@ -577,7 +585,7 @@ __global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint32
     uint64_t ns = 0;
     if (tid < nh) {
         const size_t h = s_host[tid];
-        if (a.chance)
+        if (a.chance || a.keep_rng)
             for (int k = 0; k < 4; ++k) a.rng_out[4 * h + k] = a.rng[4 * h + k];
         ns = s_run[tid];
         a.next_id_out[h] = a.next_id[h] + ns;
@@ -903,7 +911,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
         }
         if (tid < nh) {
             const size_t h = s_host[tid];
-            if (a.chance)
+            if (a.chance || a.keep_rng)
                 for (int k = 0; k < 4; ++k) a.rng_out[4 * h + k] = a.rng[4 * h + k];
             ns_total += s_run[tid];
             a.next_id_out[h] = a.next_id[h] + s_run[tid];
@@ -1372,6 +1380,7 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.dst_host = b->dst_host;
     a.payload = b->payload;
     a.chance = b->chance;
+    a.draw_cpu = R.cpu_draws ? R.draws.as<uint32_t>() : nullptr;
     a.host_node = R.host_node.as<uint32_t>();
     a.lat = R.own_table ? R.lat.as<uint64_t>() : ctx->t_lat.as<uint64_t>();
     a.loss = R.own_table ? R.loss.as<float>() : ctx->t_loss.as<float>();
@@ -1883,6 +1892,7 @@ static RelayArgs3 relay_args3(shd_ctx* ctx, const shd_batch* b, const shd_round*
     a.dst_host = b->dst_host;
     a.payload = b->payload;
     a.chance = b->chance;
+    a.keep_rng = R.cpu_draws ? 1u : 0u;
     a.host_node = R.host_node.as<uint32_t>();
     a.path = R.path.as<uint2>();
     a.order = R.order.as<uint32_t>();
@@ -1919,7 +1929,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     red_init<<<1, 64, 0, s>>>(R.red.as<unsigned long long>(), R.ev_val2.as<uint32_t>());
     RelayArgs3 a = relay_args3(ctx, b, rd, o);
     const uint64_t* seq_base = a.abs_seq ? nullptr : R.next_id.as<uint64_t>();
-    if (!b->chance && R.n_src)   // K0: the per-host generator streams
+    if (!b->chance && !R.cpu_draws && R.n_src)   // K0: the per-host generator streams
         relay_draws<<<div_up(R.n_src, 64), 64, 0, s>>>(a, R.draws.as<uint32_t>());
     if (R.n_src == 0) {
     } else if (R.hn_bits) {   // host -> node map fits the LDS: persistent stamp, no node gathers
@@ -2009,7 +2019,8 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     // stream join (~12 us from its end to the stamp's start) was the longer of the two chains, so
     // its fork is issued before anything else.  The fork event follows the caller's work on the
     // stream (e.g. the kernels that wrote the batch).
-    if (!b->chance) {   // K0: the per-host generator streams, on the side stream next to the bins
+    const bool k0 = !b->chance && !R.cpu_draws;   // (shd_relay_flush filled the draws from the CPU's)
+    if (k0) {   // K0: the per-host generator streams, on the side stream next to the bins
         SHD_HIP(hipEventRecord(ctx->sev[0], s));
         SHD_HIP(hipStreamWaitEvent(ctx->side, ctx->sev[0], 0));
         relay_draws<<<div_up(R.n_src, 64), 64, 0, ctx->side>>>(a, R.draws.as<uint32_t>());
@@ -2022,10 +2033,10 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
                                                                              R.bin_cnt.as<uint32_t>());
     else
         relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
-    if (!b->chance) SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));   // after the histogram's launch
+    if (k0) SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));   // after the histogram's launch
     bin_col_scan<<<div_up(n_bins, 64), 1024, 0, s>>>(G, n_bins, R.bin_cnt.as<uint32_t>(), seg, tot, a.red);
     bin_base_scan<<<1, 1024, 0, s>>>(n_bins, tot, R.bin_base.as<uint32_t>(), R.bin_lb.as<unsigned long long>(), a.red);
-    if (!b->chance) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
+    if (k0) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
     relay_stamp_v6<true><<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4, s>>>(
         a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     V7Out vo{o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt,
@@ -2121,6 +2132,11 @@ static shd_status relay_device(shd_ctx* ctx, const shd_batch* b, const shd_round
     o->n_events = (uint32_t)o->n_sent;
     round_note(ctx, o->min_deliver, o->min_latency);
     return SHD_OK;
+}
+
+// shd_relay_flush (flush.hip): one round on the batch it grouped on the device
+shd_status relay_flush_round(shd_ctx* ctx, const shd_batch* b, const shd_round* rd, shd_relay_out* o) {
+    return relay_device(ctx, b, rd, o);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -35,6 +35,65 @@ class RoundResult:
                         self.ev_seq[a:b].tolist(), self.ev_pkt[a:b].tolist()))
 
 
+@dataclass
+class FlushResult:
+    status: np.ndarray        # u8 per send in stage order (decoded from the 2-bit statuses)
+    ev_off: np.ndarray        # u32 [n_hosts+1]
+    events: np.ndarray        # (n_sent, 4) u32: deliver - round_end, src host, seq - seq_base[src], send index
+    seq_base: np.ndarray      # u64 [n_hosts]: each host's first event id of the round
+    min_deliver: int
+    min_latency: int
+    n_sent: int
+
+
+class PinnedStages:
+    """Staging buffers for ``Relay.flush``.  ``wrap`` points the C structs at the caller's arrays;
+    ``pinned`` copies them into shd_host_alloc memory, as a drop-in's worker threads would stage
+    into pinned buffers from the start."""
+
+    def __init__(self):
+        self.stages, self.keep, self.allocs, self.n = [], [], [], 0
+        self.array = None
+
+    @classmethod
+    def wrap(cls, run_host, run_count, sends):
+        p = cls()
+        for h, c, sd in zip(run_host, run_count, sends):
+            h = np.ascontiguousarray(h, np.uint32)
+            c = np.ascontiguousarray(c, np.uint32)
+            sd = np.ascontiguousarray(sd, np.uint32).reshape(-1, 3)
+            p.keep += [h, c, sd]
+            p.stages.append(N.Stage(len(h), N.ptr(h).value, N.ptr(c).value, sd.shape[0], N.ptr(sd).value))
+            p.n += sd.shape[0]
+        p.array = (N.Stage * max(len(p.stages), 1))(*p.stages)
+        return p
+
+    @classmethod
+    def pinned(cls, lib, run_host, run_count, sends):
+        p = cls()
+        p.lib = lib
+        for h, c, sd in zip(run_host, run_count, sends):
+            sd = np.ascontiguousarray(sd, np.uint32).reshape(-1, 3)
+            views = []
+            for a in (np.ascontiguousarray(h, np.uint32), np.ascontiguousarray(c, np.uint32), sd):
+                ptr = lib.shd_host_alloc(max(a.nbytes, 1))
+                if not ptr:
+                    p.free()
+                    raise MemoryError("shd_host_alloc")
+                p.allocs.append(ptr)
+                C.memmove(ptr, a.ctypes.data, a.nbytes)
+                views.append(ptr)
+            p.stages.append(N.Stage(len(h), views[0], views[1], sd.shape[0], views[2]))
+            p.n += sd.shape[0]
+        p.array = (N.Stage * max(len(p.stages), 1))(*p.stages)
+        return p
+
+    def free(self):
+        for ptr in self.allocs:
+            self.lib.shd_host_free(ptr)
+        self.allocs = []
+
+
 def group_by_source(n_hosts: int, src_host: np.ndarray):
     """Stable grouping of staged sends by source host -> (order, src_off).
 
@@ -131,6 +190,27 @@ class Relay:
         N.check(self.eng.lib.shd_relay_round_device(self.eng.ctx, C.byref(b), C.byref(rd), C.byref(out)),
                 "shd_relay_round_device")
         return out
+
+    def flush(self, run_host, run_count, sends, time_base: int, round_end: int, sim_end: int,
+              bootstrap_end: int = 0, pinned=None) -> "FlushResult":
+        """``shd_relay_flush``: the worker threads' staging buffers as they stand (per stage: the
+        runs' hosts and counts and the (n, 3) u32 send records {time_off, dst | SEND_PAYLOAD,
+        draw_hi}).  ``pinned``: a PinnedStages holding them in pinned memory (the drop-in's path);
+        else the arrays are passed as they are."""
+        if pinned is None:
+            pinned = PinnedStages.wrap(run_host, run_count, sends)
+        n = pinned.n
+        st2 = np.zeros((n + 3) // 4, np.uint8)
+        ev_off = np.zeros(self.n_hosts + 1, np.uint32)
+        events = np.zeros((max(n, 1), 4), np.uint32)
+        seq_base = np.zeros(self.n_hosts, np.uint64)
+        out = N.FlushOut(N.ptr(st2).value, N.ptr(ev_off).value, N.ptr(events).value, N.ptr(seq_base).value, 0, 0, 0)
+        rd = N.Round(round_end, sim_end, bootstrap_end)
+        N.check(self.eng.lib.shd_relay_flush(self.eng.ctx, pinned.array, len(pinned.stages), int(time_base),
+                                             C.byref(rd), C.byref(out)), "shd_relay_flush")
+        status = ((st2[:, None] >> (np.arange(4, dtype=np.uint8) * 2)) & 3).reshape(-1)[:n]
+        return FlushResult(status, ev_off, events[:out.n_sent], seq_base, out.min_deliver, out.min_latency,
+                           out.n_sent)
 
     def host_state(self):
         rng = np.zeros((self.n_hosts, 4), np.uint64)

@@ -215,3 +215,40 @@ def packet_batch(n_hosts: int, n_packets: int, window_start: int, window_end: in
 
 def c5_host_nodes(n_hosts: int, n_nodes: int) -> np.ndarray:
     return (np.arange(n_hosts, dtype=np.uint32) % np.uint32(n_nodes)).astype(np.uint32)
+
+
+@dataclass
+class StagedRound:
+    """A grouped batch laid out as the drop-in's per-worker-thread staging buffers
+    (shd_relay_flush): stage k = one thread's buffer, its hosts' runs in the thread's run order.
+    ``stage_of_send[i]`` = the grouped index of the send at stage-order position i."""
+    run_host: list
+    run_count: list
+    sends: list            # per stage: (n, 3) u32 records {time_off, dst | payload bit, draw_hi}
+    stage_of_send: np.ndarray
+    draw64: np.ndarray     # per grouped send: the u64 the host RNG returned (chance = draw >> 11 * 2^-53)
+
+
+def stage_round(b: PacketBatch, n_threads: int, time_base: int, seed: int = 7) -> StagedRound:
+    """Spread the hosts of ``b`` over ``n_threads`` worker threads (each host on one thread, the
+    thread_per_core scheduler's invariant), every thread running its hosts in a shuffled order, and
+    draw a u64 per send for the CPU-side loss draw (worker.rs:365)."""
+    rng = np.random.default_rng(seed)
+    H = len(b.src_off) - 1
+    thread = rng.integers(0, n_threads, size=H)
+    cnt = np.diff(b.src_off.astype(np.int64))
+    draw64 = rng.integers(0, 2**64, size=len(b.send_time), dtype=np.uint64)
+    pay = (b.payload > 0).astype(np.uint32) << np.uint32(31)
+    rec_all = np.stack([(b.send_time - np.uint64(time_base)).astype(np.uint32), b.dst_host | pay,
+                        (draw64 >> np.uint64(32)).astype(np.uint32)], axis=1)
+    run_host, run_count, sends, order = [], [], [], []
+    for k in range(n_threads):
+        hs = np.flatnonzero(thread == k).astype(np.uint32)
+        rng.shuffle(hs)
+        run_host.append(hs)
+        run_count.append(cnt[hs].astype(np.uint32))
+        c = cnt[hs]
+        idx = np.repeat(b.src_off[hs].astype(np.int64) - (np.cumsum(c) - c), c) + np.arange(int(c.sum()))
+        order.append(idx.astype(np.int64))
+        sends.append(np.ascontiguousarray(rec_all[idx]))
+    return StagedRound(run_host, run_count, sends, np.concatenate(order), draw64)

@@ -1,0 +1,132 @@
+"""shd_relay_flush -- the drop-in round barrier: worker threads' staging buffers (per-thread runs of
+12-byte sends with the CPU's top-32-bit draws) grouped on the device, 2-bit statuses and 16-byte
+events back.  Against the C restatement of send_packet in CPU-chance mode (worker.rs:328-413, the
+f64 chance of each send = the same u64 draw >> 11 * 2^-53), round after round."""
+import numpy as np
+import pytest
+
+from oracle import corc
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(H, NN, seed):
+    from shadow_amd import synth
+    el = synth.complete_graph(NN, seed)
+    used = np.arange(NN, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(NN, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    return lat, loss, synth.c5_host_nodes(H, NN), synth.host_rng_states(H, 1)
+
+
+def _check(fr, o, st, nid_before, round_end):
+    inv = np.empty(len(st.stage_of_send), np.int64)
+    inv[st.stage_of_send] = np.arange(len(st.stage_of_send))
+    assert np.array_equal(fr.status, o["status"][st.stage_of_send])
+    ev = o["events"]
+    assert np.array_equal(fr.ev_off, ev["off"])
+    assert fr.n_sent == o["n_sent"] == len(fr.events)
+    e = fr.events
+    assert np.array_equal(e[:, 0].astype(np.uint64), ev["deliver"] - np.uint64(round_end))
+    assert np.array_equal(e[:, 1], ev["src"])
+    assert np.array_equal(e[:, 2].astype(np.uint64) + fr.seq_base[e[:, 1]], ev["seq"])
+    assert np.array_equal(e[:, 3].astype(np.int64), inv[ev["pkt"].astype(np.int64)])
+    assert np.array_equal(fr.seq_base, nid_before)
+    assert (fr.min_deliver, fr.min_latency) == (o["min_deliver"], o["min_latency"])
+
+
+@pytest.mark.parametrize("n_threads", [1, 16])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_flush_rounds_vs_c_oracle(engine, n_threads, pinned):
+    from shadow_amd import synth
+    from shadow_amd.relay import PinnedStages, Relay
+    H, NN, P = 20_000, 200, 1_000_000
+    lat, loss, host_node, rng0 = _case(H, NN, 21)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    onid = np.zeros(H, np.uint64)
+    start, ra = 10**9, 10**6
+    for rnd in range(3):
+        b = synth.packet_batch(H, P, start, start + ra, seed=60 + rnd)
+        st = synth.stage_round(b, n_threads, start, seed=rnd)
+        chance = (st.draw64 >> np.uint64(11)).astype(np.float64) * 2.0**-53
+        nid_before = onid.copy()
+        boot = start + ra // 2 if rnd == 0 else 0
+        o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(),
+                             onid, start + ra, start + 100 * ra, boot, chance=chance)
+        ps = PinnedStages.pinned(engine.lib, st.run_host, st.run_count, st.sends) if pinned else None
+        try:
+            fr = rl.flush(st.run_host, st.run_count, st.sends, start, start + ra, start + 100 * ra, boot, pinned=ps)
+        finally:
+            if ps is not None:
+                ps.free()
+        _check(fr, o, st, nid_before, start + ra)
+        start += ra
+    rng, nid = rl.host_state()
+    assert np.array_equal(rng, rng0)          # the device streams were not used: the CPU drew
+    assert np.array_equal(nid, onid)          # event ids advanced by the sent packets
+
+
+def test_flush_then_device_draws_round(engine):
+    """A flush round (CPU draws) followed by a device-drawn round: ids carry over, the device
+    streams start where they were."""
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    H, NN, P = 5000, 60, 200_000
+    lat, loss, host_node, rng0 = _case(H, NN, 5)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    onid = np.zeros(H, np.uint64)
+    b = synth.packet_batch(H, P, 10**9, 10**9 + 10**6, seed=1)
+    st = synth.stage_round(b, 8, 10**9, seed=2)
+    chance = (st.draw64 >> np.uint64(11)).astype(np.float64) * 2.0**-53
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(), onid,
+                         10**9 + 10**6, 10**12, 0, chance=chance)
+    fr = rl.flush(st.run_host, st.run_count, st.sends, 10**9, 10**9 + 10**6, 10**12, 0)
+    assert np.array_equal(fr.status, o["status"][st.stage_of_send])
+    b2 = synth.packet_batch(H, P, 10**9 + 10**6, 10**9 + 2 * 10**6, seed=2)
+    orng = rng0.copy()
+    o2 = corc.relay_round(b2.src_off, b2.send_time, b2.dst_host, b2.payload, host_node, lat, loss, orng, onid,
+                          10**9 + 2 * 10**6, 10**12, 0)
+    r2 = rl.round(b2.src_off, b2.send_time, b2.dst_host, b2.payload, 10**9 + 2 * 10**6, 10**12, 0)
+    assert np.array_equal(r2.status, o2["status"])
+    assert np.array_equal(r2.ev_seq, o2["events"]["seq"])
+    rng, nid = rl.host_state()
+    assert np.array_equal(rng, orng) and np.array_equal(nid, onid)
+
+
+def test_flush_rejects_bad_staging(engine):
+    from shadow_amd import synth
+    from shadow_amd._native import ShdError
+    from shadow_amd.relay import Relay
+    H, NN, P = 2000, 30, 50_000
+    lat, loss, host_node, rng0 = _case(H, NN, 9)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    b = synth.packet_batch(H, P, 10**9, 10**9 + 10**6, seed=3)
+    st = synth.stage_round(b, 4, 10**9, seed=4)
+    args = (10**9, 10**9 + 10**6, 10**12, 0)
+    # one host in two threads' buffers
+    rh = [h.copy() for h in st.run_host]
+    rh[1][0] = rh[0][0]
+    with pytest.raises(ShdError, match="INVALID"):
+        rl.flush(rh, st.run_count, st.sends, *args)
+    # a run of a host the relay does not have
+    rh = [h.copy() for h in st.run_host]
+    rh[2][3] = H + 5
+    with pytest.raises(ShdError, match="NO_HOST"):
+        rl.flush(rh, st.run_count, st.sends, *args)
+    # runs that do not cover the stage's records
+    rc = [c.copy() for c in st.run_count]
+    rc[0][0] += 1
+    with pytest.raises(ShdError, match="INVALID"):
+        rl.flush(st.run_host, rc, st.sends, *args)
+    # a destination outside the hosts
+    sd = [s.copy() for s in st.sends]
+    sd[3][7, 1] = (sd[3][7, 1] & np.uint32(0x80000000)) | np.uint32(H + 1)
+    with pytest.raises(ShdError, match="NO_HOST"):
+        rl.flush(st.run_host, st.run_count, sd, *args)
+    # nothing was committed: the next good flush matches a fresh oracle round
+    onid = np.zeros(H, np.uint64)
+    chance = (st.draw64 >> np.uint64(11)).astype(np.float64) * 2.0**-53
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(), onid,
+                         10**9 + 10**6, 10**12, 0, chance=chance)
+    fr = rl.flush(st.run_host, st.run_count, st.sends, *args)
+    _check(fr, o, st, np.zeros(H, np.uint64), 10**9 + 10**6)

@@ -122,6 +122,8 @@ def test_c2_repeated_runs_bit_exact(engine, c2_case, group, knob):
     from shadow_amd import _native as N
     if group:
         knob("SSSP_G", int(group))
+    # the dense-CSR prune (no dense_build) and the dense_build one
+    knob("PRUNE_DENSE_BUILD", 1 if group == "4" else 0)
     el, used, lat, loss = c2_case
     g = engine_graph_from_edges(el)._cgraph()
     err = N.Error()
