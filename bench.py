@@ -304,6 +304,8 @@ def c3_leg(eng, reps=2, cpu=True):
                                        "work": "2 V^3 int ops (add + min) of the min-plus closure"})
         else:
             res[name]["roofline"] = sssp_roofline(n, arcs, n, i["ms_main"])
+            if name == "delta":   # the AUTO engine's kernel: PMC bytes per launch (profiles/pmc_traffic.json)
+                res[name]["roofline"]["traffic"] = load_pmc("c3")
     best = min(v["ms_total"] for v in res.values())
     out = dict(workload="C3: 10k-node Barabasi-Albert m=3 + self-loops, all 10k rows",
                nodes=n, arcs=arcs, node_pairs_per_s=n * n / (best * 1e-3), algorithms=res)
@@ -339,6 +341,8 @@ def c4_leg(eng, world, rank, steps, gather=True, cpu=True):
                sssp_kernel_ms_per_rank=kernel_ms, value=n * n / (r["ms_per_step"] * 1e-3),
                unit="node-pairs/s", scaling="strong", all_gather=bool(gather),
                roofline=sssp_roofline(r["rows"], arcs, n, kernel_ms))
+    if world == 1:   # PMC bytes of one full-build launch (profiles/pmc_traffic.json)
+        out["roofline"]["traffic"] = load_pmc("c4")
     if world > 1:   # the rank holding the last 64 rows (claimed rows of its slots) checks them
         from oracle import corc
         lo = n - 64

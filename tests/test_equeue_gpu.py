@@ -230,3 +230,50 @@ def test_c5_scale_rounds_vs_c_queues(engine):
         p = q.popped(q.advance_device(None, w_end))
         _cmp_popped(p, oq.pop(w_end, threads=corc.max_threads()))
     assert p.n_pending == 0
+
+
+def test_c5_scale_adopted_rounds_with_compaction_vs_c_queues(engine):
+    """The bench's path at full C5 size for 12 rounds: each round's relay output is written into the
+    slot shd_equeue_batch_buffers lends and adopted as a stored run; 1 ms windows over 1-300 ms
+    paths keep every run alive, so from round 9 on the 8-run limit forces the partial compactions
+    (the runs holding the fewest pending events merged into one) at ~40-100M pending events.  Every
+    popped event, the pending count and the next time against the C EventQueues, then a drain."""
+    from shadow_amd import synth
+    from shadow_amd.equeue import EventQueues
+    from shadow_amd.relay import Relay
+    import torch
+    H, P = 100_000, 10_000_000
+    el = synth.complete_graph(1000, 1)
+    used = np.arange(1000, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(1000, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    host_node = synth.c5_host_nodes(H, 1000)
+    rng0 = synth.host_rng_states(H, 1)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    q = EventQueues(engine, H)
+    oq = corc.EventQueues(H)
+    orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+    st = torch.empty(P, dtype=torch.uint8, device="cuda")
+    start, win, end = synth.SIM_START + 10**9, 10**6, synth.SIM_START + 10**12
+    dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()  # noqa: E731
+    for rnd in range(12):
+        b = synth.packet_batch(H, P, start, start + win, seed=240 + rnd)
+        d = [dev(b.src_off, np.int32), dev(b.send_time, np.int64), dev(b.dst_host, np.int32),
+             dev(b.payload, np.int32)]
+        torch.cuda.synchronize()
+        out = q.batch_buffers(P)
+        out.status = st.data_ptr()
+        rl.round_device_into(*d, start + win, end, 0, out)
+        o = corc.relay_round_eq(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, orng, onid,
+                                start + win, end, 0, queues=oq, batch_no=rnd, threads=corc.max_threads())
+        assert out.n_sent == o["n_sent"] and out.min_deliver == o["min_deliver"]
+        p = q.popped(q.advance_device(out, start + 2 * win))
+        op = oq.pop(start + 2 * win, threads=corc.max_threads())
+        _cmp_popped(p, op)
+        start += win
+        del d
+    assert p.n_pending > 40_000_000   # ~4 rounds of events stay pending (1-300 ms paths)
+    for w_end in (start + 150 * win, 2**63):
+        p = q.popped(q.advance_device(None, w_end))
+        _cmp_popped(p, oq.pop(w_end, threads=corc.max_threads()))
+    assert p.n_pending == 0

@@ -49,6 +49,19 @@ relay = per_launch("relay", lambda k: any(s in k for s in relay_sel))
 rounds = sum(v[2] for k, v in relay.items() if "relay_stamp" in k)
 rel_read = sum(v[0] * v[2] for v in relay.values()) / rounds
 rel_write = sum(v[1] * v[2] for v in relay.values()) / rounds
+def one_kernel(run, sel):
+    """(read, write, launches) of the kernel matching sel in a run, or None when the run is absent"""
+    if not os.path.exists(os.path.join(src, f"{run}_FETCH_SIZE")):
+        return None
+    d = per_launch(run, sel)
+    n = sum(v[2] for v in d.values())
+    if not n:
+        return None
+    return (sum(v[0] * v[2] for v in d.values()) / n, sum(v[1] * v[2] for v in d.values()) / n, n)
+
+
+c3 = one_kernel("c3", lambda k: "sssp_lds_group" in k)
+c4 = one_kernel("c4", lambda k: "sssp_global_group" in k)
 doc = {
     "source": "tools/pmc_traffic.sh + tools/pmc_traffic.py (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE in "
               "separate runs: routing from bench.py --no-relay (C2 builds), relay from tools/relay_only.py 10 "
@@ -62,16 +75,25 @@ doc = {
                                                         "write_bytes": v[1]}
                                  for k, v in relay.items()}},
 }
+for name, v, what in (("c3", c3, "sssp_lds_group on the whole C3 build (AUTO = delta buckets)"),
+                      ("c4", c4, "sssp_global_group on one full C4 build (global-label delta-stepping)")):
+    if v:
+        doc[name] = v[0] + v[1]
+        doc[name + "_detail"] = {"kernel": what, "read_bytes": v[0], "write_bytes": v[1], "launches": v[2],
+                                 "note": "read factor calibrated on streaming reads; these kernels' reads are "
+                                         "random 8-byte label accesses (an uncalibrated width, guide HBM section)"}
 os.makedirs(os.path.dirname(dst), exist_ok=True)
 json.dump(doc, open(dst, "w"), indent=1)
-print(json.dumps({k: doc[k] for k in ("read_factor", "write_factor_measured", "routing", "relay")}))
+print(json.dumps({k: doc.get(k) for k in ("read_factor", "write_factor_measured", "routing", "relay", "c3", "c4")}))
 
 # the raw per-kernel means behind the numbers above (KB per launch, uncalibrated)
 if len(sys.argv) > 3:
     with open(sys.argv[3], "w", newline="") as f:
         wr = csv.writer(f)
         wr.writerow(["run", "counter", "kernel", "launches", "mean_KB"])
-        for run in ("probe", "bench", "relay"):
+        for run in ("probe", "bench", "relay", "c3", "c4"):
+            if not os.path.exists(os.path.join(src, f"{run}_FETCH_SIZE")):
+                continue
             for c in ("FETCH_SIZE", "WRITE_SIZE"):
                 for k, v in sorted(load(run, c).items()):
                     wr.writerow([run, c, k.split("(")[0], len(v), round(sum(v) / len(v) / 1e3, 1)])
