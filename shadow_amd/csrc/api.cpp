@@ -1,5 +1,6 @@
 // C ABI entry points (include/shd_accel.h): context lifetime, routing build front ends,
 // resident-table lookups.  The relay entry points live in relay.hip.
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -59,6 +60,31 @@ shd_status wait_stream(shd_ctx* ctx, hipStream_t s) {
     if (*done != 1) SHD_HIP(hipStreamSynchronize(s));
     return SHD_OK;
 }
+shd_status readback_launch(hipStream_t s, const void* d_src, uint32_t n_words, unsigned long long* h_dst,
+                           unsigned long long* h_marker);
+
+// n_bytes (a multiple of 8) from device memory into the pinned words h_pin[at ...], and wait for
+// everything before it on stream s: one kernel writes the words and then the marker the host polls
+// (rounds.hip readback_mark), or -- SHD_SYNC_KERNEL=0 -- a D2H copy followed by wait_stream's marker
+// copy.  A wait past 20 ms falls back to hipStreamSynchronize, which also reports a failed kernel.
+shd_status readback(shd_ctx* ctx, hipStream_t s, int at, const void* d_src, size_t n_bytes) {
+    if (!ctx->spin_wait || ctx->knobs.get(K_SYNC_KERNEL, 1) == 0) {
+        SHD_HIP(hipMemcpyAsync(ctx->h_pin + at, d_src, n_bytes, hipMemcpyDeviceToHost, s));
+        return wait_stream(ctx, s);
+    }
+    volatile unsigned long long* done = ctx->h_pin + kPinMarker;
+    *done = 0;
+    SHD_TRY(readback_launch(s, d_src, (uint32_t)(n_bytes / 8), ctx->h_pin + at,
+                            const_cast<unsigned long long*>(done)));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1; *done != 1; ++i) {
+        __builtin_ia32_pause();
+        if ((i & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+    }
+    if (*done != 1) SHD_HIP(hipStreamSynchronize(s));
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return SHD_OK;
+}
 }  // namespace shd
 
 extern "C" {
@@ -110,8 +136,9 @@ shd_ctx* shd_open(int device_ordinal, shd_status* st) {
         return fail(SHD_ERR_HIP);
     }
     ctx->own_stream = true;
+    // coherent (fine-grained) pinned words: readback_mark's stores reach the host without a cache
     if (hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pin), shd::kPinWords * sizeof(unsigned long long),
-                      hipHostMallocDefault) != hipSuccess) {
+                      hipHostMallocCoherent) != hipSuccess) {
         ctx->h_pin = nullptr;
         shd_close(ctx);
         return fail(SHD_ERR_HIP);

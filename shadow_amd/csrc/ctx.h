@@ -61,6 +61,7 @@ struct EqRunBuf {   // one stored run of the event queues: a CSR of per-host sor
     DevBuf off, deliver, src, seq, tag;
     DevBuf pkt;                 // an adopted relay output keeps ev_pkt: tag = batch << 32 | pkt
     bool has_pkt = false;
+    bool fresh = false;         // adopted by the running advance: its cursor is its offsets
     uint64_t batch = 0;
     uint64_t n = 0, left = 0;   // events stored / not yet popped
     bool live = false;
@@ -176,6 +177,8 @@ constexpr int kPinWords = 72;       // h_pin words; [64] is wait_stream's marker
 constexpr int kPinMarker = 64;
 // Wait until everything enqueued on stream s has finished (see api.cpp)
 shd_status wait_stream(shd_ctx* ctx, hipStream_t s);
+// n_bytes of device words into h_pin[at ...] and wait for the stream (api.cpp)
+shd_status readback(shd_ctx* ctx, hipStream_t s, int at, const void* d_src, size_t n_bytes);
 // a committed relay round's (all-rank) reductions: the runahead update (runahead.rs:60-115) and
 // the earliest deliver time of the relay output that the queues have not merged yet (rounds.cpp)
 void round_note(shd_ctx* ctx, uint64_t min_deliver, uint64_t min_latency);

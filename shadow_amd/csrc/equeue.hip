@@ -159,21 +159,13 @@ struct EqOut {
 #endif
 constexpr uint32_t kEqStage = 160;   // 17.5 KB per 4-wave workgroup: 8 workgroups (32 waves) per CU
 
-__global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, const uint32_t* __restrict__ pop_off,
-                                                 EqOut popped, EqOut nrun, const uint32_t* __restrict__ nrun_off,
-                                                 uint32_t* __restrict__ nrun_cur, const uint2* __restrict__ ranges) {
-    __shared__ uint64_t s_t[4][kEqStage], s_q[4][kEqStage], s_g[4][kEqStage];
-    __shared__ uint32_t s_s[4][kEqStage];
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t h = blockIdx.x * 4 + w;
-    if (h >= n_hosts) return;   // wave-uniform; the kernel has no workgroup barrier
-    // lane k < S.n holds source k's popped range and its place in the LDS stage
-    uint32_t my_lo = 0, my_m = 0;
-    if (lane < S.n) {   // eqr_count's (cursor, cut) pairs of this host: one line
-        const uint2 r = ranges[(size_t)h * kEqSrcMax + lane];
-        my_lo = r.x;
-        my_m = r.y;
-    }
+// One host's merge (a wave): lane k < S.n holds source k's popped range [my_lo, my_m); po is the
+// host's first popped slot, rb_no its first slot in the new run (a batch source only).
+__device__ __forceinline__ void eq_merge_host(uint32_t h, uint32_t w, uint32_t lane, const EqSrcs& S, uint32_t my_lo,
+                                              uint32_t my_m, uint32_t po, EqOut popped, EqOut nrun, uint32_t rb_no,
+                                              uint32_t* __restrict__ nrun_cur, uint64_t (*s_t)[kEqStage],
+                                              uint64_t (*s_q)[kEqStage], uint64_t (*s_g)[kEqStage],
+                                              uint32_t (*s_s)[kEqStage]) {
     const uint32_t cnt = my_m - my_lo;
     uint32_t incl = cnt;
     for (uint32_t o = 1; o < 64; o <<= 1) {
@@ -190,10 +182,9 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
         u_c[k] = __builtin_amdgcn_readlane(cnt, k);
         u_sb[k] = __builtin_amdgcn_readlane(my_sb, k);
     }
-    const uint32_t po = pop_off[h];
     // the batch remainder's first 128 events are loaded up front: their latency overlaps the
     // merge instead of following it (its cut is the batch range's end from eqr_count)
-    uint32_t rb_m = 0, rb_e = 0, rb_no = 0;
+    uint32_t rb_m = 0, rb_e = 0;
     uint64_t pf_t[2] = {0, 0}, pf_q[2] = {0, 0};
     uint32_t pf_s[2] = {0, 0}, pf_p[2] = {0, 0};
     if (S.b >= 0) {
@@ -202,7 +193,6 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
         for (uint32_t k = 0; k < kEqSrcMax; ++k)
             if ((int32_t)k == S.b) rb_m = u_lo[k] + u_c[k];
         rb_e = q.off[h + 1];
-        rb_no = nrun_off[h];
 #pragma unroll
         for (uint32_t u = 0; u < 2; ++u) {
             const uint32_t j = rb_m + lane + 64 * u;
@@ -339,6 +329,230 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
     }
 }
 
+
+__global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, const uint32_t* __restrict__ pop_off,
+                                                 EqOut popped, EqOut nrun, const uint32_t* __restrict__ nrun_off,
+                                                 uint32_t* __restrict__ nrun_cur, const uint2* __restrict__ ranges) {
+    __shared__ uint64_t s_t[4][kEqStage], s_q[4][kEqStage], s_g[4][kEqStage];
+    __shared__ uint32_t s_s[4][kEqStage];
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t h = blockIdx.x * 4 + w;
+    if (h >= n_hosts) return;   // wave-uniform; the kernel has no workgroup barrier
+    // lane k < S.n holds source k's popped range and its place in the LDS stage
+    uint32_t my_lo = 0, my_m = 0;
+    if (lane < S.n) {   // eqr_count's (cursor, cut) pairs of this host: one line
+        const uint2 r = ranges[(size_t)h * kEqSrcMax + lane];
+        my_lo = r.x;
+        my_m = r.y;
+    }
+    eq_merge_host(h, w, lane, S, my_lo, my_m, pop_off[h], popped, nrun, S.b >= 0 ? nrun_off[h] : 0u, nrun_cur,
+                  s_t, s_q, s_g, s_s);
+}
+
+// Sixteen lanes per host (EQ_WAVE_MERGE=0; tuning variant, NOT the default): for queues popping
+// a few events per host and round, four hosts a wave put four hosts' load chains in flight in the
+// slot a wave-per-host merge leaves mostly idle.  C5 pops ~100 per host (100k hosts, 9.9M events),
+// past this kernel's 64-event stage, so most hosts take its global-search path: 525 us a launch
+// against eqr_merge's 182.5 (rocprofv3 kernel trace, tools/equeue_only.py, round 4).  The same merge: lane l < S.n holds source l's range, popped events are staged in LDS
+// (kEqStage16 a host; times, sources, sequence numbers -- the tags stay in the lanes' registers),
+// each staged event's rank = its index in its source + a bisection per other source; a host
+// popping more searches global memory; then the batch remainder goes to the new run.  The four
+// groups of a wave share nothing in LDS but their own rows, so a wave barrier is the only sync.
+constexpr uint32_t kEqG = 16;          // lanes per host
+constexpr uint32_t kEqStage16 = 64;    // staged popped events per host (4 per lane)
+constexpr uint32_t kEqPre16 = 4;       // batch remainder events per lane loaded up front
+static_assert(kEqSrcMax <= kEqG, "a lane per source");
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256) void eqr_merge16(uint32_t n_hosts, EqSrcs S, const uint32_t* __restrict__ pop_off,
+                                                   EqOut popped, EqOut nrun, const uint32_t* __restrict__ nrun_off,
+                                                   uint32_t* __restrict__ nrun_cur, const uint2* __restrict__ ranges) {
+    __shared__ uint64_t s_t[16][kEqStage16], s_q[16][kEqStage16];
+    __shared__ uint32_t s_s[16][kEqStage16];
+    __shared__ uint32_t s_lo[16][kEqSrcMax], s_c[16][kEqSrcMax], s_sb[16][kEqSrcMax];
+    const uint32_t g = threadIdx.x / kEqG, l = threadIdx.x % kEqG;
+    const uint32_t h = blockIdx.x * 16 + g;
+    const bool live = h < n_hosts;   // not wave-uniform: a dead group runs every loop zero times
+    uint32_t lo = 0, m = 0, po = 0, rb_no = 0, rb_e = 0;
+    if (live) {
+        if (l < S.n) {
+            const uint2 r = ranges[(size_t)h * kEqSrcMax + l];
+            lo = r.x;
+            m = r.y;
+        }
+        po = pop_off[h];
+        if (S.b >= 0) {
+            rb_no = nrun_off[h];
+            rb_e = S.s[S.b].off[h + 1];
+        }
+    }
+    const uint32_t cnt = m - lo;
+    uint32_t incl = cnt;
+    for (uint32_t o = 1; o < kEqG; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, kEqG);
+        if (l >= o) incl += y;
+    }
+    const uint32_t npop = __shfl(incl, kEqG - 1, kEqG);
+    if (l < kEqSrcMax) {
+        s_lo[g][l] = lo;
+        s_c[g][l] = cnt;
+        s_sb[g][l] = incl - cnt;
+    }
+    wave_sync_lds();
+    uint32_t u_lo[kEqSrcMax], u_c[kEqSrcMax], u_sb[kEqSrcMax];
+#pragma unroll
+    for (uint32_t k = 0; k < kEqSrcMax; ++k) {
+        u_lo[k] = s_lo[g][k];
+        u_c[k] = s_c[g][k];
+        u_sb[k] = s_sb[g][k];
+    }
+    // the batch remainder [rb_m, rb_e): its first kEqPre16 x 16 events loaded before the merge
+    uint32_t rb_m = rb_e;
+    uint64_t pf_t[kEqPre16], pf_q[kEqPre16];
+    uint32_t pf_s[kEqPre16], pf_p[kEqPre16];
+    if (S.b >= 0) {
+        const EqSrc& q = S.s[S.b];
+        if (live) {
+#pragma unroll
+            for (uint32_t k = 0; k < kEqSrcMax; ++k)
+                if ((int32_t)k == S.b) rb_m = u_lo[k] + u_c[k];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kEqPre16; ++u) {
+            const uint32_t j = rb_m + l + kEqG * u;
+            if (j < rb_e) {
+                pf_t[u] = q.deliver[j];
+                pf_s[u] = q.src[j];
+                pf_q[u] = q.seq[j];
+                pf_p[u] = q.pkt[j];
+            }
+        }
+    }
+    if (npop <= kEqStage16) {
+        // staged event i = l + 16 u, straight from its source (pointer selects on group-uniform
+        // values, every source's loads in flight at once); its tag stays in this lane
+        uint64_t tg[kEqStage16 / kEqG];
+        uint32_t ks[kEqStage16 / kEqG];
+#pragma unroll
+        for (uint32_t u = 0; u < kEqStage16 / kEqG; ++u) {
+            const uint32_t i = l + kEqG * u;
+            ks[u] = 0;
+            if (i < npop) {
+                uint32_t at = u_lo[0] + i, k = 0;
+#pragma unroll
+                for (uint32_t j = 1; j < kEqSrcMax; ++j)
+                    if (j < S.n && u_sb[j] <= i) {
+                        at = u_lo[j] + (i - u_sb[j]);
+                        k = j;
+                    }
+                const uint64_t* dl = S.s[0].deliver;
+                const uint64_t* qp = S.s[0].seq;
+                const uint32_t* sp = S.s[0].src;
+                const uint64_t* tp = S.s[0].tag;
+                const uint32_t* pp = S.s[0].pkt;
+                uint64_t bt = S.s[0].batch;
+#pragma unroll
+                for (uint32_t j = 1; j < kEqSrcMax; ++j)
+                    if (j == k) {
+                        dl = S.s[j].deliver;
+                        qp = S.s[j].seq;
+                        sp = S.s[j].src;
+                        tp = S.s[j].tag;
+                        pp = S.s[j].pkt;
+                        bt = S.s[j].batch;
+                    }
+                ks[u] = k;
+                s_t[g][i] = dl[at];
+                s_q[g][i] = qp[at];
+                s_s[g][i] = sp[at];
+                tg[u] = tp ? tp[at] : ((bt << 32) | pp[at]);
+            }
+        }
+        wave_sync_lds();
+#pragma unroll
+        for (uint32_t u = 0; u < kEqStage16 / kEqG; ++u) {
+            const uint32_t i = l + kEqG * u;
+            if (i >= npop) continue;
+            const uint32_t k = ks[u];
+            const uint64_t t = s_t[g][i], qq = s_q[g][i];
+            const uint32_t sv = s_s[g][i];
+            uint32_t rank = i - u_sb[k];
+            for (uint32_t k2 = 0; k2 < S.n; ++k2) {
+                if (k2 == k) continue;
+                const uint32_t sb2 = u_sb[k2];
+                uint32_t a = 0, b = u_c[k2];
+                while (a < b) {
+                    const uint32_t mid = (a + b) >> 1, x = sb2 + mid;
+                    const uint64_t tm = s_t[g][x];
+                    const bool less = tm != t ? tm < t : eq_less(tm, s_s[g][x], s_q[g][x], t, sv, qq);
+                    if (less) a = mid + 1; else b = mid;
+                }
+                rank += a;
+            }
+            popped.deliver[po + rank] = t;
+            popped.src[po + rank] = sv;
+            popped.seq[po + rank] = qq;
+            popped.tag[po + rank] = tg[u];
+        }
+    } else {
+        for (uint32_t k = 0; k < S.n; ++k) {
+            const EqSrc& q = S.s[k];
+            const uint32_t lo1 = u_lo[k], c = u_c[k];
+            for (uint32_t i = l; i < c; i += kEqG) {
+                const uint64_t t = q.deliver[lo1 + i], qq = q.seq[lo1 + i];
+                const uint32_t sv = q.src[lo1 + i];
+                const uint64_t tg = q.tag ? q.tag[lo1 + i] : ((q.batch << 32) | q.pkt[lo1 + i]);
+                uint32_t rank = i;
+                for (uint32_t k2 = 0; k2 < S.n; ++k2) {
+                    if (k2 == k) continue;
+                    const EqSrc& r = S.s[k2];
+                    const uint32_t lo2 = u_lo[k2];
+                    uint32_t a = 0, b = u_c[k2];
+                    while (a < b) {
+                        const uint32_t mid = (a + b) >> 1;
+                        const uint64_t tm = r.deliver[lo2 + mid];
+                        const bool less =
+                            tm != t ? tm < t : eq_less(tm, r.src[lo2 + mid], r.seq[lo2 + mid], t, sv, qq);
+                        if (less) a = mid + 1; else b = mid;
+                    }
+                    rank += a;
+                }
+                popped.deliver[po + rank] = t;
+                popped.src[po + rank] = sv;
+                popped.seq[po + rank] = qq;
+                popped.tag[po + rank] = tg;
+            }
+        }
+    }
+    if (S.b >= 0) {   // the batch's remainder becomes the new run, whose cursor starts at its offset
+        const EqSrc& q = S.s[S.b];
+#pragma unroll
+        for (uint32_t u = 0; u < kEqPre16; ++u) {
+            const uint32_t j = rb_m + l + kEqG * u;
+            if (j < rb_e) {
+                const uint32_t at = rb_no + (j - rb_m);
+                nrun.deliver[at] = pf_t[u];
+                nrun.src[at] = pf_s[u];
+                nrun.seq[at] = pf_q[u];
+                nrun.tag[at] = (q.batch << 32) | pf_p[u];
+            }
+        }
+        for (uint32_t j = rb_m + kEqPre16 * kEqG + l; j < rb_e; j += kEqG) {
+            const uint32_t at = rb_no + (j - rb_m);
+            nrun.deliver[at] = q.deliver[j];
+            nrun.src[at] = q.src[j];
+            nrun.seq[at] = q.seq[j];
+            nrun.tag[at] = (q.batch << 32) | q.pkt[j];
+        }
+        if (live && l == 0) nrun_cur[h] = rb_no;
+    }
+}
+
 // the call's totals (popped, kept batch events, head time, left per source) from eqr_count's
 // per-block partials, into one word array the host reads with one copy
 __global__ __launch_bounds__(1024) void eq_totals(uint32_t n_hosts, uint32_t n_part, const uint32_t* __restrict__ pop_off,
@@ -390,6 +604,7 @@ static shd_status eq_run_alloc(EqRunBuf& r, uint32_t n_hosts, uint64_t n) {
     SHD_TRY(r.seq.ensure(m * 8));
     SHD_TRY(r.tag.ensure(m * 8));
     r.has_pkt = false;
+    r.fresh = false;
     return SHD_OK;
 }
 
@@ -409,6 +624,7 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
     const uint32_t H = Q.n_hosts;
     unsigned long long* words = Q.next.as<unsigned long long>();
     unsigned long long* part = words + kEqWords;
+    const EqOut nr = nrun ? eq_run_out(*nrun) : EqOut{};
     const uint32_t gx = ctx->knobs.get(K_EQ_COUNT_BLOCKS, 0);
     const uint32_t grid_max = gx >= 1 && gx <= kEqCountBlocksMax ? gx : kEqCountBlocks;
     const uint32_t nb = std::min<uint32_t>(grid_max, div_up(((uint64_t)H + 1) * kEqLanes, 256));
@@ -419,14 +635,18 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
     // the popped offsets and the new run's offsets: one hand-written look-back scan launch (scan.h)
     SHD_TRY(scan_excl2(Q.scan, Q.pop_cnt.as<uint32_t>(), out_off, nrun ? Q.keep_cnt.as<uint32_t>() : nullptr,
                        nrun ? nrun->off.as<uint32_t>() : nullptr, H + 1, s));
-    const EqOut nr = nrun ? eq_run_out(*nrun) : EqOut{};
-    if (n_in)
-        eqr_merge<<<div_up(H, 4), 256, 0, s>>>(H, S, out_off, out, nr, nrun ? nrun->off.as<uint32_t>() : nullptr,
-                                               nrun_cur, Q.ranges.as<uint2>());
+    if (n_in) {
+        if (ctx->knobs.get(K_EQ_WAVE_MERGE, 1) != 0)   // default: a wave a host (faster on C5, see eqr_merge16)
+            eqr_merge<<<div_up(H, 4), 256, 0, s>>>(H, S, out_off, out, nr, nrun ? nrun->off.as<uint32_t>() : nullptr,
+                                                   nrun_cur, Q.ranges.as<uint2>());
+        else
+            eqr_merge16<<<div_up(H, 16), 256, 0, s>>>(H, S, out_off, out, nr,
+                                                      nrun ? nrun->off.as<uint32_t>() : nullptr, nrun_cur,
+                                                      Q.ranges.as<uint2>());
+    }
     SHD_HIP(hipGetLastError());
     eq_totals<<<1, 1024, 0, s>>>(H, nb, out_off, nrun ? nrun->off.as<uint32_t>() : nullptr, part, words);
-    SHD_HIP(hipMemcpyAsync(ctx->h_pin + kEqPinWord, words, kEqWords * 8, hipMemcpyDeviceToHost, s));
-    return wait_stream(ctx, s);
+    return readback(ctx, s, kEqPinWord, words, kEqWords * 8);
 }
 
 static uint32_t* eq_cursor(EqState& Q, int buf, int slot) {
@@ -442,7 +662,8 @@ static EqSrcs eq_sources(EqState& Q, int* slots, const bool* pick = nullptr) {
         EqRunBuf& R = Q.run[r];
         if (!R.live || (pick && !pick[r])) continue;
         slots[S.n] = r;
-        S.s[S.n++] = EqSrc{R.off.as<uint32_t>(), eq_cursor(Q, Q.ccur, r), eq_cursor(Q, 1 - Q.ccur, r),
+        // a run adopted by this call has no cursor yet: it starts at its offsets (lo = null)
+        S.s[S.n++] = EqSrc{R.off.as<uint32_t>(), R.fresh ? nullptr : eq_cursor(Q, Q.ccur, r), eq_cursor(Q, 1 - Q.ccur, r),
                            R.deliver.as<uint64_t>(), R.src.as<uint32_t>(), R.seq.as<uint64_t>(),
                            R.has_pkt ? nullptr : R.tag.as<uint64_t>(), R.has_pkt ? R.pkt.as<uint32_t>() : nullptr,
                            R.batch};
@@ -604,7 +825,7 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     if (adopt) {
         const int t = Q.lend;
         EqRunBuf& R = Q.run[t];
-        SHD_HIP(hipMemcpyAsync(eq_cursor(Q, Q.ccur, t), R.off.p, (size_t)H * 4, hipMemcpyDeviceToDevice, ctx->stream));
+        R.fresh = n_b > 0;   // the pass below reads its cursor from its offsets (no cursor copy)
         R.has_pkt = true;
         R.batch = Q.batches;
         R.n = R.left = n_b;
@@ -656,6 +877,7 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
         EqRunBuf& R = Q.run[slots[k]];
         R.left = wd[4 + k];
         R.live = R.left > 0;
+        R.fresh = false;   // its cursor is in the cut buffer now
     }
     if (has_b) {
         nrun->n = nrun->left = n_keep;

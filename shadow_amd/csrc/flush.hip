@@ -203,8 +203,7 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
                                                 R.pk_pay.as<uint32_t>(), R.draws.as<uint32_t>(),
                                                 R.fl_perm.as<uint32_t>(), R.fl_inv.as<uint32_t>());
     SHD_HIP(hipGetLastError());
-    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 32, red, 16, hipMemcpyDeviceToHost, s));   // h_pin words 32-33
-    SHD_TRY(wait_stream(ctx, s));
+    SHD_TRY(readback(ctx, s, 32, red, 16));   // h_pin words 32-33
     if (ctx->h_pin[33] != ~0ull) return SHD_ERR_NO_HOST;   // a run of a host the relay does not have
     if (ctx->h_pin[32] != ~0ull) return SHD_ERR_INVALID;   // a host with two runs (two threads, or split)
     // 3. the round on the grouped batch with the CPU's draws (the device streams stay as they are)

@@ -1958,8 +1958,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
                                            spare, rd->round_end, seq_base,
                                            o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt);
     SHD_HIP(hipGetLastError());
-    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 8, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    SHD_TRY(wait_stream(ctx, s));
+    SHD_TRY(readback(ctx, s, 8, R.red.p, 8 * sizeof(unsigned long long)));
     std::memcpy(R.red_host, ctx->h_pin + 8, sizeof(R.red_host));
     return SHD_OK;
 }
@@ -2046,8 +2045,7 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
                                              R.bin_lb.as<unsigned long long>(), o->ev_off, vo, a.red,
                                              stop);
     SHD_HIP(hipGetLastError());
-    SHD_HIP(hipMemcpyAsync(ctx->h_pin + 8, R.red.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    SHD_TRY(wait_stream(ctx, s));
+    SHD_TRY(readback(ctx, s, 8, R.red.p, 8 * sizeof(unsigned long long)));
     std::memcpy(R.red_host, ctx->h_pin + 8, sizeof(R.red_host));
     return SHD_OK;
 }

@@ -47,6 +47,25 @@ static void window_of(uint64_t min_next, uint64_t ra, uint64_t end_time, uint64_
     *run = start < end ? 1 : 0;
 }
 
+// The read-back of a call's few result words and its completion marker in ONE launch: a wave
+// copies the words into the pinned host words, a system-scope release orders them before the
+// marker, which the host polls (shd::readback).  Replaces a D2H copy plus the marker copy -- two
+// DMA operations of a few microseconds each -- on every synchronous call (SHD_SYNC_KERNEL=0: the
+// copies).
+__global__ __launch_bounds__(64) void readback_mark(const unsigned long long* __restrict__ src, uint32_t n,
+                                                    unsigned long long* dst, unsigned long long* marker) {
+    for (uint32_t i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // every lane's words reach the host first
+    if (threadIdx.x == 0) __hip_atomic_store(marker, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+shd_status readback_launch(hipStream_t s, const void* d_src, uint32_t n_words, unsigned long long* h_dst,
+                           unsigned long long* h_marker) {
+    readback_mark<<<1, 64, 0, s>>>(static_cast<const unsigned long long*>(d_src), n_words, h_dst, h_marker);
+    SHD_HIP(hipGetLastError());
+    return SHD_OK;
+}
+
 // one gather of n (row, col) pairs of the resident table
 __global__ __launch_bounds__(256) void lookup_gather(uint64_t n, const uint32_t* __restrict__ rows,
                                                      const uint32_t* __restrict__ cols, uint32_t n_cols,

@@ -173,6 +173,10 @@ __device__ __forceinline__ void relax_node_pad(uint32_t u, uint32_t gl, uint64_t
     }
 }
 
+// LDS kernels on unpadded lists: a queued node of more than kHubDeg arcs is relaxed by its whole
+// wave (sssp_row).  C3 (BA m = 3, 10k nodes), full build on one box: off 8.80-8.85 ms, 16: 7.27,
+// 32: 7.02, 64: 7.18, 128: 7.62 (SHD_SSSP_HUB; 0 = off)
+constexpr uint32_t kHubDeg = 32;
 constexpr uint32_t kQCap = 64;   // per-wave expansion queue: flushed at kQCap, one scan step adds <= 64
 constexpr uint32_t kQStride = kQCap + 64;
 constexpr uint32_t kFlatWords = 257;   // per-wave scratch of expand_flat: pre[65], beg, lat, q [64]
@@ -436,7 +440,8 @@ __device__ __forceinline__ void sssp_row(
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
     uint32_t seed_stride, uint8_t* bkt, uint32_t* flat, uint32_t* nh_out, uint32_t* pred,
     uint32_t lat_guard, const uint2* __restrict__ arcs8 = nullptr, const float* __restrict__ aq = nullptr,
-    uint32_t* offl = nullptr, uint64_t* llab = nullptr, uint32_t kl = 0, uint32_t* wmin = nullptr) {
+    uint32_t* offl = nullptr, uint64_t* llab = nullptr, uint32_t kl = 0, uint32_t* wmin = nullptr,
+    uint32_t hub_deg = 0) {
     // bkt (global labels + delta-stepping): per node, the bucket of the latency that last
     // activated it, in LDS, so choosing a sweep's nodes reads no global label
     constexpr uint32_t NW = BLOCK / 64, NG = 64 / G;
@@ -562,15 +567,48 @@ __device__ __forceinline__ void sssp_row(
                 expand_flat<false>(q, qn, lane, lab, bits, CACHE ? rng : nullptr, abeg, aend, arcs,
                                    flat + wave * kFlatWords, ovf, dirty, nullptr, inv_delta, V + lane, mnext, offl);
             } else {
+                if constexpr (PADR == 0 && !GLAB) {
+                    // hubs (sparse power-law graphs, C3): a queued node of more than hub_deg arcs is
+                    // relaxed by the whole wave first, 128 arcs per step, instead of by one lane group
+                    // that the other groups of the wave -- and the sweep's other waves at its
+                    // barrier -- would wait for
+                    if (hub_deg) {
+                        for (uint32_t t0 = 0; t0 < qn; t0 += 64) {
+                            const uint32_t qi = t0 + lane;
+                            const uint32_t u = qi < qn ? q[qi] : 0xFFFFFFFFu;
+                            uint32_t deg = 0;
+                            if (u != 0xFFFFFFFFu) {
+                                const uint2 r = CACHE ? rng[u] : offl ? make_uint2(offl[u], offl[u + 1])
+                                                                      : make_uint2(abeg[u], aend[u]);
+                                deg = r.y - r.x;
+                            }
+                            uint64_t big = __ballot(deg > hub_deg);
+                            while (big) {   // wave-uniform
+                                const uint32_t b = (uint32_t)__ffsll((unsigned long long)big) - 1u;
+                                big &= big - 1ull;
+                                relax_node<64, 2, CACHE, GLAB>((uint32_t)__shfl((int)u, (int)b), lane, lab, bits,
+                                                               V + lane, rng, offl, abeg, aend, arcs, ovf, dirty,
+                                                               bkt, inv_delta, mnext);
+                            }
+                            if (deg > hub_deg) q[qi] = 0xFFFFFFFFu;   // done: the group pass skips it
+                        }
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    }
+                }
                 for (uint32_t t = 0; t < qn; t += NG) {
                     const uint32_t qi = t + grp;
                     if (qi >= qn) continue;
-                    if constexpr (PADR != 0)   // padded lists: a whole 64-slot list per group step
+                    if constexpr (PADR != 0) {   // padded lists: a whole 64-slot list per group step
                         relax_node_pad<G, PADR, CACHE>(q[qi], gl, lab, bits, rng, abeg, aend, arcs, lat_guard,
                                                        ovf, dirty, mnext);
-                    else
-                        relax_node<G, R, CACHE, GLAB>(q[qi], gl, lab, bits, V + lane, rng, offl, abeg, aend, arcs,
-                                                      ovf, dirty, bkt, inv_delta, mnext);
+                    } else {
+                        const uint32_t u = q[qi];
+                        if (u != 0xFFFFFFFFu)
+                            relax_node<G, R, CACHE, GLAB>(u, gl, lab, bits, V + lane, rng, offl, abeg, aend, arcs,
+                                                          ovf, dirty, bkt, inv_delta, mnext);
+                    }
                 }
             }
             qn = 0;
@@ -851,7 +889,7 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
     unsigned long long* __restrict__ unreach, uint32_t delta,
     unsigned long long* __restrict__ stats, const uint32_t* __restrict__ seed_lat,
     uint32_t seed_stride, uint32_t* __restrict__ nh_out, uint32_t lat_guard, uint32_t use_offl,
-    uint32_t flat_off) {
+    uint32_t flat_off, uint32_t hub_deg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr uint32_t NW = BLOCK / 64;
     uint32_t* flat = FLATL ? reinterpret_cast<uint32_t*>(smem + flat_off) : nullptr;   // expand_flat scratch
@@ -872,7 +910,8 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
                                               row_begin + blockIdx.x, (size_t)blockIdx.x * n_used,
                                               diag_lat, diag_loss, out_lat, out_loss, flags, unreach,
                                               delta, stats, seed_lat, seed_stride, nullptr, flat, nh_out,
-                                              pred, lat_guard, nullptr, nullptr, offl);
+                                              pred, lat_guard, nullptr, nullptr, offl, nullptr, 0u, nullptr,
+                                              hub_deg);
 }
 
 // Kernel 1b: labels in global memory, for graphs whose labels do not fit the LDS (C4: 50k
@@ -1529,8 +1568,7 @@ static shd_status upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
 
 // one pinned read-back of the build flags (overflow word, first unreachable pair) and one sync
 static shd_status read_flags(shd_ctx* ctx) {
-    SHD_HIP(hipMemcpyAsync(ctx->h_pin, ctx->g_flags.p, 24, hipMemcpyDeviceToHost, ctx->stream));
-    return wait_stream(ctx, ctx->stream);
+    return readback(ctx, ctx->stream, 0, ctx->g_flags.p, 24);
 }
 static bool flag_ovf(const shd_ctx* ctx) { return (uint32_t)ctx->h_pin[0] != 0; }
 
@@ -1752,7 +1790,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
                                   (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
                                   (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(),
                                   (const float*)ctx->g_diag_loss.as<float>(), d_lat, d_loss, flags, unreach, delta,
-                                  stats, seed, seed_stride, ctx->nh_out, lat_guard, use_offl, 0u);
+                                  stats, seed, seed_stride, ctx->nh_out, lat_guard, use_offl, 0u, 0u);
             return;
         }
     }
@@ -1767,7 +1805,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
                           (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
                           (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(), (const float*)ctx->g_diag_loss.as<float>(),
                           d_lat, d_loss, flags, unreach, delta, stats, seed, seed_stride, ctx->nh_out, 0u,
-                          use_offl, (uint32_t)flat_off);
+                          use_offl, (uint32_t)flat_off, flatl ? 0u : ctx->knobs.get(K_SSSP_HUB, kHubDeg));
 }
 
 static size_t sssp_lds_bytes(uint32_t V, uint32_t block, bool cache) {
@@ -2129,8 +2167,12 @@ static shd_status prepare_reordered(shd_ctx* ctx, const HostGraph& H, const uint
 
 // the dominant kernel's device time, when this build was timed (shd_routing_set_timing)
 static float main_ms(shd_ctx* ctx) {
+    // the read-back kernel (readback) can return before the runtime has seen the stop event
+    // complete: wait for it, on timed builds only
     float ms = -1.0f;
-    if (ctx->time_now && hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]) != hipSuccess) ms = -1.0f;
+    if (ctx->time_now && (hipEventSynchronize(ctx->ev[3]) != hipSuccess ||
+                          hipEventElapsedTime(&ms, ctx->ev[2], ctx->ev[3]) != hipSuccess))
+        ms = -1.0f;
     return ms;
 }
 

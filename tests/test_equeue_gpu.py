@@ -23,10 +23,13 @@ def _check(p, oq, H, window_end):
     assert p.next_time == (min(heads) if heads else 2**64 - 1)
 
 
+@pytest.mark.parametrize("wave_merge", [0, 1])
 @pytest.mark.parametrize("chance_mode,H,P", [(False, 3000, 120_000), (True, 3000, 120_000), (False, 40, 40_000)])
-def test_queues_across_rounds_vs_oracle(engine, chance_mode, H, P):
-    """H=40: ~1000 events per host and round, past the merge's LDS stage (640 pending / 192
-    batch events per host), so the global-search path of eq_merge is the one checked."""
+def test_queues_across_rounds_vs_oracle(engine, chance_mode, H, P, wave_merge, knob):
+    """H=3000: ~40 popped events per host and round, some hosts past the 16-lane merge's LDS
+    stage (64); H=40: ~1000, past both stages (64 / 160), so the global-search path is the one
+    checked.  wave_merge: eqr_merge (a wave a host, default) or eqr_merge16 (four hosts a wave)."""
+    knob("EQ_WAVE_MERGE", wave_merge)
     from shadow_amd import synth
     from shadow_amd.equeue import EventQueues
     from shadow_amd.relay import Relay
@@ -135,14 +138,16 @@ def _cmp_popped(p, op):
     assert np.array_equal(p.tag, op["tag"])
 
 
+@pytest.mark.parametrize("wave_merge", [0, 1])
 @pytest.mark.parametrize("adopt", [True, False])
-def test_adopted_batches_vs_c_queues(engine, adopt):
+def test_adopted_batches_vs_c_queues(engine, adopt, wave_merge, knob):
     """The relay writes each round straight into the slot shd_equeue_batch_buffers hands out and
     the advance adopts it as a stored run (no copy) -- or, adopt=False, into the caller's own
     device arrays (copied).  5 ms windows over 1-300 ms paths for 14 rounds: the run limit forces
     partial compactions (the runs holding the fewest pending events) from round 8 on.  Every
     popped event, the pending count and the next time against the C EventQueues; then pending()
-    against the heaps' contents."""
+    against the heaps' contents.  wave_merge: as in test_queues_across_rounds_vs_oracle."""
+    knob("EQ_WAVE_MERGE", wave_merge)
     import torch
     from shadow_amd import synth
     from shadow_amd.equeue import EventQueues

@@ -18,7 +18,9 @@ from shadow_amd.routing import Engine  # noqa: E402
 
 builds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
 eng = Engine(0)
-n = prepare(eng, synth.complete_graph(1000, 1))
+# PROBE_GRAPH=c3: the 10k-node BA graph (AUTO = delta buckets, the 1024-thread LDS kernel)
+c3 = os.environ.get("PROBE_GRAPH") == "c3"
+n = prepare(eng, synth.barabasi_albert(10_000, 3, 2) if c3 else synth.complete_graph(1000, 1))
 lat = torch.empty((n, n), dtype=torch.int64, device="cuda")
 loss = torch.empty((n, n), dtype=torch.float32, device="cuda")
 lib = C.CDLL(_native.LIB_PATH)
