@@ -638,11 +638,12 @@ EQ_BYTES_POPPED = 52   # a popped event read from its run (deliver 8, src 4, seq
                        # to the output (deliver, src, seq, tag 8)
 
 
-def equeue_leg(eng, rl, lat_table, loss_table, rounds=16, timed=8, cpu=False):
+def equeue_leg(eng, rl, lat_table, loss_table, rounds=40, timed=24, cpu=False):
     """The north star's whole relay path, round after round on C5 (1 ms windows, 1-300 ms paths:
     events stay pending for many rounds): the relay round, then shd_equeue_advance -- the merge of
     its events into the device-resident destination queues and the pop of the next window.  The
-    timed rounds include a compaction (the run limit is reached at round 8).
+    24 timed rounds (16-39: the pending set at its steady ~41M events) span several compaction
+    cycles of the stored runs, so the mean carries their share whatever the run limit.
     Roofline bytes = the relay's SURVEY 8(d) bytes + the merge's (24 B per batch event read, 28 B
     per kept event written, 56 B per popped event read + written).  CPU baseline: the C
     restatement doing the same rounds -- send_packet with push_packet_to_host into persistent

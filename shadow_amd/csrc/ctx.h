@@ -54,7 +54,15 @@ struct CodelState {   // CoDel router queues (codel.hip)
     bool ready = false;
 };
 
-constexpr int kEqMaxRuns = 8;   // stored runs of the event queues before they are compacted
+// Stored runs of the event queues before they are compacted (the limit, SHD_EQ_MAX_RUNS knob,
+// may be set lower, down to 2).  Each advance merges one source per run, each compaction half
+// the runs: on C5 (24 rounds at the steady ~41M pending events) the advance averaged 0.370 ms
+// at 8 runs, 0.359 at 12 and 0.355 at 15 (a compaction every ~3 / ~6 / ~7 rounds against more
+// sources in every pass); 12 keeps the count kernel's lanes to 13 of its 16.
+#ifndef SHD_EQ_MAX_RUNS
+#define SHD_EQ_MAX_RUNS 12   // (tuning builds: tools/build_variant.sh -DSHD_EQ_MAX_RUNS=n, n <= 15)
+#endif
+constexpr int kEqMaxRuns = SHD_EQ_MAX_RUNS;
 constexpr int kEqSlots = kEqMaxRuns + 2;   // + the compaction target + a batch slot handed out for adoption
 
 struct EqRunBuf {   // one stored run of the event queues: a CSR of per-host sorted events
@@ -173,8 +181,10 @@ struct PreparedGraph {
 
 struct shd_ctx;
 namespace shd {
-constexpr int kPinWords = 72;       // h_pin words; [64] is wait_stream's marker
-constexpr int kPinMarker = 64;
+// h_pin words: [0, 3) routing flags, [8, 16) relay reductions, [32, 34) flush checks,
+// [48, 48 + 4 + runs + 1) event-queue counts; [80] is the polled marker
+constexpr int kPinWords = 88;
+constexpr int kPinMarker = 80;
 // Wait until everything enqueued on stream s has finished (see api.cpp)
 shd_status wait_stream(shd_ctx* ctx, hipStream_t s);
 // n_bytes of device words into h_pin[at ...] and wait for the stream (api.cpp)

@@ -13,11 +13,13 @@
 // of per-host sorted events with a per-host cursor (its first unpopped event).  An advance
 // (shd_equeue_advance) never rewrites the pending events: per host it finds every run's prefix
 // below window_end (a binary search from the cursor), merges those prefixes and the batch's into
-// the popped output -- an event's rank is its index in its own run plus the number of smaller
-// events in each other run, binary searches over the deliver times staged in LDS, no atomics,
-// deterministic (keys are unique: (src, seq) never repeats) -- moves the cursors, and stores the
+// the popped output -- the host's popped events staged in LDS and ranked by a wave sort of their
+// deliver times (equal times: by searches, an event's rank being its index in its own run plus
+// the number of smaller (time, src, seq) keys in each other run); no atomics, deterministic
+// (keys are unique: (src, seq) never repeats) -- moves the cursors, and stores the
 // batch's remainder as a new run.  A run whose events are all popped is dropped; when
-// kEqMaxRuns runs are alive, they are first compacted into one (the same merge, every event).
+// the run limit is reached (kEqMaxRuns, or the EQ_MAX_RUNS knob), half of them -- those holding
+// the fewest pending events -- are first compacted into one (the same merge, every event).
 // Traffic per advance ~ the batch (read + its remainder written) + the popped events (read +
 // written), instead of every pending event read and written each round.
 #include <cstdlib>
@@ -25,6 +27,7 @@
 #include <cstring>
 
 #include "scan.h"
+#include "wave.h"
 
 namespace shd {
 
@@ -157,15 +160,112 @@ struct EqOut {
 #ifndef SHD_EQ_SEL
 #define SHD_EQ_SEL 1   // staging: lane per staged event (0: source after source, for A/B)
 #endif
+// (an LDS table of the sources' arrays read by a per-lane source index, instead of the selects
+// over every source's pointers, measured slower: C5 advance 0.395 against 0.377 ms)
 constexpr uint32_t kEqStage = 160;   // 17.5 KB per 4-wave workgroup: 8 workgroups (32 waves) per CU
 
+// u64 minimum / maximum over the wave
+__device__ __forceinline__ uint64_t eq_wave_min64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t x = __shfl_xor(v, o);
+        v = x < v ? x : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t eq_wave_max64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t x = __shfl_xor(v, o);
+        v = x > v ? x : v;
+    }
+    return v;
+}
+
+// Rank a host's staged popped events by a wave sort instead of searches: (t - tmin) << 8 | staged
+// index is a unique key, 32 bits when the deliver times span less than 2^24 ns (a window of up
+// to ~16 ms: every normal pass), 64 bits otherwise (a compaction's whole runs), and a bitonic
+// network over the wave (wave.h: one DPP / swizzle / permlane exchange per stage, 28 stages for
+// 128 events) orders them -- a bisection per other source per event costs several times the
+// VALU issue, which is what bounds the merge (~100 events per host on C5) -- and the events
+// leave in rank order (coalesced stores).  Equal times, whose order needs (src, seq), return
+// false: the caller's searches take the host.
+template <int NPL>
+__device__ __forceinline__ bool eq_sort_emit(uint32_t npop, uint32_t lane, const uint64_t* st, const uint32_t* ss,
+                                             const uint64_t* sq, const uint64_t* sg, uint32_t po, EqOut popped) {
+    static_assert(64 * NPL <= 256, "staged index in 8 key bits");
+    uint64_t t[NPL], tmn = ~0ull, tmx = 0;
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t i = lane + 64u * c;
+        t[c] = i < npop ? st[i] : 0ull;
+        if (i < npop) {
+            tmn = t[c] < tmn ? t[c] : tmn;
+            tmx = t[c] > tmx ? t[c] : tmx;
+        }
+    }
+    tmn = eq_wave_min64(tmn);
+    tmx = eq_wave_max64(tmx);
+    uint32_t idx[NPL];
+    bool tie = false;   // equal times in sorted neighbours r, r + 1
+    if (tmx - tmn < (1ull << 24)) {   // wave-uniform
+        uint32_t k[NPL];
+#pragma unroll
+        for (int c = 0; c < NPL; ++c) {
+            const uint32_t i = lane + 64u * c;   // npop < 256 here: no valid key reaches ~0u
+            k[c] = i < npop ? ((uint32_t)(t[c] - tmn) << 8) | i : ~0u;
+        }
+        wave_bitonic32<NPL>(k, lane);
+#pragma unroll
+        for (int c = 0; c < NPL; ++c) {
+            // (both shuffles with every lane active: a read of an inactive lane returns 0)
+            const uint32_t down = (uint32_t)__shfl_down((int)k[c], 1);
+            const uint32_t first = c + 1 < NPL ? (uint32_t)__shfl((int)k[c + 1 < NPL ? c + 1 : c], 0) : ~0u;
+            const uint32_t nx = lane == 63 ? first : down;
+            if (lane + 64u * c + 1 < npop && (nx >> 8) == (k[c] >> 8)) tie = true;
+            idx[c] = k[c] & 0xFFu;
+        }
+    } else if (tmx - tmn < (1ull << 56)) {
+        uint64_t k[NPL];
+#pragma unroll
+        for (int c = 0; c < NPL; ++c) {
+            const uint32_t i = lane + 64u * c;
+            k[c] = i < npop ? ((t[c] - tmn) << 8) | i : ~0ull;
+        }
+        wave_bitonic<NPL>(k, lane);
+#pragma unroll
+        for (int c = 0; c < NPL; ++c) {
+            const uint64_t down = __shfl_down(k[c], 1);
+            const uint64_t first = c + 1 < NPL ? __shfl(k[c + 1 < NPL ? c + 1 : c], 0) : ~0ull;
+            const uint64_t nx = lane == 63 ? first : down;
+            if (lane + 64u * c + 1 < npop && (nx >> 8) == (k[c] >> 8)) tie = true;
+            idx[c] = (uint32_t)k[c] & 0xFFu;
+        }
+    } else {
+        return false;
+    }
+    if (__ballot(tie) != 0) return false;
+#pragma unroll
+    for (int c = 0; c < NPL; ++c) {
+        const uint32_t r = lane + 64u * c;
+        if (r < npop) {
+            const uint32_t i = idx[c];
+            popped.deliver[po + r] = st[i];
+            popped.src[po + r] = ss[i];
+            popped.seq[po + r] = sq[i];
+            popped.tag[po + r] = sg[i];
+        }
+    }
+    return true;
+}
+
 // One host's merge (a wave): lane k < S.n holds source k's popped range [my_lo, my_m); po is the
-// host's first popped slot, rb_no its first slot in the new run (a batch source only).
+// host's first popped slot, rb_no its first slot in the new run (a batch source only); sort_rank:
+// rank staged hosts by eq_sort_emit first (SHD_EQ_SEARCH_ONLY=1: the searches alone).
+template <uint32_t STAGE>
 __device__ __forceinline__ void eq_merge_host(uint32_t h, uint32_t w, uint32_t lane, const EqSrcs& S, uint32_t my_lo,
                                               uint32_t my_m, uint32_t po, EqOut popped, EqOut nrun, uint32_t rb_no,
-                                              uint32_t* __restrict__ nrun_cur, uint64_t (*s_t)[kEqStage],
-                                              uint64_t (*s_q)[kEqStage], uint64_t (*s_g)[kEqStage],
-                                              uint32_t (*s_s)[kEqStage]) {
+                                              uint32_t* __restrict__ nrun_cur, uint64_t (*s_t)[STAGE],
+                                              uint64_t (*s_q)[STAGE], uint64_t (*s_g)[STAGE],
+                                              uint32_t (*s_s)[STAGE], bool sort_rank) {
     const uint32_t cnt = my_m - my_lo;
     uint32_t incl = cnt;
     for (uint32_t o = 1; o < 64; o <<= 1) {
@@ -204,7 +304,7 @@ __device__ __forceinline__ void eq_merge_host(uint32_t h, uint32_t w, uint32_t l
             }
         }
     }
-    if (npop <= kEqStage) {
+    if (npop <= STAGE) {
         uint64_t* st = s_t[w];
         uint64_t* sq = s_q[w];
         uint64_t* sg = s_g[w];
@@ -253,7 +353,12 @@ __device__ __forceinline__ void eq_merge_host(uint32_t h, uint32_t w, uint32_t l
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t i0 = lane; i0 < npop; i0 += 64) {
+        static_assert(STAGE <= 256, "staged index in 8 key bits");
+        const bool sorted = sort_rank && npop > 1 &&
+                            (npop <= 64    ? eq_sort_emit<1>(npop, lane, st, ss, sq, sg, po, popped)
+                             : npop <= 128 ? eq_sort_emit<2>(npop, lane, st, ss, sq, sg, po, popped)
+                                           : eq_sort_emit<4>(npop, lane, st, ss, sq, sg, po, popped));
+        for (uint32_t i0 = sorted ? npop : lane; i0 < npop; i0 += 64) {
             uint32_t k = 0;   // staged event i0 belongs to source k: u_sb[k] <= i0 < u_sb[k + 1]
             for (uint32_t j = 1; j < S.n; ++j) k = u_sb[j] <= i0 ? j : k;
             const uint64_t t = st[i0], qq = sq[i0];
@@ -330,11 +435,16 @@ __device__ __forceinline__ void eq_merge_host(uint32_t h, uint32_t w, uint32_t l
 }
 
 
+// STAGE: staged events per host -- kEqStage on the normal passes (8 workgroups per CU), 256 on a
+// compaction's (whole runs: ~100-250 pending per host on C5, sorted rather than searched in
+// global memory)
+template <uint32_t STAGE>
 __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, const uint32_t* __restrict__ pop_off,
                                                  EqOut popped, EqOut nrun, const uint32_t* __restrict__ nrun_off,
-                                                 uint32_t* __restrict__ nrun_cur, const uint2* __restrict__ ranges) {
-    __shared__ uint64_t s_t[4][kEqStage], s_q[4][kEqStage], s_g[4][kEqStage];
-    __shared__ uint32_t s_s[4][kEqStage];
+                                                 uint32_t* __restrict__ nrun_cur, const uint2* __restrict__ ranges,
+                                                 uint32_t sort_rank) {
+    __shared__ uint64_t s_t[4][STAGE], s_q[4][STAGE], s_g[4][STAGE];
+    __shared__ uint32_t s_s[4][STAGE];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t h = blockIdx.x * 4 + w;
     if (h >= n_hosts) return;   // wave-uniform; the kernel has no workgroup barrier
@@ -345,8 +455,8 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
         my_lo = r.x;
         my_m = r.y;
     }
-    eq_merge_host(h, w, lane, S, my_lo, my_m, pop_off[h], popped, nrun, S.b >= 0 ? nrun_off[h] : 0u, nrun_cur,
-                  s_t, s_q, s_g, s_s);
+    eq_merge_host<STAGE>(h, w, lane, S, my_lo, my_m, pop_off[h], popped, nrun, S.b >= 0 ? nrun_off[h] : 0u,
+                         nrun_cur, s_t, s_q, s_g, s_s, sort_rank != 0);
 }
 
 // Sixteen lanes per host (EQ_WAVE_MERGE=0; tuning variant, NOT the default): for queues popping
@@ -613,6 +723,7 @@ static EqOut eq_run_out(EqRunBuf& r) {
 }
 
 constexpr int kEqPinWord = 48;   // ctx->h_pin words [48, 48 + kEqWords)
+static_assert(kEqPinWord + (int)kEqWords <= kPinMarker, "queue counts below the polled marker");
 
 // One pass: per-host cuts at window_end, scans, the merge of every source's popped prefix into
 // `out` at offsets out_off, and (nrun) the batch's remainder into a new run whose cursor goes to
@@ -637,8 +748,9 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
                        nrun ? nrun->off.as<uint32_t>() : nullptr, H + 1, s));
     if (n_in) {
         if (ctx->knobs.get(K_EQ_WAVE_MERGE, 1) != 0)   // default: a wave a host (faster on C5, see eqr_merge16)
-            eqr_merge<<<div_up(H, 4), 256, 0, s>>>(H, S, out_off, out, nr, nrun ? nrun->off.as<uint32_t>() : nullptr,
-                                                   nrun_cur, Q.ranges.as<uint2>());
+            (window_end == ~0ull ? eqr_merge<256> : eqr_merge<kEqStage>)<<<div_up(H, 4), 256, 0, s>>>(
+                H, S, out_off, out, nr, nrun ? nrun->off.as<uint32_t>() : nullptr, nrun_cur, Q.ranges.as<uint2>(),
+                ctx->knobs.get(K_EQ_SEARCH_ONLY, 0) == 1 ? 0u : 1u);
         else
             eqr_merge16<<<div_up(H, 16), 256, 0, s>>>(H, S, out_off, out, nr,
                                                       nrun ? nrun->off.as<uint32_t>() : nullptr, nrun_cur,
@@ -821,7 +933,9 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     }
     int live = 0;
     for (int r = 0; r < kEqSlots; ++r) live += Q.run[r].live ? 1 : 0;
-    if (has_b && n_b && live >= kEqMaxRuns) SHD_TRY(eq_compact(ctx, false));   // room for the batch's run
+    const int max_runs = (int)std::min<int64_t>(std::max<int64_t>(ctx->knobs.get(K_EQ_MAX_RUNS, kEqMaxRuns), 2),
+                                                kEqMaxRuns);
+    if (has_b && n_b && live >= max_runs) SHD_TRY(eq_compact(ctx, false));   // room for the batch's run
     if (adopt) {
         const int t = Q.lend;
         EqRunBuf& R = Q.run[t];

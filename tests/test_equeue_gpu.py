@@ -23,13 +23,18 @@ def _check(p, oq, H, window_end):
     assert p.next_time == (min(heads) if heads else 2**64 - 1)
 
 
-@pytest.mark.parametrize("wave_merge", [0, 1])
+MERGE_KNOBS = {"sort": {}, "search": {"EQ_SEARCH_ONLY": 1}, "merge16": {"EQ_WAVE_MERGE": 0}}
+
+
+@pytest.mark.parametrize("merge", list(MERGE_KNOBS))
 @pytest.mark.parametrize("chance_mode,H,P", [(False, 3000, 120_000), (True, 3000, 120_000), (False, 40, 40_000)])
-def test_queues_across_rounds_vs_oracle(engine, chance_mode, H, P, wave_merge, knob):
+def test_queues_across_rounds_vs_oracle(engine, chance_mode, H, P, merge, knob):
     """H=3000: ~40 popped events per host and round, some hosts past the 16-lane merge's LDS
     stage (64); H=40: ~1000, past both stages (64 / 160), so the global-search path is the one
-    checked.  wave_merge: eqr_merge (a wave a host, default) or eqr_merge16 (four hosts a wave)."""
-    knob("EQ_WAVE_MERGE", wave_merge)
+    checked.  merge: eqr_merge ranking staged hosts by a wave sort (default) or by searches
+    alone, or eqr_merge16 (four hosts a wave)."""
+    for k, v in MERGE_KNOBS[merge].items():
+        knob(k, v)
     from shadow_amd import synth
     from shadow_amd.equeue import EventQueues
     from shadow_amd.relay import Relay
@@ -89,10 +94,11 @@ def test_empty_queues_and_empty_batch(engine):
     assert p.n_pending == 1 and p.next_time == 40
 
 
-def test_run_compaction_and_pending_vs_oracle(engine):
+def test_run_compaction_and_pending_vs_oracle(engine, knob):
     """5 ms windows against 1-300 ms path latencies: no stored run drains for many rounds, so the
-    8-run limit compacts the runs (from round 9 on), and pending() -- a compaction itself --
+    8-run limit (EQ_MAX_RUNS knob) compacts the runs (from round 9 on), and pending() -- a compaction itself --
     returns every host's queue in EventQueue order, as the oracle's heaps hold it."""
+    knob("EQ_MAX_RUNS", 8)
     from shadow_amd import synth
     from shadow_amd.equeue import EventQueues
     from shadow_amd.relay import Relay
@@ -138,16 +144,19 @@ def _cmp_popped(p, op):
     assert np.array_equal(p.tag, op["tag"])
 
 
-@pytest.mark.parametrize("wave_merge", [0, 1])
+@pytest.mark.parametrize("merge,max_runs", [(m, 8) for m in MERGE_KNOBS] + [("sort", 3), ("sort", 12)])
 @pytest.mark.parametrize("adopt", [True, False])
-def test_adopted_batches_vs_c_queues(engine, adopt, wave_merge, knob):
+def test_adopted_batches_vs_c_queues(engine, adopt, merge, max_runs, knob):
     """The relay writes each round straight into the slot shd_equeue_batch_buffers hands out and
     the advance adopts it as a stored run (no copy) -- or, adopt=False, into the caller's own
-    device arrays (copied).  5 ms windows over 1-300 ms paths for 14 rounds: the run limit forces
-    partial compactions (the runs holding the fewest pending events) from round 8 on.  Every
+    device arrays (copied).  5 ms windows over 1-300 ms paths for 14 rounds: the run limit
+    (EQ_MAX_RUNS knob: 8, or 3 -- a compaction nearly every round -- or the default 12) forces
+    partial compactions (the runs holding the fewest pending events) from then on.  Every
     popped event, the pending count and the next time against the C EventQueues; then pending()
-    against the heaps' contents.  wave_merge: as in test_queues_across_rounds_vs_oracle."""
-    knob("EQ_WAVE_MERGE", wave_merge)
+    against the heaps' contents.  merge: as in test_queues_across_rounds_vs_oracle."""
+    for k, v in MERGE_KNOBS[merge].items():
+        knob(k, v)
+    knob("EQ_MAX_RUNS", max_runs)
     import torch
     from shadow_amd import synth
     from shadow_amd.equeue import EventQueues
@@ -237,12 +246,14 @@ def test_c5_scale_rounds_vs_c_queues(engine):
     assert p.n_pending == 0
 
 
-def test_c5_scale_adopted_rounds_with_compaction_vs_c_queues(engine):
+def test_c5_scale_adopted_rounds_with_compaction_vs_c_queues(engine, knob):
     """The bench's path at full C5 size for 12 rounds: each round's relay output is written into the
     slot shd_equeue_batch_buffers lends and adopted as a stored run; 1 ms windows over 1-300 ms
-    paths keep every run alive, so from round 9 on the 8-run limit forces the partial compactions
-    (the runs holding the fewest pending events merged into one) at ~40-100M pending events.  Every
-    popped event, the pending count and the next time against the C EventQueues, then a drain."""
+    paths keep every run alive, so from round 9 on an 8-run limit (EQ_MAX_RUNS knob; the default
+    12 would compact once) forces the partial compactions (the runs holding the fewest pending
+    events merged into one) at ~40-100M pending events.  Every popped event, the pending count and
+    the next time against the C EventQueues, then a drain."""
+    knob("EQ_MAX_RUNS", 8)
     from shadow_amd import synth
     from shadow_amd.equeue import EventQueues
     from shadow_amd.relay import Relay
