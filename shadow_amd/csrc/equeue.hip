@@ -109,7 +109,13 @@ __global__ __launch_bounds__(256) void eqr_count(uint32_t n_hosts, EqSrcs S, uin
         if (h < n_hosts && k < S.n) {
             const EqSrc& q = S.s[k];
             const uint32_t lo = q.lo ? q.lo[h] : q.off[h], hi = q.off[h + 1];
-            const uint32_t m = lower_bound_gallop(q.deliver, lo, hi, window_end);
+            // a compaction (window_end = ~0) takes every event: one load confirms the run's last
+            // event is below it, instead of a gallop across the whole run
+            // (loading the first 8 or 16 times of the run at once and counting, instead of the
+            // gallop's dependent loads, measured slower: C5 advance 0.37 / 0.45 ms against 0.35)
+            const uint32_t m = window_end == ~0ull && lo < hi && q.deliver[hi - 1] < window_end
+                                   ? hi
+                                   : lower_bound_gallop(q.deliver, lo, hi, window_end);
             q.cut[h] = m;
             ranges[(size_t)h * kEqSrcMax + k] = make_uint2(lo, m);   // eqr_merge: one line per host
             np = m - lo;
