@@ -146,23 +146,31 @@ def sharded_build(eng, world, rank, n, algo, steps, warmup, keep=False, gather=T
     loss = torch.empty((max(rows, 1), n), dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
 
+    # the call's arguments are made once: the timed loop holds the build calls and nothing else
+    lat_p, loss_p, err = N.ptr(lat), N.ptr(loss), N.Error()
+    run = eng.lib.shd_routing_run
+
     def step():
         if world > 1 and gather:
             D.routing_run_sharded(eng, algo, lat, loss)
         elif re > rb:
-            run_rows(eng, algo, rb, re, lat, loss)
+            st = run(eng.ctx, algo, rb, re, lat_p, loss_p, C.byref(err))
+            if st != 0:
+                N.check(st, "shd_routing_run", err)
 
     for _ in range(warmup):
         step()
     barrier_sync(world)
     infos = []
     # the dominant kernel is timed (HIP events on its dispatch) on every 4th step of the timed
-    # region: each timed build pays a few microseconds of queue gap for its events
+    # region (each timed build pays a few microseconds of queue gap for its events); the build
+    # info is read after those steps only
     eng.lib.shd_routing_set_timing(eng.ctx, TIME_EVERY)
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
         step()
-        infos.append(eng.last_info())
+        if i % TIME_EVERY == 0 or i == steps - 1:
+            infos.append(eng.last_info())
     barrier_sync(world)
     dt = max_over_ranks(time.perf_counter() - t0, world)
     eng.lib.shd_routing_set_timing(eng.ctx, 1)
