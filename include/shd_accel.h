@@ -347,6 +347,9 @@ void shd_host_free(void* p);
  *                        torch.distributed ...); collective over the ranks
  *   shd_comm_init_local  every rank in this process (one host thread per rank must then drive
  *                        each sharded call concurrently): device copies between the contexts
+ *   shd_comm_init_host   ranks are processes the caller connects itself (MPI, gloo, sockets):
+ *                        one all-to-all-v callback moves host bytes; the device bytes are staged
+ *                        through pinned host memory around it (slower than RCCL: PCIe both ways)
  * Shards are contiguous blocks of ceil(total / n_ranks) (shd_shard_range).  Initialising or
  * destroying a communicator requires shd_relay_setup again.
  */
@@ -354,6 +357,17 @@ void shd_host_free(void* p);
 shd_status shd_comm_unique_id(uint8_t* id /* SHD_COMM_ID_BYTES */);
 shd_status shd_comm_init(shd_ctx* ctx, int32_t n_ranks, int32_t rank, const uint8_t* id);
 shd_status shd_comm_init_local(shd_ctx** ctxs, int32_t n_ranks);
+/* The host transport of shd_comm_init_host.  all_to_allv: every rank calls it together; the
+ * send_bytes[r] bytes at send + send_off[r] go to rank r (offsets may repeat: the same bytes to
+ * several ranks), the recv_bytes[q] bytes from rank q land at recv + recv_off[q]; host memory,
+ * the sizes already agree between the ranks.  Returns 0 on success (anything else fails the
+ * call with SHD_ERR_HIP on this rank; the peers are the transport's to release). */
+typedef struct shd_host_comm_ops {
+    void* user;
+    int (*all_to_allv)(void* user, const void* send, const uint64_t* send_bytes, const uint64_t* send_off,
+                       void* recv, const uint64_t* recv_bytes, const uint64_t* recv_off);
+} shd_host_comm_ops;
+shd_status shd_comm_init_host(shd_ctx* ctx, int32_t n_ranks, int32_t rank, const shd_host_comm_ops* ops);
 shd_status shd_comm_info(const shd_ctx* ctx, int32_t* n_ranks, int32_t* rank);
 shd_status shd_comm_destroy(shd_ctx* ctx);
 shd_status shd_shard_range(uint32_t total, int32_t n_ranks, int32_t rank, uint32_t* lo, uint32_t* hi);

@@ -38,8 +38,17 @@ EXPORTED = [
     "shd_runahead_setup", "shd_runahead_get", "shd_round_window", "shd_window_compute", "shd_copy_to_host",
     "shd_routing_lookup_batch", "shd_routing_mirror", "shd_equeue_batch_buffers",
     "shd_set_knob", "shd_get_knob", "shd_relay_flush", "shd_host_alloc", "shd_host_free",
+    "shd_comm_init_host",
 ]
 COMM_ID_BYTES = 128
+
+# shd_host_comm_ops (include/shd_accel.h): the all-to-all-v callback of shd_comm_init_host
+_U64P = C.POINTER(C.c_uint64)
+ALL_TO_ALLV = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, _U64P, _U64P, C.c_void_p, _U64P, _U64P)
+
+
+class HostCommOps(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("all_to_allv", ALL_TO_ALLV)]
 
 
 class ShdError(RuntimeError):
@@ -203,6 +212,7 @@ def load(path: str = LIB_PATH) -> C.CDLL:
         "shd_host_alloc": (P, [C.c_size_t]),
         "shd_host_free": (None, [P]),
         "shd_get_knob": (I32, [P, C.c_char_p, P]),
+        "shd_comm_init_host": (I32, [P, I32, I32, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -170,6 +170,145 @@ struct LocalComm final : Comm {
     }
 };
 
+// ------------------------------------------------------------------------------------ host
+// The caller's host transport (shd_comm_init_host): ranks are processes the caller already
+// connects (MPI, torch.distributed gloo, Shadow's own sockets), one all-to-all-v callback moves
+// host bytes between them.  Each collective stages the device bytes through pinned host memory
+// (the stream is synchronised before the callback), and every rank's block leads with its entry
+// status, so all ranks return the lowest failing rank's status, as under LocalComm.  The same
+// sharded code paths run as under RCCL; only the transport differs (and is slower: PCIe both
+// ways), which is what a multi-process run on hosts without RCCL peers needs.
+struct HostComm final : Comm {
+    shd_host_comm_ops ops{};
+    unsigned char* hs = nullptr;   // pinned staging: the blocks sent
+    unsigned char* hr = nullptr;   // and received
+    size_t hs_cap = 0, hr_cap = 0;
+    ~HostComm() override {
+        if (hs) (void)hipHostFree(hs);
+        if (hr) (void)hipHostFree(hr);
+    }
+    static shd_status grow(unsigned char*& p, size_t& cap, size_t n) {
+        if (n <= cap) return SHD_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&p), n) != hipSuccess) return SHD_ERR_NOMEM;
+        cap = n;
+        return SHD_OK;
+    }
+    // One collective: the block to rank r is 8 status bytes + the parts src[r][k] (device, sizes
+    // sb[r][k]), its host image at send offset so[r] (blocks may share an offset: the same bytes
+    // to every rank); the block from rank q lands at its receive offset and its parts go to
+    // dst[q][k] (sizes rb[q][k]).  The own rank's parts are copied on the device.
+    shd_status run(int n_parts, const std::vector<const void*>& src, const std::vector<size_t>& sb,
+                   const std::vector<size_t>& so, const std::vector<void*>& dst, const std::vector<size_t>& rb,
+                   hipStream_t s, shd_status st) {
+        const int n = size;
+        std::vector<uint64_t> s_bytes(n), s_off(n), r_bytes(n), r_off(n);
+        size_t s_end = 0, r_end = 0;
+        for (int r = 0; r < n; ++r) {
+            size_t t = 8;
+            if (r != rank)
+                for (int k = 0; k < n_parts; ++k) t += sb[(size_t)r * n_parts + k];
+            s_bytes[r] = t;
+            s_off[r] = so[r];
+            s_end = std::max(s_end, so[r] + t);
+            size_t u = 8;
+            if (r != rank)
+                for (int k = 0; k < n_parts; ++k) u += rb[(size_t)r * n_parts + k];
+            r_bytes[r] = u;
+            r_off[r] = r_end;
+            r_end += u;
+        }
+        if (st == SHD_OK) st = grow(hs, hs_cap, s_end);
+        if (st == SHD_OK) st = grow(hr, hr_cap, r_end);
+        // a rank that cannot stage still takes part with its status alone (sizes of 8 bytes are
+        // what its peers expect from a failed rank only if they fail too: the sizes were agreed
+        // before, so a staging failure is reported and the transport is left to the caller)
+        if (st != SHD_OK) return st;
+        for (int r = 0; r < n; ++r) {
+            size_t at = so[r] + 8;
+            for (int k = 0; k < n_parts; ++k) {
+                const size_t i = (size_t)r * n_parts + k;
+                if (r == rank) {
+                    if (sb[i] != rb[i]) st = SHD_ERR_INVALID;
+                    else if (sb[i] && dst[i] != src[i] &&
+                             hipMemcpyAsync(dst[i], src[i], sb[i], hipMemcpyDeviceToDevice, s) != hipSuccess)
+                        st = SHD_ERR_HIP;
+                    continue;
+                }
+                if (sb[i] && hipMemcpyAsync(hs + at, src[i], sb[i], hipMemcpyDeviceToHost, s) != hipSuccess)
+                    st = SHD_ERR_HIP;
+                at += sb[i];
+            }
+        }
+        if (hipStreamSynchronize(s) != hipSuccess && st == SHD_OK) st = SHD_ERR_HIP;
+        for (int r = 0; r < n; ++r) {
+            const uint64_t w = (uint64_t)st;
+            std::memcpy(hs + so[r], &w, 8);   // shared offsets get the same word
+        }
+        if (ops.all_to_allv(ops.user, hs, s_bytes.data(), s_off.data(), hr, r_bytes.data(), r_off.data()) != 0)
+            return SHD_ERR_HIP;   // the transport failed: the caller's to handle, as RCCL's would be
+        shd_status all = SHD_OK;
+        for (int q = 0; q < n && all == SHD_OK; ++q) {
+            uint64_t w = 0;
+            std::memcpy(&w, hr + r_off[q], 8);
+            all = (shd_status)w;
+        }
+        if (all != SHD_OK) return all;
+        for (int q = 0; q < n; ++q) {
+            if (q == rank) continue;
+            size_t at = r_off[q] + 8;
+            for (int k = 0; k < n_parts; ++k) {
+                const size_t i = (size_t)q * n_parts + k;
+                if (rb[i] && hipMemcpyAsync(dst[i], hr + at, rb[i], hipMemcpyHostToDevice, s) != hipSuccess)
+                    all = SHD_ERR_HIP;
+                at += rb[i];
+            }
+        }
+        if (hipStreamSynchronize(s) != hipSuccess && all == SHD_OK) all = SHD_ERR_HIP;   // staging reused next call
+        return all;
+    }
+    shd_status all_to_all_u64(const uint64_t* send, uint64_t* recv, size_t count, hipStream_t s) override {
+        std::vector<const void*> src(size);
+        std::vector<void*> dst(size);
+        std::vector<size_t> sb(size, count * 8), rb(size, count * 8), so(size);
+        size_t off = 0;
+        for (int r = 0; r < size; ++r) {
+            src[r] = send + (size_t)r * count;
+            dst[r] = recv + (size_t)r * count;
+            so[r] = off;
+            off += 8 + (r == rank ? 0 : count * 8);
+        }
+        return run(1, src, sb, so, dst, rb, s, SHD_OK);
+    }
+    shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes, void* const* recv,
+                        const size_t* recv_bytes, hipStream_t s) override {
+        if (n_parts < 1) return SHD_ERR_INVALID;
+        const size_t m = (size_t)size * n_parts;
+        std::vector<const void*> src(send, send + m);
+        std::vector<void*> dst(recv, recv + m);
+        std::vector<size_t> sb(send_bytes, send_bytes + m), rb(recv_bytes, recv_bytes + m), so(size);
+        size_t off = 0;
+        for (int r = 0; r < size; ++r) {
+            so[r] = off;
+            off += 8;
+            if (r != rank)
+                for (int k = 0; k < n_parts; ++k) off += sb[(size_t)r * n_parts + k];
+        }
+        return run(n_parts, src, sb, so, dst, rb, s, SHD_OK);
+    }
+    shd_status all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+        // one staged block (status + bytes) sent to every peer: every send offset is 0
+        std::vector<const void*> src(size, send);
+        std::vector<void*> dst(size);
+        std::vector<size_t> sb(size, bytes), rb(size, bytes), so(size, 0);
+        for (int r = 0; r < size; ++r) dst[r] = static_cast<char*>(recv) + (size_t)r * bytes;
+        // (run() stages the part for every peer at the shared offset 8: the same bytes each time)
+        return run(1, src, sb, so, dst, rb, s, SHD_OK);
+    }
+};
+
 }  // namespace shd
 
 using namespace shd;
@@ -232,6 +371,21 @@ shd_status shd_comm_init_local(shd_ctx** ctxs, int32_t n_ranks) {
         ctxs[r]->relay.ready = false;
         ctxs[r]->eq.ready = false;
     }
+    return SHD_OK;
+}
+
+shd_status shd_comm_init_host(shd_ctx* ctx, int32_t n_ranks, int32_t rank, const shd_host_comm_ops* ops) {
+    if (!ctx || !ops || !ops->all_to_allv || n_ranks < 1 || rank < 0 || rank >= n_ranks) return SHD_ERR_INVALID;
+    SHD_HIP(hipSetDevice(ctx->device));
+    auto c = std::unique_ptr<HostComm>(new (std::nothrow) HostComm());
+    if (!c) return SHD_ERR_NOMEM;
+    SHD_TRY(ctx->comm_scratch.ensure(comm_scratch_bytes(n_ranks)));
+    c->ops = *ops;
+    c->rank = rank;
+    c->size = n_ranks;
+    ctx->comm = std::move(c);
+    ctx->relay.ready = false;
+    ctx->eq.ready = false;
     return SHD_OK;
 }
 

@@ -53,6 +53,52 @@ def comm_init_local(engines):
     N.check(engines[0].lib.shd_comm_init_local(arr, len(engines)), "shd_comm_init_local")
 
 
+def host_all_to_allv(group=None):
+    """The all-to-all-v of shd_comm_init_host over a torch.distributed CPU group (gloo): a Python
+    callable with the C callback's arguments (raw host pointers and per-rank sizes / offsets)."""
+    def a2av(send, s_bytes, s_off, recv, r_bytes, r_off):
+        world = dist.get_world_size(group)
+        sb = [int(s_bytes[r]) for r in range(world)]
+        rb = [int(r_bytes[q]) for q in range(world)]
+        # the blocks to the ranks, back to back (a block's offset may repeat: the same bytes)
+        parts = [np.ctypeslib.as_array(C.cast(C.c_void_p(send + int(s_off[r])), C.POINTER(C.c_uint8)), (sb[r],))
+                 if sb[r] else np.zeros(0, np.uint8) for r in range(world)]
+        inp = torch.from_numpy(np.concatenate(parts) if parts else np.zeros(0, np.uint8))
+        out = torch.empty(sum(rb), dtype=torch.uint8)
+        dist.all_to_all_single(out, inp, rb, sb, group=group)
+        o = out.numpy()
+        at = 0
+        for q in range(world):
+            if rb[q]:
+                dst = np.ctypeslib.as_array(C.cast(C.c_void_p(recv + int(r_off[q])), C.POINTER(C.c_uint8)), (rb[q],))
+                dst[:] = o[at:at + rb[q]]
+            at += rb[q]
+    return a2av
+
+
+class HostComm:
+    """An engine communicator over the caller's host transport (shd_comm_init_host): here
+    torch.distributed on a CPU group (gloo), for processes that cannot pair up over RCCL (several
+    processes on one GPU, hosts without an RCCL peer).  Keep the object alive while the engine
+    uses the communicator (it holds the C callback)."""
+
+    def __init__(self, engine, group=None):
+        fn = host_all_to_allv(group)
+
+        def cb(user, send, s_bytes, s_off, recv, r_bytes, r_off):
+            try:
+                fn(send, s_bytes, s_off, recv, r_bytes, r_off)
+                return 0
+            except Exception:   # noqa: BLE001 -- a failed transport is reported to the engine
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._cb = N.ALL_TO_ALLV(cb)
+        self._ops = N.HostCommOps(None, self._cb)
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        N.check(engine.lib.shd_comm_init_host(engine.ctx, world, rank, C.byref(self._ops)), "shd_comm_init_host")
+
+
 def shard_range(total: int, world: int, rank: int):
     lib = N.load()
     lo, hi = C.c_uint32(0), C.c_uint32(0)
