@@ -2111,18 +2111,35 @@ __global__ __launch_bounds__(256) void merge_runs24(uint32_t n_runs, uint32_t n_
                                                     const uint32_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ out_t, uint32_t* __restrict__ out_s,
                                                     uint64_t* __restrict__ out_q, uint32_t* __restrict__ out_p) {
+    // The event's destination d: a run's events are in destination order and a block takes 256
+    // consecutive events, so threads 0 and 1 search the whole offset row for the block's first
+    // and last event (when both lie in one run) and every thread then searches only between the
+    // two (~3 destinations on C5) -- instead of 17 dependent loads over 100k offsets per event.
+    __shared__ uint32_t s_d[2];
+    const uint32_t total = base[n_runs];
     const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-    if (e >= base[n_runs]) return;
-    uint32_t r = 0;
-    while (r + 1 < n_runs && base[r + 1] <= e) ++r;
+    const uint32_t e0 = blockIdx.x * 256, e1 = min(e0 + 255, total - 1);
+    auto run_of = [&](uint32_t x) {
+        uint32_t r = 0;
+        while (r + 1 < n_runs && base[r + 1] <= x) ++r;
+        return r;
+    };
+    auto dst_of = [&](const uint32_t* o, uint32_t le, uint32_t lo, uint32_t hi) {   // o[d] <= le < o[d+1]
+        while (hi - lo > 1) {
+            const uint32_t m = (lo + hi) >> 1;
+            if (o[m] <= le) lo = m; else hi = m;
+        }
+        return lo;
+    };
+    const uint32_t rb0 = run_of(e0), rb1 = run_of(e1);
+    const uint32_t* ob = off + (size_t)rb0 * (n_dst + 1);
+    if (rb0 == rb1 && threadIdx.x < 2) s_d[threadIdx.x] = dst_of(ob, (threadIdx.x ? e1 : e0) - base[rb0], 0, n_dst);
+    __syncthreads();
+    if (e >= total) return;   // no barrier follows
+    const uint32_t r = rb0 == rb1 ? rb0 : run_of(e);
     const uint32_t le = e - base[r];
     const uint32_t* o = off + (size_t)r * (n_dst + 1);
-    uint32_t lo = 0, hi = n_dst;   // d with o[d] <= le < o[d+1]
-    while (hi - lo > 1) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (o[m] <= le) lo = m; else hi = m;
-    }
-    const uint32_t d = lo;
+    const uint32_t d = rb0 == rb1 ? dst_of(o, le, s_d[0], s_d[1] + 1) : dst_of(o, le, 0, n_dst);
     const Ev24 x = in[e];
     uint32_t rank = le - o[d];
     for (uint32_t r2 = 0; r2 < n_runs; ++r2) {
