@@ -17,7 +17,7 @@ namespace shd {
     X(SSSP_NO_DELTA) X(SSSP_DELTA) X(SSSP_STATS) X(SPIN_WAIT)                                   \
     X(PRUNE_DENSE_BUILD) X(SSSP_HUB) X(SYNC_KERNEL)                                               \
     X(EQ_COUNT_BLOCKS) X(EQ_WAVE_MERGE) X(EQ_SEARCH_ONLY) X(EQ_MAX_RUNS) X(RELAY_GROUP_SENDS) X(HIST_SCALAR) X(B7_STOP) X(RELAY_FORCE_V1)         \
-    X(RELAY_FORCE_V3) X(RELAY_NO_LDS_MAP) X(SHARD_CHUNK_ROWS) X(SHARD_REPLICATE_MB)             \
+    X(RELAY_FORCE_V3) X(RELAY_NO_LDS_MAP) X(MERGE_BY_EVENT) X(SHARD_CHUNK_ROWS) X(SHARD_REPLICATE_MB)             \
     X(SHARD_RESERVE_SLOTS)
 
 enum Knob : int {

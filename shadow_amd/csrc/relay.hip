@@ -2161,6 +2161,138 @@ __global__ __launch_bounds__(256) void merge_runs24(uint32_t n_runs, uint32_t n_
     out_p[pos] = x.pkt;
 }
 
+// merge_runs24 by destination (default): a wave per destination takes the destination's
+// events of every sender run (<= 128: C5 has ~100 per destination), sorts the unique keys
+// (deliver - tmin) << 8 | index with the wave network (wave.h) and stores them in rank order,
+// coalesced -- instead of a thread per event searching every sibling run's segment (a chain of
+// dependent 24-byte loads per run).  A destination with more events, a deliver-time span of
+// 2^24 ns or more, or two equal deliver times (their order needs (src, seq)) is merged by the
+// per-event searches in the same wave.
+__global__ __launch_bounds__(256) void merge_dst24(uint32_t n_runs, uint32_t n_dst, const uint32_t* __restrict__ base,
+                                                   const uint32_t* __restrict__ off, const Ev24* __restrict__ in,
+                                                   const uint32_t* __restrict__ out_off, uint64_t* __restrict__ out_t,
+                                                   uint32_t* __restrict__ out_s, uint64_t* __restrict__ out_q,
+                                                   uint32_t* __restrict__ out_p) {
+    constexpr int NPL = 2;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t d = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (d >= n_dst) return;   // wave-uniform; no barrier in this kernel
+    // lane q < n_runs: run q's segment of destination d
+    uint32_t seg = 0, cnt = 0;
+    if (lane < n_runs) {
+        const uint32_t* o = off + (size_t)lane * (n_dst + 1);
+        seg = base[lane] + o[d];
+        cnt = o[d + 1] - o[d];
+    }
+    uint32_t incl = cnt;
+    for (uint32_t k = 1; k < 64; k <<= 1) {
+        const uint32_t y = __shfl_up(incl, k);
+        if (lane >= k) incl += y;
+    }
+    const uint32_t n = __shfl(incl, 63), pre = incl - cnt;
+    const uint32_t out0 = out_off[d];
+    bool done = false;
+    if (n <= 64u * NPL && n_runs <= 64) {
+        Ev24 x[NPL];
+        uint64_t tmn = ~0ull, tmx = 0;
+#pragma unroll
+        for (int c = 0; c < NPL; ++c) {
+            const uint32_t i = lane + 64u * c;
+            // the run holding staged index i: the last q whose prefix is <= i (ballot over lanes)
+            const uint64_t m = __ballot(lane < n_runs && cnt > 0);
+            uint32_t at = 0;
+            for (uint64_t mm = m; mm; mm &= mm - 1) {
+                const int q = __builtin_ctzll(mm);
+                const uint32_t pq = __shfl(pre, q), sq = __shfl(seg, q);
+                if (i < n && pq <= i) at = sq + (i - pq);
+            }
+            x[c] = i < n ? in[at] : Ev24{~0ull, 0, 0, 0};
+            if (i < n) {
+                tmn = x[c].deliver < tmn ? x[c].deliver : tmn;
+                tmx = x[c].deliver > tmx ? x[c].deliver : tmx;
+            }
+        }
+        for (int k = 32; k > 0; k >>= 1) {
+            const uint64_t a = __shfl_xor(tmn, k), b = __shfl_xor(tmx, k);
+            tmn = a < tmn ? a : tmn;
+            tmx = b > tmx ? b : tmx;
+        }
+        if (n > 0 && tmx - tmn < (1ull << 24)) {
+            uint32_t k32[NPL];
+#pragma unroll
+            for (int c = 0; c < NPL; ++c) {
+                const uint32_t i = lane + 64u * c;
+                k32[c] = i < n ? ((uint32_t)(x[c].deliver - tmn) << 8) | i : ~0u;
+            }
+            wave_bitonic32<NPL>(k32, lane);
+            bool tie = false;
+#pragma unroll
+            for (int c = 0; c < NPL; ++c) {
+                const uint32_t down = (uint32_t)__shfl_down((int)k32[c], 1);
+                const uint32_t first = c + 1 < NPL ? (uint32_t)__shfl((int)k32[c + 1 < NPL ? c + 1 : c], 0) : ~0u;
+                const uint32_t nx = lane == 63 ? first : down;
+                if (lane + 64u * c + 1 < n && (nx >> 8) == (k32[c] >> 8)) tie = true;
+            }
+            if (__ballot(tie) == 0) {
+#pragma unroll
+                for (int c = 0; c < NPL; ++c) {
+                    const uint32_t r = lane + 64u * c, i = k32[c] & 0xFFu;
+                    const int src_lane = (int)(i & 63u);
+                    // element i sits in lane i % 64, register i / 64 (every lane shuffles both)
+                    Ev24 y{0, 0, 0, 0};
+#pragma unroll
+                    for (int c2 = 0; c2 < NPL; ++c2) {
+                        const uint64_t t = __shfl(x[c2].deliver, src_lane), q = __shfl(x[c2].seq, src_lane);
+                        const uint32_t sv = (uint32_t)__shfl((int)x[c2].src, src_lane);
+                        const uint32_t pv = (uint32_t)__shfl((int)x[c2].pkt, src_lane);
+                        if ((i >> 6) == (uint32_t)c2) y = Ev24{t, q, sv, pv};
+                    }
+                    if (r < n) {
+                        out_t[out0 + r] = y.deliver;
+                        out_s[out0 + r] = y.src;
+                        out_q[out0 + r] = y.seq;
+                        out_p[out0 + r] = y.pkt;
+                    }
+                }
+                done = true;
+            }
+        }
+    }
+    if (done) return;
+    // per-event searches (merge_runs24's rank rule) over this destination's events
+    for (uint32_t i = lane; i < n; i += 64) {
+        uint32_t q0 = 0, at = 0, rank = 0;
+        uint32_t acc = 0;   // i's run: the segment counts' running sum
+        for (uint32_t q = 0; q < n_runs; ++q) {
+            const uint32_t* o = off + (size_t)q * (n_dst + 1);
+            const uint32_t c = o[d + 1] - o[d];
+            if (i >= acc && i < acc + c) {
+                q0 = q;
+                at = base[q] + o[d] + (i - acc);
+                rank = i - acc;
+            }
+            acc += c;
+        }
+        const Ev24 x = in[at];
+        for (uint32_t r2 = 0; r2 < n_runs; ++r2) {
+            if (r2 == q0) continue;
+            const uint32_t* o2 = off + (size_t)r2 * (n_dst + 1);
+            uint32_t a = base[r2] + o2[d], b = base[r2] + o2[d + 1];
+            const uint32_t a0 = a;
+            while (a < b) {
+                const uint32_t m = (a + b) >> 1;
+                const Ev24 y = in[m];
+                if (ev3_less(y.deliver, y.src, y.seq, x.deliver, x.src, x.seq)) a = m + 1; else b = m;
+            }
+            rank += a - a0;
+        }
+        out_t[out0 + rank] = x.deliver;
+        out_s[out0 + rank] = x.src;
+        out_q[out0 + rank] = x.seq;
+        out_p[out0 + rank] = x.pkt;
+    }
+}
+
 // sharded rounds' buffers that depend only on the host count and the ranks (shd_relay_setup)
 static shd_status relay_shard_alloc(shd_ctx* ctx) {
     RelayState& R = ctx->relay;
@@ -2292,7 +2424,12 @@ static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const sh
     SHD_HIP(hipMemcpyAsync(d_base, rbase.data(), (world + 1) * 4, hipMemcpyHostToDevice, s));
     merge_offsets<<<div_up((uint64_t)n_own + 1, 256), 256, 0, s>>>(world, n_own, R.x_roff.as<uint32_t>(),
                                                                   R.m_off.as<uint32_t>());
-    if (n_recv)
+    if (n_recv && ctx->knobs.get(K_MERGE_BY_EVENT, 0) != 1)
+        merge_dst24<<<div_up(n_own, 4), 256, 0, s>>>(world, n_own, d_base, R.x_roff.as<uint32_t>(),
+                                                     R.x_rrec.as<Ev24>(), R.m_off.as<uint32_t>(),
+                                                     R.m_deliver.as<uint64_t>(), R.m_src.as<uint32_t>(),
+                                                     R.m_seq.as<uint64_t>(), R.m_pkt.as<uint32_t>());
+    else if (n_recv)
         merge_runs24<<<div_up(n_recv, 256), 256, 0, s>>>(world, n_own, d_base, R.x_roff.as<uint32_t>(),
                                                         R.x_rrec.as<Ev24>(), R.m_off.as<uint32_t>(),
                                                         R.m_deliver.as<uint64_t>(), R.m_src.as<uint32_t>(),
