@@ -220,12 +220,20 @@ struct HostComm final : Comm {
             r_off[r] = r_end;
             r_end += u;
         }
-        if (st == SHD_OK) st = grow(hs, hs_cap, s_end);
-        if (st == SHD_OK) st = grow(hr, hr_cap, r_end);
-        // a rank that cannot stage still takes part with its status alone (sizes of 8 bytes are
-        // what its peers expect from a failed rank only if they fail too: the sizes were agreed
-        // before, so a staging failure is reported and the transport is left to the caller)
-        if (st != SHD_OK) return st;
+        // Every rank enters the transport, whatever happens locally: its peers are already
+        // blocked in the caller's collective.  Pinned staging that cannot grow falls back to
+        // pageable memory for this call; only when that fails too is the rank unable to take part.
+        std::vector<unsigned char> hs_tmp, hr_tmp;
+        unsigned char* S = hs;
+        unsigned char* Rv = hr;
+        try {
+            if (grow(hs, hs_cap, s_end) == SHD_OK) S = hs;
+            else { hs_tmp.resize(s_end); S = hs_tmp.data(); }
+            if (grow(hr, hr_cap, r_end) == SHD_OK) Rv = hr;
+            else { hr_tmp.resize(r_end); Rv = hr_tmp.data(); }
+        } catch (...) {
+            return SHD_ERR_NOMEM;
+        }
         for (int r = 0; r < n; ++r) {
             size_t at = so[r] + 8;
             for (int k = 0; k < n_parts; ++k) {
@@ -237,7 +245,7 @@ struct HostComm final : Comm {
                         st = SHD_ERR_HIP;
                     continue;
                 }
-                if (sb[i] && hipMemcpyAsync(hs + at, src[i], sb[i], hipMemcpyDeviceToHost, s) != hipSuccess)
+                if (sb[i] && hipMemcpyAsync(S + at, src[i], sb[i], hipMemcpyDeviceToHost, s) != hipSuccess)
                     st = SHD_ERR_HIP;
                 at += sb[i];
             }
@@ -245,14 +253,14 @@ struct HostComm final : Comm {
         if (hipStreamSynchronize(s) != hipSuccess && st == SHD_OK) st = SHD_ERR_HIP;
         for (int r = 0; r < n; ++r) {
             const uint64_t w = (uint64_t)st;
-            std::memcpy(hs + so[r], &w, 8);   // shared offsets get the same word
+            std::memcpy(S + so[r], &w, 8);   // shared offsets get the same word
         }
-        if (ops.all_to_allv(ops.user, hs, s_bytes.data(), s_off.data(), hr, r_bytes.data(), r_off.data()) != 0)
+        if (ops.all_to_allv(ops.user, S, s_bytes.data(), s_off.data(), Rv, r_bytes.data(), r_off.data()) != 0)
             return SHD_ERR_HIP;   // the transport failed: the caller's to handle, as RCCL's would be
         shd_status all = SHD_OK;
         for (int q = 0; q < n && all == SHD_OK; ++q) {
             uint64_t w = 0;
-            std::memcpy(&w, hr + r_off[q], 8);
+            std::memcpy(&w, Rv + r_off[q], 8);
             all = (shd_status)w;
         }
         if (all != SHD_OK) return all;
@@ -261,7 +269,7 @@ struct HostComm final : Comm {
             size_t at = r_off[q] + 8;
             for (int k = 0; k < n_parts; ++k) {
                 const size_t i = (size_t)q * n_parts + k;
-                if (rb[i] && hipMemcpyAsync(dst[i], hr + at, rb[i], hipMemcpyHostToDevice, s) != hipSuccess)
+                if (rb[i] && hipMemcpyAsync(dst[i], Rv + at, rb[i], hipMemcpyHostToDevice, s) != hipSuccess)
                     all = SHD_ERR_HIP;
                 at += rb[i];
             }

@@ -655,7 +655,9 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
     __shared__ uint32_t s_rowof[kS5Hosts], s_rownode[kS5Hosts], s_run[kS5Hosts], s_base[kS5Hosts];
     __shared__ uint32_t s_wsum[kS6Threads / 64], s_nrows;
     __shared__ uint8_t s_own[kS6Cap];   // chunk position -> host slot in the group
-    __shared__ uint32_t s_pfnode[kS5RowLds / kS6Threads], s_pfn;   // next group's path rows
+    // next group's distinct source nodes: up to one per host of the group (a group of kS5Hosts
+    // hosts spans at most kS5Hosts nodes; the prefetch stages pn * n_nodes <= kS5RowLds entries)
+    __shared__ uint32_t s_pfnode[kS5Hosts], s_pfn;
     static_assert(kS5RowLds % kS6Threads == 0, "row prefetch: whole entries per thread");
     constexpr uint32_t kPf = kS5RowLds / kS6Threads;
     uint2 pf[kPf];             // the next group's staged path rows, prefetched during this group
@@ -764,7 +766,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 const uint64_t fm = __ballot(first);
                 if (first) {
                     const uint32_t ri = (uint32_t)__popcll(fm & ((2ull << tid) - 1ull)) - 1u;
-                    if (ri < kPf) s_pfnode[ri] = nd;
+                    s_pfnode[ri] = nd;   // ri < nh2 <= kS5Hosts
                 }
                 if (tid == 0) s_pfn = (uint32_t)__popcll(fm);
             }
@@ -1871,12 +1873,15 @@ static bool relay_v7_ok(shd_ctx* ctx, uint64_t n) {
     RelayState& R = ctx->relay;
     if (!R.hn_bits || R.force_v3 || R.n_hosts > kV7MaxHosts || n > kV7MaxPackets) return false;
     if (R.n_src == 0 || std::min<uint32_t>(div_up(R.n_src, kS5Hosts), (uint32_t)ctx->n_cu) > kColMaxG) return false;
-    static size_t stat_lds = 0;
-    if (!stat_lds) {
+    // the stamp's static LDS, asked once (a function-local static: initialised once even when
+    // two in-process ranks call the relay from two threads)
+    static const size_t stat_lds = [] {
         hipFuncAttributes at{};
-        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&relay_stamp_v6<true>)) != hipSuccess) return false;
-        stat_lds = at.sharedSizeBytes;
-    }
+        return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&relay_stamp_v6<true>)) == hipSuccess
+                   ? (size_t)at.sharedSizeBytes
+                   : (size_t)0;
+    }();
+    if (!stat_lds) return false;
     const uint32_t n_bins = div_up(R.n_hosts, kBinDst);
     return stat_lds + (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4 <= 160 * 1024;
 }
@@ -2189,8 +2194,9 @@ __global__ __launch_bounds__(256) void merge_dst24(uint32_t n_runs, uint32_t n_d
         const uint32_t y = __shfl_up(incl, k);
         if (lane >= k) incl += y;
     }
-    const uint32_t n = __shfl(incl, 63), pre = incl - cnt;
-    const uint32_t out0 = out_off[d];
+    const uint32_t pre = incl - cnt;
+    // the destination's event count from the merged offsets (every run, also past lane 63)
+    const uint32_t out0 = out_off[d], n = out_off[d + 1] - out0;
     bool done = false;
     if (n <= 64u * NPL && n_runs <= 64) {
         Ev24 x[NPL];
