@@ -484,7 +484,9 @@ shd_status shd_relay_set_counters(shd_ctx* ctx, int32_t enabled);
 shd_status shd_path_packet_counts(shd_ctx* ctx, uint64_t* counts);
 
 /* Which device pipeline ran the last successful round (diagnostics; no reference counterpart):
- * 7 = destination-bin placement, 3 = radix sort by destination, 1 = 64-bit records. */
+ * 7 = destination-bin placement, 3 = radix sort by destination, 1 = 64-bit records; 8 = a
+ * sharded round whose pipeline-7 bins went to their destination ranks as stamped and were sorted
+ * there (no packing or merge pass; otherwise a sharded round reports the local pipeline). */
 shd_status shd_relay_last_pipeline(const shd_ctx* ctx, int32_t* pipeline);
 
 /* ---------------------------------------------------------------------------------------

@@ -43,6 +43,25 @@ struct DevBuf {
     }
 };
 
+struct PinBuf {   // grow-only pinned host memory
+    void* p = nullptr;
+    size_t bytes = 0;
+    PinBuf() = default;
+    PinBuf(const PinBuf&) = delete;
+    PinBuf& operator=(const PinBuf&) = delete;
+    ~PinBuf() { if (p) (void)hipHostFree(p); }
+    shd_status ensure(size_t need) {
+        if (need <= bytes) return SHD_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipHostMalloc(&p, need, hipHostMallocDefault) != hipSuccess) return SHD_ERR_NOMEM;
+        bytes = need;
+        return SHD_OK;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
 struct ScanScratch {   // look-back states of the hand-written scans (scan.h)
     DevBuf state;       // [tiles][2] u64
     uint32_t epoch = 0;
@@ -144,6 +163,10 @@ struct RelayState {
     // received, and the merged events of this rank's destinations (engine-owned outputs)
     DevBuf x_rec, x_words, x_off, x_roff, x_rrec, m_off, m_deliver, m_src, m_seq, m_pkt;
     uint64_t x_cap = 0;   // events x_rrec and m_* hold (grown with a growth agreement, never between collectives)
+    // relay_round_sharded_v7: the senders' bin scans, the sizing summary (+ its pinned copy) and
+    // the per-sender receive / packet bases
+    DevBuf xs_sc, xs_out, xs_b;
+    PinBuf xs_pin;
     // shd_relay_flush (flush.hip): the round's draws came from the CPU (top 32 bits in `draws`), the
     // staged runs and records as uploaded, the send permutation (grouped <-> stage order) and the
     // packed outputs

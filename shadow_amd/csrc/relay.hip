@@ -350,6 +350,11 @@ struct RelayArgs3 {
     const uint32_t* seg_pre;
     uint32_t n_bins;
     uint32_t gs;         // hosts per group of relay_stamp_v6 / relay_bin_hist (<= kS5Hosts)
+    // v7 under a communicator (relay_round_sharded_v7): every rank's destinations [r * sh_per,
+    // ...) start a fresh bin, so rank r's bins are [r * sh_bpr, ...) and the records bound for it
+    // one contiguous slice; sh_mul = ceil(2^40 / sh_per).  sh_per = 0: bins of consecutive hosts.
+    uint32_t sh_per, sh_bpr;
+    uint64_t sh_mul;
 };
 
 #ifndef SHD_DRAW_SLICE
@@ -640,6 +645,20 @@ __device__ unsigned long long g_stamp_prof[12];
 // status and the destination's low bits so bin_sort_v7 can filter and split them.
 constexpr uint32_t kBinShift = 5;
 constexpr uint32_t kBinDst = 1u << kBinShift;
+
+// the bin of a destination and its place dl in the bin (RelayArgs3::sh_per)
+__device__ __forceinline__ uint32_t dst_bin(const RelayArgs3& a, uint32_t dst, uint32_t& dl) {
+    if (a.sh_per == 0) {
+        dl = dst & (kBinDst - 1);
+        return dst >> kBinShift;
+    }
+    // dst / sh_per: exact for dst, sh_per < 2^18 (the error of the rounded-up reciprocal stays
+    // below 2^-22, under the smallest distance 1 / sh_per of a fraction from the next integer)
+    const uint32_t r = (uint32_t)(((uint64_t)dst * a.sh_mul) >> 40);
+    const uint32_t x = dst - r * a.sh_per;
+    dl = x & (kBinDst - 1);
+    return r * a.sh_bpr + (x >> kBinShift);
+}
 constexpr uint32_t kHistSplit = 2;   // histogram rows per stamp workgroup (relay_bin_hist)
 
 template <bool BIN>
@@ -891,12 +910,13 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                         a.key[idx[i]] = st[i] == kStSent ? dst[i] : a.n_hosts;
                         if (st[i] == kStSent) a.rec[idx[i]] = make_uint4(doff[i], s_host[hl[i]], local, idx[i]);
                     } else if (dst[i] < a.n_hosts) {
-                        const uint32_t bin = dst[i] >> kBinShift, sh = (bin & 3u) * 8u;
+                        uint32_t dl;
+                        const uint32_t bin = dst_bin(a, dst[i], dl), sh = (bin & 3u) * 8u;
                         const uint32_t old = atomicAdd(&s_cur[bin >> 2], 1u << sh);
                         const uint32_t slot = a.bin_base[bin] + a.seg_pre[(size_t)blockIdx.x * a.n_bins + bin] +
                                               ((old >> sh) & 0xFFu);
                         a.rec[slot] = make_uint4(doff[i],
-                                                 s_host[hl[i]] | ((dst[i] & (kBinDst - 1)) << 18) |
+                                                 s_host[hl[i]] | (dl << 18) |
                                                      ((uint32_t)st[i] << 24),
                                                  local, idx[i]);
                     }
@@ -1401,7 +1421,10 @@ __global__ __launch_bounds__(256) void relay_bin_hist(RelayArgs3 a, uint32_t G, 
             }
 #pragma unroll
             for (uint32_t u = 0; u < kHistUnroll; ++u)
-                if (d[u] < a.n_hosts) atomicAdd(&s_cnt[d[u] >> kBinShift], 1u);
+                if (d[u] < a.n_hosts) {
+                    uint32_t dl;
+                    atomicAdd(&s_cnt[dst_bin(a, d[u], dl)], 1u);
+                }
         }
     }
     __syncthreads();
@@ -1442,7 +1465,10 @@ __global__ __launch_bounds__(kHist4Threads) void relay_bin_hist4(RelayArgs3 a, u
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const uint32_t i = 4 * c + u;
-                if (i >= b && i < e && d[u] < a.n_hosts) atomicAdd(&s_cnt[d[u] >> kBinShift], 1u);
+                if (i >= b && i < e && d[u] < a.n_hosts) {
+                    uint32_t dl;
+                    atomicAdd(&s_cnt[dst_bin(a, d[u], dl)], 1u);
+                }
             }
         }
     }
@@ -1656,40 +1682,95 @@ __device__ __forceinline__ void v7_sort_run(uint32_t n, uint32_t lane, const uin
     }
 }
 
+// K4 of a sharded round (relay_round_sharded_v7, X = true): bin j of this rank's own bins takes
+// its records from every sender's received slice: sender q's records of the bin start at
+// rbase[q] + sc[q * stride + fb + j] - sc[q * stride + fb] (sc: the senders' exclusive bin scans
+// from the gathered sizing rows).  Packet indices are per sender; the sort key uses the global
+// packet order (the senders' batches back to back, pbase[q] = packets of the senders before q),
+// which is (src host, event id) order because the senders own increasing source ranges.
+struct XSrc {
+    uint32_t world, me, fb, stride, kq;
+    const uint32_t* sc;
+    const uint32_t* rbase;   // sender q's slice in the received records (q != me)
+    const uint32_t* pbase;
+    const uint4* own;        // this rank's own records stay where its stamp put them (never exchanged)
+};
+
 // K4 (v7): one workgroup per bin, bins taken in ticket order so the event offsets can use a
 // decoupled look-back (publish the bin's sent count, add the predecessors' counts).  The bin's
 // records are staged in LDS, grouped by destination, each run sorted by one wave into the
 // bin's output order, and the bin's events stored in that order (coalesced).
+template <bool X>
 __global__ __launch_bounds__(kB7Threads) void bin_sort_v7(uint32_t n_hosts, uint32_t n_bins,
                                                           const uint32_t* __restrict__ bin_base,
                                                           const uint4* __restrict__ rec,
                                                           unsigned long long* __restrict__ lb,
                                                           uint32_t* __restrict__ ev_off, V7Out o,
                                                           const unsigned long long* __restrict__ red,
-                                                          uint32_t stop) {   // tuning: stop after phase
+                                                          uint32_t stop,   // tuning: stop after phase
+                                                          XSrc xs) {
     __shared__ uint4 x[kB7Cap];
     __shared__ uint16_t ls[kB7Cap], pm[kB7Cap];
     __shared__ uint32_t s_cnt[kBinDst], s_off[kBinDst + 1], s_cur[kBinDst], s_bin, s_excl;
-    if (red[6]) return;   // overflow: the host reruns the round on v3
+    __shared__ uint32_t s_qpre[X ? 65 : 1], s_qat[X ? 64 : 1], s_pb[X ? 64 : 1];
+    // (X: the own sender's records are read from xs.own, every other sender's from rec)
+    if (!X && red[6]) return;   // overflow: the host reruns the round on v3
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) s_bin = atomicAdd(reinterpret_cast<unsigned int*>(&lb[n_bins]), 1u);
     if (tid < kBinDst) s_cnt[tid] = s_cur[tid] = 0;
     __syncthreads();
     const uint32_t bin = s_bin;
-    const uint32_t B = bin_base[bin], N = bin_base[bin + 1] - B;
+    uint32_t B = 0, N = 0;
+    if constexpr (X) {   // wave 0: every sender's segment of the bin
+        if (tid < 64) {
+            uint32_t c = 0, at = 0, pb = 0;
+            if (lane < xs.world) {
+                const uint32_t* sq = xs.sc + (size_t)lane * xs.stride + xs.fb;
+                const uint32_t a0 = sq[0], a1 = sq[bin], a2 = sq[bin + 1];
+                at = lane == xs.me ? a1 : xs.rbase[lane] + (a1 - a0);
+                c = a2 - a1;
+                pb = xs.pbase[lane];
+            }
+            uint32_t incl = c;
+            for (uint32_t q = 1; q < 64; q <<= 1) {
+                const uint32_t y = __shfl_up(incl, q);
+                if (lane >= q) incl += y;
+            }
+            s_qpre[lane + 1] = incl;
+            if (lane == 0) s_qpre[0] = 0;
+            s_qat[lane] = at;
+            s_pb[lane] = pb;
+        }
+        __syncthreads();
+        N = s_qpre[xs.world];   // <= kB7Cap: the host checked every bin's total before the exchange
+    } else {
+        B = bin_base[bin];
+        N = bin_base[bin + 1] - B;
+    }
     {   // every load of the bin in flight at once (N <= kB7Cap)
         uint4 r[kB7Per];
 #pragma unroll
         for (uint32_t u = 0; u < kB7Per; ++u) {
             const uint32_t i = tid + u * kB7Threads;
-            if (i < N) r[u] = rec[B + i];
+            if (i < N) {
+                if constexpr (X) {
+                    uint32_t q = 0;   // the sender of staged index i: the last q with s_qpre[q] <= i
+                    for (uint32_t k = xs.kq; k > 0; k >>= 1)   // (kq: the largest power of two < world)
+                        if (q + k < xs.world && s_qpre[q + k] <= i) q += k;
+                    r[u] = (q == xs.me ? xs.own : rec)[s_qat[q] + (i - s_qpre[q])];
+                    r[u].w += s_pb[q];   // global packet order
+                    r[u].y |= q << 26;   // the sender, for the packet index of the output
+                } else {
+                    r[u] = rec[B + i];
+                }
+            }
         }
 #pragma unroll
         for (uint32_t u = 0; u < kB7Per; ++u) {
             const uint32_t i = tid + u * kB7Threads;
             if (i < N) {
                 x[i] = r[u];
-                if ((r[u].y >> 24) == kStSent) atomicAdd(&s_cnt[(r[u].y >> 18) & (kBinDst - 1)], 1u);
+                if (((r[u].y >> 24) & 3u) == kStSent) atomicAdd(&s_cnt[(r[u].y >> 18) & (kBinDst - 1)], 1u);
             }
         }
     }
@@ -1740,7 +1821,7 @@ __global__ __launch_bounds__(kB7Threads) void bin_sort_v7(uint32_t n_hosts, uint
     if (stop == 2) return;
     for (uint32_t i = tid; i < N; i += kB7Threads) {
         const uint32_t y = x[i].y;
-        if ((y >> 24) == kStSent) {
+        if (((y >> 24) & 3u) == kStSent) {
             const uint32_t dl = (y >> 18) & (kBinDst - 1);
             ls[s_off[dl] + atomicAdd(&s_cur[dl], 1u)] = (uint16_t)i;
         }
@@ -1767,7 +1848,14 @@ __global__ __launch_bounds__(kB7Threads) void bin_sort_v7(uint32_t n_hosts, uint
     }
     __syncthreads();
     if (stop == 4) return;
-    for (uint32_t p = tid; p < S; p += kB7Threads) v7_emit(o, (size_t)excl + p, x[pm[p]]);
+    for (uint32_t p = tid; p < S; p += kB7Threads) {
+        uint4 r = x[pm[p]];
+        if constexpr (X) {
+            r.w -= s_pb[r.y >> 26];   // back to the index in the sender's batch
+            r.y &= kV7MaxHosts - 1;
+        }
+        v7_emit(o, (size_t)excl + p, r);
+    }
 }
 
 // Narrow pipeline: K1 stamp, K2 radix sort by destination, K3 offsets, K4 per-run sort; one
@@ -1869,7 +1957,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
 
 // v7 eligibility: narrow table, LDS host map, src ids and packet indices within the record /
 // key fields, and the stamp's LDS (map + slot counters) within the CU's 160 KB
-static bool relay_v7_ok(shd_ctx* ctx, uint64_t n) {
+static bool relay_v7_ok(shd_ctx* ctx, uint64_t n, uint32_t n_bins) {
     RelayState& R = ctx->relay;
     if (!R.hn_bits || R.force_v3 || R.n_hosts > kV7MaxHosts || n > kV7MaxPackets) return false;
     if (R.n_src == 0 || std::min<uint32_t>(div_up(R.n_src, kS5Hosts), (uint32_t)ctx->n_cu) > kColMaxG) return false;
@@ -1882,7 +1970,6 @@ static bool relay_v7_ok(shd_ctx* ctx, uint64_t n) {
                    : (size_t)0;
     }();
     if (!stat_lds) return false;
-    const uint32_t n_bins = div_up(R.n_hosts, kBinDst);
     return stat_lds + (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4 <= 160 * 1024;
 }
 
@@ -1899,14 +1986,37 @@ static uint32_t v7_group_size(const shd_ctx* ctx, uint32_t n_src, uint32_t G, ui
     return (uint32_t)std::min<uint64_t>(kS5Hosts, std::max<uint64_t>(1, div_up((uint64_t)n_src, (uint64_t)G * m)));
 }
 
+// The bins of a sharded round (relay_round_sharded_v7): rank r's destinations [r * per, ...)
+// start bin r * bpr; n_bins over all ranks
+struct XShard {
+    uint32_t per = 0, bpr = 0, n_bins = 0;
+    uint64_t mul = 0;
+    uint32_t first_bin(uint32_t r) const { return std::min<uint32_t>(r * bpr, n_bins); }
+};
+
+static XShard xshard(uint32_t H, uint32_t world) {
+    XShard x;
+    x.per = (uint32_t)div_up((uint64_t)H, (uint64_t)world);
+    x.bpr = div_up(x.per, kBinDst);
+    x.mul = ((1ull << 40) + x.per - 1) / x.per;
+    for (uint32_t r = 0; r < world; ++r) {
+        uint32_t lo = 0, hi = 0;
+        shard_range(H, (int)world, (int)r, &lo, &hi);
+        x.n_bins += div_up(hi - lo, kBinDst);
+    }
+    return x;
+}
+
+// v7 up to and including the stamp; with xsh (a sharded round) the records stay in their bins
+// for the exchange (no bin sort, no read-back), else the bin sort and the reductions' read-back
 static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
-                                  shd_relay_out* o) {
+                                  shd_relay_out* o, const XShard* xsh = nullptr) {
     RelayState& R = ctx->relay;
     hipStream_t s = ctx->stream;
     const uint64_t n = b->n_packets;
     const uint32_t H = R.n_hosts;
     const size_t nn = std::max<uint64_t>(n, 1);
-    const uint32_t n_bins = div_up(H, kBinDst);
+    const uint32_t n_bins = xsh ? xsh->n_bins : div_up(H, kBinDst);
     const uint32_t G = std::min<uint32_t>(div_up(R.n_src, kS5Hosts), (uint32_t)ctx->n_cu);
     SHD_TRY(R.rec.ensure(nn * 16));
     SHD_TRY(R.draws.ensure(nn * 4));
@@ -1915,6 +2025,11 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     SHD_TRY(R.bin_lb.ensure((size_t)(n_bins + 1) * 8));
     RelayArgs3 a = relay_args3(ctx, b, rd, o);
     a.gs = v7_group_size(ctx, R.n_src, G, n);
+    if (xsh) {
+        a.sh_per = xsh->per;
+        a.sh_bpr = xsh->bpr;
+        a.sh_mul = xsh->mul;
+    }
     uint32_t* tot = R.bin_base.as<uint32_t>() + n_bins + 1;
     a.bin_base = R.bin_base.as<uint32_t>();
     a.n_bins = n_bins;
@@ -1944,12 +2059,16 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     if (k0) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
     relay_stamp_v6<true><<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4, s>>>(
         a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
+    if (xsh) {
+        SHD_HIP(hipGetLastError());
+        return SHD_OK;
+    }
     V7Out vo{o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt,
              a.abs_seq ? nullptr : R.next_id.as<uint64_t>(), rd->round_end};
     const uint32_t stop = ctx->knobs.get(K_B7_STOP, 0);   // tuning only: partial K4 (wrong output)
-    bin_sort_v7<<<n_bins, kB7Threads, 0, s>>>(H, n_bins, R.bin_base.as<uint32_t>(), R.rec.as<uint4>(),
-                                             R.bin_lb.as<unsigned long long>(), o->ev_off, vo, a.red,
-                                             stop);
+    bin_sort_v7<false><<<n_bins, kB7Threads, 0, s>>>(H, n_bins, R.bin_base.as<uint32_t>(), R.rec.as<uint4>(),
+                                                    R.bin_lb.as<unsigned long long>(), o->ev_off, vo, a.red,
+                                                    stop, XSrc{});
     SHD_HIP(hipGetLastError());
     SHD_TRY(readback(ctx, s, 8, R.red.p, 8 * sizeof(unsigned long long)));
     std::memcpy(R.red_host, ctx->h_pin + 8, sizeof(R.red_host));
@@ -1986,7 +2105,7 @@ static shd_status relay_run(shd_ctx* ctx, const shd_batch* b, const shd_round* r
     R.last_pipe = 1;
     if (v2) {
         bool done = false;
-        if (relay_v7_ok(ctx, b->n_packets)) {
+        if (relay_v7_ok(ctx, b->n_packets, div_up(H, kBinDst))) {
             SHD_TRY(zero_counts());
             SHD_TRY(relay_device_v7(ctx, b, rd, o));
             done = !R.red_host[6];   // else a bin overflowed: redo with the radix pipeline
@@ -2299,6 +2418,124 @@ __global__ __launch_bounds__(256) void merge_dst24(uint32_t n_runs, uint32_t n_d
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Sharded rounds without the merge (relay_round_sharded_v7, the default when every rank runs
+// pipeline 7).  The stamp places every record into its destination bin as on one GPU, but the
+// bins restart at every rank's first destination (XShard), so the records bound for rank r are
+// one contiguous slice of the stamp's output and each of r's bins is a sub-slice of it.  The
+// exchange moves those 16-byte records as they lie -- no packing, no per-peer offsets: every
+// rank's per-bin counts ride in the one sizing all-gather -- and the receiver runs the bin sort
+// over its own bins with each bin's records gathered from every sender's slice (bin_sort_v7<X>):
+// that yields its destinations' events in EventQueue order directly, so no merge pass follows.
+// One host sync sizes the exchange (statuses, reductions, counts, fallback flags of every
+// rank); a second reads the number of events received.
+// The sizing row of a rank (u64 words): [0] status [1] min deliver [2] min latency [3] sent
+// [4] receive capacity (events) [5] fallback flags [6] packets [7] spare, then the u32 record
+// count of every bin (all ranks' bins) from word kXsHead on.
+constexpr uint32_t kXsHead = 8;
+constexpr uint32_t kXsOverflow = 1, kXsWide = 2, kXsHost = 4;
+
+static size_t xs_row_words(uint32_t n_bins) { return kXsHead + ((size_t)n_bins + 1) / 2; }
+
+__global__ __launch_bounds__(256) void xs_row(const unsigned long long* __restrict__ red, const uint32_t* __restrict__ tot,
+                                              uint32_t n_bins, uint32_t ran, int32_t st_local, uint64_t cap,
+                                              uint64_t n_pkt, uint32_t host_flags, int32_t st_nohost,
+                                              int32_t st_invalid, uint64_t* __restrict__ row) {
+    const uint32_t t = threadIdx.x;
+    uint32_t* rt = reinterpret_cast<uint32_t*>(row + kXsHead);
+    for (uint32_t b = t; b < n_bins; b += 256) rt[b] = ran ? tot[b] : 0u;
+    if (t == 0) {
+        uint64_t st = (uint64_t)(int64_t)st_local, md = ~0ull, ml = ~0ull, ns = 0;
+        uint32_t fl = host_flags;
+        if (ran) {
+            if (red[6]) {
+                fl |= kXsOverflow;   // the stamp did not run: the fallback reruns the round
+            } else {
+                if (red[3] != ~0ull) st = (uint64_t)(int64_t)st_nohost;   // as relay_run: NO_HOST first
+                else if (red[5]) st = (uint64_t)(int64_t)st_invalid;
+                if (red[4]) fl |= kXsWide;
+                md = red[0];
+                ml = red[1];
+                ns = red[2];
+            }
+        }
+        row[0] = st;
+        row[1] = md;
+        row[2] = ml;
+        row[3] = ns;
+        row[4] = cap;
+        row[5] = fl;
+        row[6] = n_pkt;
+        row[7] = 0;
+    }
+}
+
+// block q: exclusive scan of sender q's bin counts -> sc[q * (n_bins + 1) + b]
+__global__ __launch_bounds__(1024) void xs_scan(const uint64_t* __restrict__ rows, size_t row_words, uint32_t n_bins,
+                                                uint32_t* __restrict__ sc) {
+    __shared__ uint32_t s_w[16];
+    const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t* t = reinterpret_cast<const uint32_t*>(rows + (size_t)q * row_words + kXsHead);
+    uint32_t* o = sc + (size_t)q * (n_bins + 1);
+    const uint32_t per = (n_bins + 1023) / 1024, b0 = min(n_bins, tid * per), b1 = min(n_bins, b0 + per);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += t[b];
+    uint32_t incl = sum;
+    for (uint32_t k = 1; k < 64; k <<= 1) {
+        const uint32_t y = __shfl_up(incl, k);
+        if (lane >= k) incl += y;
+    }
+    if (lane == 63) s_w[w] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum;
+    for (uint32_t u = 0; u < w; ++u) run += s_w[u];
+    for (uint32_t b = b0; b < b1; ++b) {
+        o[b] = run;
+        run += t[b];
+    }
+    if (tid == 1023) o[n_bins] = run;
+}
+
+// the sizing summary every rank derives alike from the gathered rows: out[0] = the largest bin
+// over all senders (the receiver's LDS stage bound), out[1 ..] the world headers, then the record
+// counts M[q][r] (sender q -> rank r); xb[q] = sender q's slice in this rank's received records
+// (own records are not received), xb[world + q] = the packets of the senders before q
+__global__ __launch_bounds__(256) void xs_mat(const uint64_t* __restrict__ rows, size_t row_words, const uint32_t* __restrict__ sc,
+                                              uint32_t n_bins, uint32_t world, uint32_t me, uint32_t bpr,
+                                              uint64_t* __restrict__ out, uint32_t* __restrict__ xb) {
+    __shared__ uint32_t s_max;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) s_max = 0;
+    __syncthreads();
+    uint32_t mx = 0;
+    for (uint32_t b = t; b < n_bins; b += 256) {
+        uint32_t tot = 0;
+        for (uint32_t q = 0; q < world; ++q) tot += reinterpret_cast<const uint32_t*>(rows + (size_t)q * row_words + kXsHead)[b];
+        mx = max(mx, tot);
+    }
+    atomicMax(&s_max, mx);
+    for (uint32_t i = t; i < world * kXsHead; i += 256) out[1 + i] = rows[(size_t)(i / kXsHead) * row_words + i % kXsHead];
+    uint64_t* M = out + 1 + (size_t)world * kXsHead;
+    for (uint32_t i = t; i < world * world; i += 256) {
+        const uint32_t q = i / world, r = i % world;
+        const uint32_t* sq = sc + (size_t)q * (n_bins + 1);
+        M[i] = sq[min(r * bpr + bpr, n_bins)] - sq[min(r * bpr, n_bins)];
+    }
+    if (t == 0) {
+        uint32_t rb = 0;
+        uint64_t pb = 0;
+        for (uint32_t q = 0; q < world; ++q) {
+            const uint32_t* sq = sc + (size_t)q * (n_bins + 1);
+            xb[q] = rb;
+            if (q != me) rb += sq[min(me * bpr + bpr, n_bins)] - sq[min(me * bpr, n_bins)];
+            xb[world + q] = (uint32_t)pb;
+            pb += rows[(size_t)q * row_words + 6];
+        }
+    }
+    __syncthreads();
+    if (t == 0) out[0] = s_max;
+}
+
 // sharded rounds' buffers that depend only on the host count and the ranks (shd_relay_setup)
 static shd_status relay_shard_alloc(shd_ctx* ctx) {
     RelayState& R = ctx->relay;
@@ -2306,7 +2543,14 @@ static shd_status relay_shard_alloc(shd_ctx* ctx) {
     uint32_t own_lo = 0, own_hi = 0;
     shard_range(H, (int)world, ctx->comm->rank, &own_lo, &own_hi);
     const size_t n_own = own_hi - own_lo;
-    SHD_TRY(R.x_words.ensure((size_t)world * (kXHead + world) * 8 + (size_t)world * 8 + 64));
+    const XShard xsh = xshard(H, world);
+    const size_t rw = std::max<size_t>(xs_row_words(xsh.n_bins), kXHead + world);
+    SHD_TRY(R.x_words.ensure((size_t)world * rw * 8 + (size_t)world * 8 + 64));
+    SHD_TRY(R.xs_sc.ensure((size_t)world * (xsh.n_bins + 1) * 4));
+    const size_t out_bytes = (1 + (size_t)world * kXsHead + (size_t)world * world) * 8 + 64;
+    SHD_TRY(R.xs_out.ensure(out_bytes));
+    SHD_TRY(R.xs_pin.ensure(out_bytes));
+    SHD_TRY(R.xs_b.ensure((size_t)world * 8 + 64));
     SHD_TRY(R.x_off.ensure(((size_t)H + world) * 4));
     SHD_TRY(R.x_roff.ensure((size_t)world * (n_own + 1) * 4 + (size_t)(world + 1) * 4));
     SHD_TRY(R.m_off.ensure((n_own + 1) * 4));
@@ -2327,8 +2571,8 @@ static shd_status relay_recv_grow(RelayState& R, uint64_t n) {
     return SHD_OK;
 }
 
-static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
-                                      shd_relay_out* d_out) {
+static shd_status relay_round_sharded_x24(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                                          shd_relay_out* d_out) {
     RelayState& R = ctx->relay;
     Comm& C = *ctx->comm;
     hipStream_t s = ctx->stream;
@@ -2456,6 +2700,163 @@ static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const sh
     round_note(ctx, md, ml);
     R.last_recv = n_recv;
     return SHD_OK;
+}
+
+
+// One sharded round without the merge (see xs_row above).  *fallback = true (the same on every
+// rank: the decision reads only the gathered rows) when any rank cannot take this path -- not
+// pipeline 7, a bin over its LDS stage or an 8-bit slot counter, a deliver offset or event ids
+// past 32 bits, more than 2^24 packets over all ranks -- and the caller then runs the packing
+// path (relay_round_sharded_x24), which reruns the round from the uncommitted state.
+static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
+                                         shd_relay_out* d_out, bool* fallback) {
+    RelayState& R = ctx->relay;
+    Comm& C = *ctx->comm;
+    hipStream_t s = ctx->stream;
+    const uint32_t H = R.n_hosts, world = (uint32_t)C.size, me = (uint32_t)C.rank;
+    const uint64_t n = b->n_packets;
+    const XShard xsh = xshard(H, world);
+    const uint32_t n_bins = xsh.n_bins;
+    const size_t rw = xs_row_words(n_bins);
+    *fallback = false;
+    // 1. the local pipeline up to the stamp (records left in their bins); a failure is this
+    //    rank's status in its sizing row, not a return
+    const bool ok7 = world <= 64 && R.n_src > 0 && R.table_narrow && !R.force_v1 && relay_v7_ok(ctx, n, n_bins);
+    const bool abs_seq = R.seq_bound + n < (1ull << 32);
+    shd_status st = SHD_OK;
+    shd_relay_out lo{};
+    lo.status = d_out->status;
+    bool ran = false;
+    if (ok7 && abs_seq) {
+        const uint64_t nn = (uint64_t)R.n_nodes * R.n_nodes;   // the round's counter increments start at 0
+        if (R.red.ensure(64) != SHD_OK || (R.count_on && R.counts_round.ensure(nn * 8) != SHD_OK))
+            st = SHD_ERR_NOMEM;
+        else if (R.count_on && hipMemsetAsync(R.counts_round.p, 0, nn * 8, s) != hipSuccess)
+            st = SHD_ERR_HIP;
+        if (st == SHD_OK) st = relay_device_v7(ctx, b, rd, &lo, &xsh);
+        ran = st == SHD_OK;
+    }
+    uint64_t* rows = R.x_words.as<uint64_t>();
+    uint64_t* agree = rows + (size_t)world * rw;
+    xs_row<<<1, 256, 0, s>>>(ran ? R.red.as<unsigned long long>() : nullptr,
+                             ran ? R.bin_base.as<uint32_t>() + n_bins + 1 : nullptr, n_bins, ran ? 1u : 0u,
+                             (int32_t)st, R.x_cap, n, (ok7 && abs_seq) ? 0u : kXsHost, (int32_t)SHD_ERR_NO_HOST,
+                             (int32_t)SHD_ERR_INVALID, rows + (size_t)me * rw);
+    if (hipGetLastError() != hipSuccess && st == SHD_OK) st = SHD_ERR_HIP;   // (rides in no row: the collective must run)
+    SHD_TRY(C.all_gather(rows + (size_t)me * rw, rows, rw * 8, s));   // agreed (LocalComm) / fatal (RCCL)
+    // 2. the sizing summary, one host sync
+    uint32_t* xb = R.xs_b.as<uint32_t>();
+    xs_scan<<<world, 1024, 0, s>>>(rows, rw, n_bins, R.xs_sc.as<uint32_t>());
+    xs_mat<<<1, 256, 0, s>>>(rows, rw, R.xs_sc.as<uint32_t>(), n_bins, world, me, xsh.bpr, R.xs_out.as<uint64_t>(), xb);
+    const size_t out_words = 1 + (size_t)world * kXsHead + (size_t)world * world;
+    SHD_HIP(hipMemcpyAsync(R.xs_pin.p, R.xs_out.p, out_words * 8, hipMemcpyDeviceToHost, s));
+    SHD_TRY(wait_stream(ctx, s));
+    if (st != SHD_OK) return st;   // (a launch failure after the gather: local, no collective follows)
+    const uint64_t* pin = R.xs_pin.as<uint64_t>();
+    auto hdr = [&](uint32_t q) { return pin + 1 + (size_t)q * kXsHead; };
+    auto M = [&](uint32_t q, uint32_t r) { return pin[1 + (size_t)world * kXsHead + (size_t)q * world + r]; };
+    for (uint32_t q = 0; q < world; ++q)
+        if ((shd_status)hdr(q)[0] != SHD_OK) return (shd_status)hdr(q)[0];   // the lowest failing rank's
+    uint64_t pk = 0;
+    bool fb = pin[0] > kB7Cap;
+    for (uint32_t q = 0; q < world; ++q) {
+        fb = fb || hdr(q)[5] != 0;
+        pk += hdr(q)[6];
+    }
+    if (fb || pk >= kV7MaxPackets) {
+        *fallback = true;
+        return SHD_OK;
+    }
+    uint64_t md = ~0ull, ml = ~0ull, ns = 0;
+    for (uint32_t q = 0; q < world; ++q) {
+        md = std::min<uint64_t>(md, hdr(q)[1]);
+        ml = std::min<uint64_t>(ml, hdr(q)[2]);
+        ns += hdr(q)[3];
+    }
+    // receive capacity (records, and the events they hold): whether any rank grows is known to all
+    bool grow = false;
+    uint64_t n_recv = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+        uint64_t t = 0;
+        for (uint32_t q = 0; q < world; ++q) t += M(q, r);
+        grow = grow || t > hdr(r)[4];
+        if (r == me) n_recv = t;
+    }
+    if (grow) {   // every rank takes this branch: one more agreement, on the growth's outcome
+        shd_status gs = n_recv > R.x_cap ? relay_recv_grow(R, n_recv) : SHD_OK;
+        ctx->h_pin[44] = (uint64_t)gs;
+        if (hipMemcpyAsync(agree + me, ctx->h_pin + 44, 8, hipMemcpyHostToDevice, s) != hipSuccess && gs == SHD_OK)
+            gs = SHD_ERR_HIP;   // (the row still goes out: the peers wait for it)
+        SHD_TRY(C.all_gather(agree + me, agree, 8, s));
+        std::vector<uint64_t> a(world);
+        SHD_HIP(hipMemcpyAsync(a.data(), agree, world * 8, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipStreamSynchronize(s));
+        for (uint32_t q = 0; q < world; ++q)
+            if ((shd_status)a[q] != SHD_OK) return (shd_status)a[q];
+        if (gs != SHD_OK) return gs;
+    }
+    // 3. the exchange: the records of rank r's bins, as the stamp laid them out (own: none)
+    std::vector<const void*> sp(world);
+    std::vector<void*> rp(world);
+    std::vector<size_t> sb(world), rb(world);
+    uint64_t sent_before = 0, recv_before = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+        sp[r] = R.rec.as<uint4>() + sent_before;
+        sb[r] = r == me ? 0 : (size_t)M(me, r) * 16;
+        sent_before += M(me, r);
+        rp[r] = R.x_rrec.as<uint4>() + recv_before;
+        rb[r] = r == me ? 0 : (size_t)M(r, me) * 16;
+        if (r != me) recv_before += M(r, me);
+    }
+    SHD_TRY(C.exchange(1, sp.data(), sb.data(), rp.data(), rb.data(), s));   // agreed (LocalComm) / fatal (RCCL)
+    // 4. the bin sort of this rank's bins over every sender's records (no collective follows)
+    uint32_t own_lo = 0, own_hi = 0;
+    shard_range(H, (int)world, (int)me, &own_lo, &own_hi);
+    const uint32_t n_own = own_hi - own_lo;
+    const uint32_t fb_me = xsh.first_bin(me), nb = xsh.first_bin(me + 1) - fb_me;
+    if (nb) {
+        V7Out vo{R.m_deliver.as<uint64_t>(), R.m_src.as<uint32_t>(), R.m_seq.as<uint64_t>(), R.m_pkt.as<uint32_t>(),
+                 nullptr, rd->round_end};
+        uint32_t kq = 0;
+        while ((kq ? 2 * kq : 1u) < world) kq = kq ? 2 * kq : 1u;
+        XSrc xs{world, me, fb_me, n_bins + 1, kq, R.xs_sc.as<uint32_t>(), xb, xb + world, R.rec.as<uint4>()};
+        bin_sort_v7<true><<<nb, kB7Threads, 0, s>>>(n_own, nb, nullptr, R.x_rrec.as<uint4>(),
+                                                    R.bin_lb.as<unsigned long long>(), R.m_off.as<uint32_t>(), vo,
+                                                    nullptr, 0u, xs);
+    } else {
+        SHD_HIP(hipMemsetAsync(R.m_off.p, 0, 4, s));
+    }
+    SHD_HIP(hipGetLastError());
+    R.red_host[0] = hdr(me)[1];
+    R.red_host[1] = hdr(me)[2];
+    R.red_host[2] = hdr(me)[3];
+    R.last_pipe = 8;   // pipeline 7's stamp, its bins exchanged and sorted by their destination ranks
+    R.last_v2 = true;
+    SHD_TRY(relay_commit(ctx, &lo));
+    // 5. the number of events this rank received (= its destinations' sent events)
+    SHD_HIP(hipMemcpyAsync(R.xs_pin.p, R.m_off.as<uint32_t>() + n_own, 4, hipMemcpyDeviceToHost, s));
+    SHD_TRY(wait_stream(ctx, s));
+    const uint32_t n_ev = *R.xs_pin.as<uint32_t>();
+    d_out->ev_off = R.m_off.as<uint32_t>();
+    d_out->ev_deliver = R.m_deliver.as<uint64_t>();
+    d_out->ev_src = R.m_src.as<uint32_t>();
+    d_out->ev_seq = R.m_seq.as<uint64_t>();
+    d_out->ev_pkt = R.m_pkt.as<uint32_t>();
+    d_out->min_deliver = md;
+    d_out->min_latency = ml;
+    d_out->n_sent = ns;
+    d_out->n_dst = n_own;
+    d_out->n_events = n_ev;
+    round_note(ctx, md, ml);
+    R.last_recv = n_ev;
+    return SHD_OK;
+}
+
+static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const shd_round* rd, shd_relay_out* d_out) {
+    if (ctx->knobs.on(K_RELAY_SHARD_X24)) return relay_round_sharded_x24(ctx, b, rd, d_out);
+    bool fallback = false;
+    SHD_TRY(relay_round_sharded_v7(ctx, b, rd, d_out, &fallback));
+    return fallback ? relay_round_sharded_x24(ctx, b, rd, d_out) : SHD_OK;
 }
 
 }  // namespace shd

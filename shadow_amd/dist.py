@@ -179,6 +179,13 @@ class ShardedRelay:
         status = d_status.cpu().numpy()[: len(send_time)].copy()
         return status, ev, out.min_deliver, out.min_latency, out.n_sent
 
+    def last_pipeline(self) -> int:
+        """8: the bins went to their destination ranks as stamped (relay_round_sharded_v7); else the
+        packing path ran on the local pipeline 7, 3 or 1."""
+        p = C.c_int32(0)
+        N.check(self.eng.lib.shd_relay_last_pipeline(self.eng.ctx, C.byref(p)), "shd_relay_last_pipeline")
+        return p.value
+
     def host_state(self):
         rng = np.zeros((self.n_hosts, 4), np.uint64)
         nid = np.zeros(self.n_hosts, np.uint64)

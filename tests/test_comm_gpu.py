@@ -64,7 +64,11 @@ def _check_rank(rank_out, o, lo, hi, a_of, b):
     assert (md, ml, ns) == (o["min_deliver"], o["min_latency"], o["n_sent"])
 
 
-def test_local_two_ranks_relay_rounds(engine):
+@pytest.mark.parametrize("path", ["bins", "x24"])
+def test_local_two_ranks_relay_rounds(engine, knob, path):
+    """Three rounds on two ranks, both exchange forms: the stamp's bins sent to their destination
+    ranks and sorted there (default, pipeline 8), and the packed 24-byte events merged per
+    destination (RELAY_SHARD_X24, the fallback form)."""
     from shadow_amd import dist as D
     from shadow_amd import synth
     from shadow_amd.routing import Engine
@@ -72,6 +76,8 @@ def test_local_two_ranks_relay_rounds(engine):
     _, lat, loss, host_node, rng0 = _case(H, NN, 3)
     engines = [Engine(0), Engine(0)]
     try:
+        for e in engines:
+            knob("RELAY_SHARD_X24", 1 if path == "x24" else 0, eng=e)
         D.comm_init_local(engines)
         rels = [D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss) for e in engines]
         assert [(r.lo, r.hi) for r in rels] == [(0, 2500), (2500, 5000)]
@@ -84,6 +90,7 @@ def test_local_two_ranks_relay_rounds(engine):
             rd = (start + ra, start + 10**12, start + ra // 2 if rnd == 0 else 0)
             parts = [_slice_batch(b, r.lo, r.hi) for r in rels]
             outs = _run_ranks([lambda r=r, p=p: r.round(*p[:4], rd) for r, p in zip(rels, parts)])
+            assert [r.last_pipeline() for r in rels] == ([8, 8] if path == "bins" else [7, 7])
             bases = np.array([p[4] for p in parts], np.int64)
 
             def a_of(src):

@@ -195,6 +195,7 @@ def test_probe_batch_two_ranks(engine, same_instant):
                                  np.diff(b.src_off.astype(np.int64)))
             assert br["pf_rows_max"] >= 3, br
         outs = _run_ranks([lambda r=r, p=p: r.round(*p[:4], rd) for r, p in zip(rels, parts)])
+        assert [r.last_pipeline() for r in rels] == [8, 8]   # the bins went to their ranks as stamped
         bases = np.array([p[4] for p in parts], np.int64)
         split = rels[1].lo
 

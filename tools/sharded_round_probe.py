@@ -42,6 +42,8 @@ def main():
     e1 = Engine(0)
     D.comm_init_local([e1])
     one = D.ShardedRelay(e1, host_node, rng0, np.zeros(H, np.uint64), lat, loss)
+    counters = int(os.environ.get("PROBE_COUNTERS", "0"))   # the bench's relay leg runs without them
+    N.check(e1.lib.shd_relay_set_counters(e1.ctx, counters), "set_counters")
     d1 = [dev(b.src_off, np.int32), dev(b.send_time, np.int64), dev(b.dst_host, np.int32), dev(b.payload, np.int32)]
     st1 = torch.empty(P, dtype=torch.uint8, device="cuda")
     t_one = []
@@ -52,12 +54,15 @@ def main():
         one.round_device(*d1, (start + (k + 2) * 10**6, start + 10**12, 0), st1)
         if k >= 2:
             t_one.append((time.perf_counter() - t0) * 1e3)
+    p1 = one.last_pipeline()
     e1.close()
 
     # ---- two in-process ranks on the same GPU, each its half of the sources
     engines = [Engine(0), Engine(0)]
     D.comm_init_local(engines)
     rels = [D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss) for e in engines]
+    for e in engines:
+        N.check(e.lib.shd_relay_set_counters(e.ctx, counters), "set_counters")
     parts = []
     for r in rels:
         a, z = int(b.src_off[r.lo]), int(b.src_off[r.hi])
@@ -79,11 +84,13 @@ def main():
             t.join()
         if k >= 2:
             t_two.append((time.perf_counter() - t0) * 1e3)
+    p2 = [r.last_pipeline() for r in rels]
     for e in engines:
         e.close()
     m1, m2 = statistics.median(t_one), statistics.median(t_two)
     print(f"one context (world 1), whole C5 round: {m1:.3f} ms; two in-process ranks on the same GPU (halves + "
-          f"exchange + merge): {m2:.3f} ms; sharded-path overhead {m2 - m1:.3f} ms per round", flush=True)
+          f"exchange + merge): {m2:.3f} ms; sharded-path overhead {m2 - m1:.3f} ms per round; pipelines "
+          f"{p1} / {p2} (SHD_RELAY_SHARD_X24={os.environ.get('SHD_RELAY_SHARD_X24', '')})", flush=True)
 
 
 if __name__ == "__main__":
