@@ -68,14 +68,18 @@ shd_status readback_launch(hipStream_t s, const void* d_src, uint32_t n_words, u
 // (rounds.hip readback_mark), or -- SHD_SYNC_KERNEL=0 -- a D2H copy followed by wait_stream's marker
 // copy.  A wait past 20 ms falls back to hipStreamSynchronize, which also reports a failed kernel.
 shd_status readback(shd_ctx* ctx, hipStream_t s, int at, const void* d_src, size_t n_bytes) {
+    return readback_into(ctx, s, d_src, n_bytes, ctx->h_pin + at);
+}
+
+// readback into any coherent pinned host words (PinBuf)
+shd_status readback_into(shd_ctx* ctx, hipStream_t s, const void* d_src, size_t n_bytes, unsigned long long* h_dst) {
     if (!ctx->spin_wait || ctx->knobs.get(K_SYNC_KERNEL, 1) == 0) {
-        SHD_HIP(hipMemcpyAsync(ctx->h_pin + at, d_src, n_bytes, hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipMemcpyAsync(h_dst, d_src, n_bytes, hipMemcpyDeviceToHost, s));
         return wait_stream(ctx, s);
     }
     volatile unsigned long long* done = ctx->h_pin + kPinMarker;
     *done = 0;
-    SHD_TRY(readback_launch(s, d_src, (uint32_t)(n_bytes / 8), ctx->h_pin + at,
-                            const_cast<unsigned long long*>(done)));
+    SHD_TRY(readback_launch(s, d_src, (uint32_t)(n_bytes / 8), h_dst, const_cast<unsigned long long*>(done)));
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 1; *done != 1; ++i) {
         __builtin_ia32_pause();

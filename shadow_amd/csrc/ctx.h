@@ -43,7 +43,7 @@ struct DevBuf {
     }
 };
 
-struct PinBuf {   // grow-only pinned host memory
+struct PinBuf {   // grow-only coherent pinned host memory (a kernel's stores reach the host: readback_into)
     void* p = nullptr;
     size_t bytes = 0;
     PinBuf() = default;
@@ -55,7 +55,7 @@ struct PinBuf {   // grow-only pinned host memory
         if (p) (void)hipHostFree(p);
         p = nullptr;
         bytes = 0;
-        if (hipHostMalloc(&p, need, hipHostMallocDefault) != hipSuccess) return SHD_ERR_NOMEM;
+        if (hipHostMalloc(&p, need, hipHostMallocCoherent) != hipSuccess) return SHD_ERR_NOMEM;
         bytes = need;
         return SHD_OK;
     }
@@ -212,6 +212,8 @@ constexpr int kPinMarker = 80;
 shd_status wait_stream(shd_ctx* ctx, hipStream_t s);
 // n_bytes of device words into h_pin[at ...] and wait for the stream (api.cpp)
 shd_status readback(shd_ctx* ctx, hipStream_t s, int at, const void* d_src, size_t n_bytes);
+// the same into coherent pinned words of the caller's (PinBuf; n_bytes a multiple of 8, 8-aligned)
+shd_status readback_into(shd_ctx* ctx, hipStream_t s, const void* d_src, size_t n_bytes, unsigned long long* h_dst);
 // a committed relay round's (all-rank) reductions: the runahead update (runahead.rs:60-115) and
 // the earliest deliver time of the relay output that the queues have not merged yet (rounds.cpp)
 void round_note(shd_ctx* ctx, uint64_t min_deliver, uint64_t min_latency);

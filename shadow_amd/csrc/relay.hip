@@ -2749,8 +2749,7 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
     xs_scan<<<world, 1024, 0, s>>>(rows, rw, n_bins, R.xs_sc.as<uint32_t>());
     xs_mat<<<1, 256, 0, s>>>(rows, rw, R.xs_sc.as<uint32_t>(), n_bins, world, me, xsh.bpr, R.xs_out.as<uint64_t>(), xb);
     const size_t out_words = 1 + (size_t)world * kXsHead + (size_t)world * world;
-    SHD_HIP(hipMemcpyAsync(R.xs_pin.p, R.xs_out.p, out_words * 8, hipMemcpyDeviceToHost, s));
-    SHD_TRY(wait_stream(ctx, s));
+    SHD_TRY(readback_into(ctx, s, R.xs_out.p, out_words * 8, R.xs_pin.as<unsigned long long>()));
     if (st != SHD_OK) return st;   // (a launch failure after the gather: local, no collective follows)
     const uint64_t* pin = R.xs_pin.as<uint64_t>();
     auto hdr = [&](uint32_t q) { return pin + 1 + (size_t)q * kXsHead; };
@@ -2834,9 +2833,9 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
     R.last_v2 = true;
     SHD_TRY(relay_commit(ctx, &lo));
     // 5. the number of events this rank received (= its destinations' sent events)
-    SHD_HIP(hipMemcpyAsync(R.xs_pin.p, R.m_off.as<uint32_t>() + n_own, 4, hipMemcpyDeviceToHost, s));
-    SHD_TRY(wait_stream(ctx, s));
-    const uint32_t n_ev = *R.xs_pin.as<uint32_t>();
+    // (8 aligned bytes holding m_off[n_own]; m_off has room past its n_own + 1 words)
+    SHD_TRY(readback_into(ctx, s, R.m_off.as<uint32_t>() + (n_own & ~1u), 8, R.xs_pin.as<unsigned long long>()));
+    const uint32_t n_ev = R.xs_pin.as<uint32_t>()[n_own & 1u];
     d_out->ev_off = R.m_off.as<uint32_t>();
     d_out->ev_deliver = R.m_deliver.as<uint64_t>();
     d_out->ev_src = R.m_src.as<uint32_t>();
