@@ -298,6 +298,20 @@ shd_status shd_relay_round_device(shd_ctx* ctx, const shd_batch* d_batch, const 
  * Device RNG streams are not used (the draws are the CPU's); event ids, counters and the runahead
  * update as in shd_relay_round.  SHD_ERR_NO_HOST: a run's host or a destination is not a relay
  * host; SHD_ERR_INVALID: a host with two runs, or runs that do not cover a stage's records.
+ *
+ * Under a communicator of > 1 ranks (shd_relay_setup after it) every rank is handed the SAME
+ * stages -- every worker thread's buffer, holding hosts of every shard -- and keeps its own hosts
+ * [lo, hi) = shd_shard_range(n_hosts): the device groups every send (one pass, no CPU split), runs
+ * its own hosts' sends through shd_relay_round_sharded and returns
+ *   status2   every send in stage order: the own hosts' statuses, 0 for the other ranks' sends (an
+ *             OR of the ranks' arrays gives every status)
+ *   ev_off    [hi - lo + 1]; events: the own destinations' n_events events, seq_off relative to
+ *             the source host's first id of the round and send = the index in stage order, for
+ *             sources of any rank
+ *   seq_base  entries [lo, hi) only (the ranks may share one array)
+ *   min_deliver, min_latency, n_sent over all ranks.
+ * A failed check (NO_HOST / INVALID runs) returns before the round's collectives on every rank
+ * (they all see the same stages); a failure inside the round fails it on every rank.
  */
 #define SHD_SEND_PAYLOAD 0x80000000u
 typedef struct shd_send12 {
@@ -326,9 +340,11 @@ typedef struct shd_flush_out {
     uint32_t* ev_off;
     shd_event16* events;
     uint64_t* seq_base;
-    uint64_t min_deliver;   /* as shd_relay_out */
+    uint64_t min_deliver;   /* as shd_relay_out (under a communicator: over all ranks) */
     uint64_t min_latency;
     uint64_t n_sent;
+    uint64_t n_events;      /* events returned (= n_sent on one context; the own destinations' events
+                               under a communicator) */
 } shd_flush_out;
 
 shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_stages, uint64_t time_base,

@@ -171,6 +171,10 @@ struct RelayState {
     // staged runs and records as uploaded, the send permutation (grouped <-> stage order) and the
     // packed outputs
     bool cpu_draws = false;
+    // a sharded shd_relay_flush round: event ids leave the device relative to their source host's
+    // first id of the round (a receiver does not hold the other ranks' hosts' ids)
+    bool rel_ids = false;
+    DevBuf fl_goff;   // the flush's grouped offsets over every host (sharded: all ranks' hosts)
     DevBuf fl_runh, fl_runc, fl_runo, fl_hrun, fl_hcnt, fl_send, fl_perm, fl_inv, fl_st2, fl_ev16;
 };
 

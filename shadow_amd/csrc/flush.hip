@@ -24,8 +24,10 @@
 
 namespace shd {
 
-// relay.hip: the round (pipelines + checks + commit) on a grouped device batch
+// relay.hip: the round (pipelines + checks + commit) on a grouped device batch; the sharded
+// round on this rank's grouped sends
 shd_status relay_flush_round(shd_ctx* ctx, const shd_batch* b, const shd_round* rd, shd_relay_out* o);
+shd_status relay_flush_round_sharded(shd_ctx* ctx, const shd_batch* b, const shd_round* rd, shd_relay_out* o);
 
 struct Send12 {
     uint32_t time_off, dst, draw_hi;
@@ -58,41 +60,77 @@ __global__ __launch_bounds__(256) void fl_host_counts(uint32_t n_hosts, const ui
 }
 
 // one wave per host: its run's records into the grouped arrays the pipelines read, the permutation
-// both ways (grouped position <-> send index in stage order)
+// both ways (grouped position <-> send index in stage order).  Under a communicator every rank
+// groups every host's sends (the permutation covers all of them) but writes the arrays of its own
+// hosts [lo, hi) only, from position src_off[lo] on.
 __global__ __launch_bounds__(256) void fl_gather(uint32_t n_hosts, const uint32_t* __restrict__ hrun,
                                                  const uint32_t* __restrict__ run_off,
                                                  const uint32_t* __restrict__ src_off, const Send12* __restrict__ in,
                                                  uint64_t time_base, uint64_t* __restrict__ send_time,
                                                  uint32_t* __restrict__ dst_host, uint32_t* __restrict__ payload,
                                                  uint32_t* __restrict__ draws, uint32_t* __restrict__ perm,
-                                                 uint32_t* __restrict__ inv) {
+                                                 uint32_t* __restrict__ inv, uint32_t lo, uint32_t hi) {
     const uint32_t h = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (h >= n_hosts) return;
     const uint32_t r = hrun[h];
     if (!r) return;
     const uint32_t from = run_off[r - 1], to = src_off[h], cnt = src_off[h + 1] - to;
+    const bool own = h >= lo && h < hi;
+    const uint32_t base = src_off[lo];
     for (uint32_t k = lane; k < cnt; k += 64) {
-        const Send12 x = in[from + k];
         const uint32_t p = to + k;
-        send_time[p] = time_base + x.time_off;
-        dst_host[p] = x.dst & ~SHD_SEND_PAYLOAD;
-        payload[p] = x.dst >> 31;
-        draws[p] = x.draw_hi;
         perm[p] = from + k;
         inv[from + k] = p;
+        if (!own) continue;
+        const Send12 x = in[from + k];
+        const uint32_t q = p - base;
+        send_time[q] = time_base + x.time_off;
+        dst_host[q] = x.dst & ~SHD_SEND_PAYLOAD;
+        payload[q] = x.dst >> 31;
+        draws[q] = x.draw_hi;
     }
 }
 
-// 2-bit statuses in stage order: byte j holds sends 4j .. 4j+3 (send 4j + k in bits 2k, 2k+1)
+// a sharded flush: this rank's hosts' offsets from 0 (the batch of the sharded round), and its
+// grouped range [src_off[lo], src_off[hi]) in red[2], red[3] for the host
+__global__ __launch_bounds__(256) void fl_rebase(const uint32_t* __restrict__ goff, uint32_t lo, uint32_t n_own,
+                                                 uint32_t* __restrict__ off, unsigned long long* __restrict__ red) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k <= n_own) off[k] = goff[lo + k] - goff[lo];
+    if (k == 0) {
+        red[2] = goff[lo];
+        red[3] = goff[lo + n_own];
+    }
+}
+
+// 2-bit statuses in stage order: byte j holds sends 4j .. 4j+3 (send 4j + k in bits 2k, 2k+1);
+// sharded: the statuses of grouped positions [base, base + n_own) (this rank's hosts), 0 elsewhere
 __global__ __launch_bounds__(256) void fl_status2(uint64_t n, const uint32_t* __restrict__ inv,
-                                                  const uint8_t* __restrict__ st, uint8_t* __restrict__ out) {
+                                                  const uint8_t* __restrict__ st, uint8_t* __restrict__ out,
+                                                  uint32_t base, uint32_t n_own) {
     const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (j * 4 >= n) return;
     uint32_t v = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k)
-        if (j * 4 + k < n) v |= (uint32_t)(st[inv[j * 4 + k]] & 3u) << (2 * k);
+        if (j * 4 + k < n) {
+            const uint32_t p = inv[j * 4 + k] - base;
+            if (p < n_own) v |= (uint32_t)(st[p] & 3u) << (2 * k);
+        }
     out[j] = (uint8_t)v;
+}
+
+// 16-byte event records of a sharded flush: the ids are already relative (RelayState::rel_ids);
+// ev_pkt indexes its sender rank's grouped sends, which start at goff[first host of that rank]
+__global__ __launch_bounds__(256) void fl_events16x(uint64_t n, uint64_t round_end, const uint64_t* __restrict__ deliver,
+                                                    const uint32_t* __restrict__ src, const uint64_t* __restrict__ seq,
+                                                    const uint32_t* __restrict__ pkt, const uint32_t* __restrict__ goff,
+                                                    uint32_t per, const uint32_t* __restrict__ perm,
+                                                    uint4* __restrict__ out) {
+    const uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t s = src[e], first = (s / per) * per;
+    out[e] = make_uint4((uint32_t)(deliver[e] - round_end), s, (uint32_t)seq[e], perm[goff[first] + pkt[e]]);
 }
 
 // 16-byte event records (already grouped by destination in EventQueue order)
@@ -126,7 +164,8 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
                            const shd_round* round, shd_flush_out* out) {
     if (!ctx || !round || !out || (n_stages && !stages)) return SHD_ERR_INVALID;
     RelayState& R = ctx->relay;
-    if (!R.ready || R.sharded) return SHD_ERR_STATE;
+    if (!R.ready) return SHD_ERR_STATE;
+    if (R.sharded && (!R.x_words.p || !R.xs_pin.p)) return SHD_ERR_STATE;   // set up before the communicator
     // host-side shape checks (each stage's runs cover exactly its records)
     uint64_t n = 0, n_runs = 0;
     for (uint32_t k = 0; k < n_stages; ++k) {
@@ -166,6 +205,10 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
     SHD_TRY(R.ev_seq.ensure(nn * 8));
     SHD_TRY(R.ev_pkt.ensure(nn * 4));
     SHD_TRY(R.red.ensure(64));
+    SHD_TRY(R.fl_goff.ensure((size_t)(H + 1) * 4));
+    // under a communicator: this rank's hosts [lo, hi) (the stages hold every rank's hosts)
+    uint32_t lo = 0, hi = H;
+    if (R.sharded) shard_range(H, ctx->comm->size, ctx->comm->rank, &lo, &hi);
     // 1. the staging buffers, stage after stage (pinned host memory -- shd_host_alloc -- moves at
     //    the link's rate; pageable memory is staged by the runtime)
     {
@@ -195,19 +238,26 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
     }
     fl_host_counts<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(H, R.fl_hrun.as<uint32_t>(), R.fl_runc.as<uint32_t>(),
                                                                 R.fl_hcnt.as<uint32_t>());
-    SHD_TRY(scan_excl2(R.scan, R.fl_hcnt.as<uint32_t>(), R.pk_off.as<uint32_t>(), nullptr, nullptr, (uint64_t)H + 1, s));
+    uint32_t* goff = R.sharded ? R.fl_goff.as<uint32_t>() : R.pk_off.as<uint32_t>();   // grouped offsets, all hosts
+    SHD_TRY(scan_excl2(R.scan, R.fl_hcnt.as<uint32_t>(), goff, nullptr, nullptr, (uint64_t)H + 1, s));
     if (n)
-        fl_gather<<<div_up(H, 4), 256, 0, s>>>(H, R.fl_hrun.as<uint32_t>(), R.fl_runo.as<uint32_t>(),
-                                                R.pk_off.as<uint32_t>(), R.fl_send.as<Send12>(), time_base,
-                                                R.pk_time.as<uint64_t>(), R.pk_dst.as<uint32_t>(),
-                                                R.pk_pay.as<uint32_t>(), R.draws.as<uint32_t>(),
-                                                R.fl_perm.as<uint32_t>(), R.fl_inv.as<uint32_t>());
+        fl_gather<<<div_up(H, 4), 256, 0, s>>>(H, R.fl_hrun.as<uint32_t>(), R.fl_runo.as<uint32_t>(), goff,
+                                                R.fl_send.as<Send12>(), time_base, R.pk_time.as<uint64_t>(),
+                                                R.pk_dst.as<uint32_t>(), R.pk_pay.as<uint32_t>(), R.draws.as<uint32_t>(),
+                                                R.fl_perm.as<uint32_t>(), R.fl_inv.as<uint32_t>(), lo, hi);
+    if (R.sharded)
+        fl_rebase<<<div_up((uint64_t)(hi - lo) + 1, 256), 256, 0, s>>>(goff, lo, hi - lo, R.pk_off.as<uint32_t>(), red);
     SHD_HIP(hipGetLastError());
-    SHD_TRY(readback(ctx, s, 32, red, 16));   // h_pin words 32-33
+    // h_pin words 32-35: the checks (and, sharded, this rank's grouped range).  Under a communicator a
+    // failed check is this rank's alone: the flush returns before the round's collectives, as a call
+    // with invalid arguments would, on whichever ranks see the bad runs (every rank sees the same
+    // stages, so all of them do).
+    SHD_TRY(readback(ctx, s, 32, red, R.sharded ? 32 : 16));
     if (ctx->h_pin[33] != ~0ull) return SHD_ERR_NO_HOST;   // a run of a host the relay does not have
     if (ctx->h_pin[32] != ~0ull) return SHD_ERR_INVALID;   // a host with two runs (two threads, or split)
+    const uint64_t base = R.sharded ? ctx->h_pin[34] : 0, n_own = R.sharded ? ctx->h_pin[35] - ctx->h_pin[34] : n;
     // 3. the round on the grouped batch with the CPU's draws (the device streams stay as they are)
-    shd_batch db{n, R.pk_off.as<uint32_t>(), R.pk_time.as<uint64_t>(), R.pk_dst.as<uint32_t>(),
+    shd_batch db{n_own, R.pk_off.as<uint32_t>(), R.pk_time.as<uint64_t>(), R.pk_dst.as<uint32_t>(),
                  R.pk_pay.as<uint32_t>(), nullptr};
     shd_relay_out dout{};
     dout.status = R.st.as<uint8_t>();
@@ -217,28 +267,39 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
     dout.ev_seq = R.ev_seq.as<uint64_t>();
     dout.ev_pkt = R.ev_pkt.as<uint32_t>();
     R.cpu_draws = true;
-    const shd_status st = relay_flush_round(ctx, &db, round, &dout);
+    R.rel_ids = R.sharded;
+    const shd_status st = R.sharded ? relay_flush_round_sharded(ctx, &db, round, &dout)
+                                    : relay_flush_round(ctx, &db, round, &dout);
     R.cpu_draws = false;
+    R.rel_ids = false;
     SHD_TRY(st);
-    // 4. compact outputs (the round committed: next_id2 holds every host's first id of the round)
-    const uint64_t ns = dout.n_sent;
+    // 4. compact outputs (the round committed: next_id2 holds every own host's first id of the round)
+    const uint64_t ns = dout.n_sent, n_ev = R.sharded ? dout.n_events : ns;
     const uint64_t* seq_base = R.next_id2.as<uint64_t>();
     if (n) fl_status2<<<div_up((n + 3) / 4, 256), 256, 0, s>>>(n, R.fl_inv.as<uint32_t>(), R.st.as<uint8_t>(),
-                                                              R.fl_st2.as<uint8_t>());
-    if (ns)
+                                                              R.fl_st2.as<uint8_t>(), (uint32_t)base, (uint32_t)n_own);
+    if (n_ev && R.sharded)
+        fl_events16x<<<div_up(n_ev, 256), 256, 0, s>>>(n_ev, round->round_end, dout.ev_deliver, dout.ev_src,
+                                                       dout.ev_seq, dout.ev_pkt, goff,
+                                                       (uint32_t)div_up((uint64_t)H, (uint64_t)ctx->comm->size),
+                                                       R.fl_perm.as<uint32_t>(), R.fl_ev16.as<uint4>());
+    else if (n_ev)
         fl_events16<<<div_up(ns, 256), 256, 0, s>>>(ns, round->round_end, R.ev_deliver.as<uint64_t>(),
                                                     R.ev_src.as<uint32_t>(), R.ev_seq.as<uint64_t>(),
                                                     R.ev_pkt.as<uint32_t>(), seq_base, R.fl_perm.as<uint32_t>(),
                                                     R.fl_ev16.as<uint4>());
     SHD_HIP(hipGetLastError());
     if (out->status2 && n) SHD_HIP(hipMemcpyAsync(out->status2, R.fl_st2.p, (n + 3) / 4, hipMemcpyDeviceToHost, s));
-    if (out->ev_off) SHD_HIP(hipMemcpyAsync(out->ev_off, R.ev_off.p, (size_t)(H + 1) * 4, hipMemcpyDeviceToHost, s));
-    if (out->events && ns) SHD_HIP(hipMemcpyAsync(out->events, R.fl_ev16.p, ns * 16, hipMemcpyDeviceToHost, s));
-    if (out->seq_base) SHD_HIP(hipMemcpyAsync(out->seq_base, seq_base, (size_t)H * 8, hipMemcpyDeviceToHost, s));
+    if (out->ev_off)
+        SHD_HIP(hipMemcpyAsync(out->ev_off, dout.ev_off, (size_t)(hi - lo + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (out->events && n_ev) SHD_HIP(hipMemcpyAsync(out->events, R.fl_ev16.p, n_ev * 16, hipMemcpyDeviceToHost, s));
+    if (out->seq_base && hi > lo)
+        SHD_HIP(hipMemcpyAsync(out->seq_base + lo, seq_base + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost, s));
     SHD_TRY(wait_stream(ctx, s));
     out->min_deliver = dout.min_deliver;
     out->min_latency = dout.min_latency;
     out->n_sent = ns;
+    out->n_events = n_ev;
     return SHD_OK;
 }
 

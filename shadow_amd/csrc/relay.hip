@@ -1896,7 +1896,8 @@ static RelayArgs3 relay_args3(shd_ctx* ctx, const shd_batch* b, const shd_round*
     a.sim_end = rd->sim_end;
     a.bootstrap_end = rd->bootstrap_end;
     // event ids below 2^32 for the whole round: records carry absolute ids, no per-event gather
-    a.abs_seq = R.seq_bound + n < (1ull << 32) ? 1u : 0u;
+    // (rel_ids: records keep the id relative to the host's first of the round)
+    a.abs_seq = !R.rel_ids && R.seq_bound + n < (1ull << 32) ? 1u : 0u;
     a.status = o->status;
     a.rec = R.rec.as<uint4>();
     a.key = R.ev_val.as<uint32_t>();
@@ -2190,11 +2191,14 @@ static_assert(sizeof(Ev24) == 24, "24-byte event record");
 // capacity (events) [5..7] spare, then [kXHead + r] = events for rank r
 constexpr uint32_t kXHead = 8;
 
+// rel (a sharded flush, RelayState::rel_ids): ids relative to the source host's first id of the
+// round, which only the sender holds
 __global__ __launch_bounds__(256) void pack_events24(uint64_t n, const uint64_t* __restrict__ t,
                                                      const uint64_t* __restrict__ q, const uint32_t* __restrict__ sv,
-                                                     const uint32_t* __restrict__ p, Ev24* __restrict__ out) {
+                                                     const uint32_t* __restrict__ p, const uint64_t* __restrict__ rel,
+                                                     Ev24* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) out[i] = Ev24{t[i], q[i], sv[i], p[i]};
+    if (i < n) out[i] = Ev24{t[i], rel ? q[i] - rel[sv[i]] : q[i], sv[i], p[i]};
 }
 
 __device__ __forceinline__ void shard_of(uint32_t total, uint32_t world, uint32_t r, uint32_t* lo, uint32_t* hi) {
@@ -2601,7 +2605,8 @@ static shd_status relay_round_sharded_x24(shd_ctx* ctx, const shd_batch* b, cons
     const uint64_t ns_local = st == SHD_OK ? R.red_host[2] : 0;
     if (st == SHD_OK && ns_local)
         pack_events24<<<div_up(ns_local, 256), 256, 0, s>>>(ns_local, lo.ev_deliver, lo.ev_seq, lo.ev_src,
-                                                            lo.ev_pkt, R.x_rec.as<Ev24>());
+                                                            lo.ev_pkt, R.rel_ids ? R.next_id.as<uint64_t>() : nullptr,
+                                                            R.x_rec.as<Ev24>());
     shard_words<<<1, 64, 0, s>>>(world, H, st == SHD_OK ? lo.ev_off : nullptr, (uint64_t)st,
                                  st == SHD_OK ? R.red_host[0] : ~0ull, st == SHD_OK ? R.red_host[1] : ~0ull,
                                  ns_local, R.x_cap, rows + (size_t)C.rank * WR);
@@ -2722,7 +2727,8 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
     // 1. the local pipeline up to the stamp (records left in their bins); a failure is this
     //    rank's status in its sizing row, not a return
     const bool ok7 = world <= 64 && R.n_src > 0 && R.table_narrow && !R.force_v1 && relay_v7_ok(ctx, n, n_bins);
-    const bool abs_seq = R.seq_bound + n < (1ull << 32);
+    // absolute ids must fit the records' 32 bits; relative ids (a sharded flush) always do
+    const bool abs_seq = R.rel_ids || R.seq_bound + n < (1ull << 32);
     shd_status st = SHD_OK;
     shd_relay_out lo{};
     lo.status = d_out->status;
@@ -2856,6 +2862,11 @@ static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const sh
     bool fallback = false;
     SHD_TRY(relay_round_sharded_v7(ctx, b, rd, d_out, &fallback));
     return fallback ? relay_round_sharded_x24(ctx, b, rd, d_out) : SHD_OK;
+}
+
+// shd_relay_flush under a communicator (flush.hip): this rank's grouped sends, the CPU's draws
+shd_status relay_flush_round_sharded(shd_ctx* ctx, const shd_batch* b, const shd_round* rd, shd_relay_out* o) {
+    return relay_round_sharded(ctx, b, rd, o);
 }
 
 }  // namespace shd

@@ -179,6 +179,29 @@ class ShardedRelay:
         status = d_status.cpu().numpy()[: len(send_time)].copy()
         return status, ev, out.min_deliver, out.min_latency, out.n_sent
 
+    def flush(self, run_host, run_count, sends, time_base: int, round_end: int, sim_end: int,
+              bootstrap_end: int = 0, pinned=None):
+        """``shd_relay_flush`` under the communicator: every rank passes the SAME stages (all worker
+        threads' buffers); this rank's result: statuses of its own hosts' sends in stage order (0
+        for the other ranks' sends), its destinations' events (ev_off over [lo, hi]), seq_base
+        entries [lo, hi), and the all-rank reductions."""
+        from .relay import FlushResult, PinnedStages
+        if pinned is None:
+            pinned = PinnedStages.wrap(run_host, run_count, sends)
+        n = pinned.n
+        st2 = np.zeros((n + 3) // 4, np.uint8)
+        ev_off = np.zeros(self.hi - self.lo + 1, np.uint32)
+        events = np.zeros((max(n, 1), 4), np.uint32)
+        seq_base = np.zeros(self.n_hosts, np.uint64)
+        out = N.FlushOut(N.ptr(st2).value, N.ptr(ev_off).value, N.ptr(events).value, N.ptr(seq_base).value,
+                         0, 0, 0, 0)
+        rd = N.Round(round_end, sim_end, bootstrap_end)
+        N.check(self.eng.lib.shd_relay_flush(self.eng.ctx, pinned.array, len(pinned.stages), int(time_base),
+                                             C.byref(rd), C.byref(out)), "shd_relay_flush")
+        status = ((st2[:, None] >> (np.arange(4, dtype=np.uint8) * 2)) & 3).reshape(-1)[:n]
+        return FlushResult(status, ev_off, events[:out.n_events], seq_base, out.min_deliver, out.min_latency,
+                           out.n_sent)
+
     def last_pipeline(self) -> int:
         """8: the bins went to their destination ranks as stamped (relay_round_sharded_v7); else the
         packing path ran on the local pipeline 7, 3 or 1."""

@@ -204,7 +204,7 @@ class Relay:
         ev_off = np.zeros(self.n_hosts + 1, np.uint32)
         events = np.zeros((max(n, 1), 4), np.uint32)
         seq_base = np.zeros(self.n_hosts, np.uint64)
-        out = N.FlushOut(N.ptr(st2).value, N.ptr(ev_off).value, N.ptr(events).value, N.ptr(seq_base).value, 0, 0, 0)
+        out = N.FlushOut(N.ptr(st2).value, N.ptr(ev_off).value, N.ptr(events).value, N.ptr(seq_base).value, 0, 0, 0, 0)
         rd = N.Round(round_end, sim_end, bootstrap_end)
         N.check(self.eng.lib.shd_relay_flush(self.eng.ctx, pinned.array, len(pinned.stages), int(time_base),
                                              C.byref(rd), C.byref(out)), "shd_relay_flush")

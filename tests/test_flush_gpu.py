@@ -130,3 +130,74 @@ def test_flush_rejects_bad_staging(engine):
                          10**9 + 10**6, 10**12, 0, chance=chance)
     fr = rl.flush(st.run_host, st.run_count, st.sends, *args)
     _check(fr, o, st, np.zeros(H, np.uint64), 10**9 + 10**6)
+
+
+@pytest.mark.parametrize("path", ["bins", "x24"])
+def test_flush_two_ranks_vs_c_oracle(engine, knob, path):
+    """shd_relay_flush under a two-rank communicator: both ranks get the same 16 stages (every
+    thread's buffer mixes both ranks' hosts); each keeps its own hosts' runs.  The OR of the ranks'
+    statuses, each rank's destinations' events (relative ids, sends in stage order) and the reduced
+    round outputs against the C restatement in CPU-chance mode, three rounds; both exchange forms."""
+    import threading
+
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd.routing import Engine
+    H, NN, P = 6000, 60, 400_000
+    lat, loss, host_node, rng0 = _case(H, NN, 13)
+    engines = [Engine(0), Engine(0)]
+    try:
+        for e in engines:
+            knob("RELAY_SHARD_X24", 1 if path == "x24" else 0, eng=e)
+        D.comm_init_local(engines)
+        rels = [D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss) for e in engines]
+        onid = np.zeros(H, np.uint64)
+        start, ra = 10**9, 10**6
+        for rnd in range(3):
+            b = synth.packet_batch(H, P, start, start + ra, seed=70 + rnd)
+            st = synth.stage_round(b, 16, start, seed=10 + rnd)
+            chance = (st.draw64 >> np.uint64(11)).astype(np.float64) * 2.0**-53
+            nid_before = onid.copy()
+            boot = start + ra // 2 if rnd == 0 else 0
+            o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(),
+                                 onid, start + ra, start + 100 * ra, boot, chance=chance)
+            res, errs = [None, None], []
+
+            def go(i):
+                try:
+                    res[i] = rels[i].flush(st.run_host, st.run_count, st.sends, start, start + ra, start + 100 * ra, boot)
+                except BaseException as ex:   # noqa: BLE001
+                    errs.append(ex)
+            ts = [threading.Thread(target=go, args=(i,)) for i in range(2)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join(timeout=300)
+            assert not errs, errs
+            assert [r.last_pipeline() for r in rels] == ([8, 8] if path == "bins" else [7, 7])
+            inv = np.empty(len(st.stage_of_send), np.int64)
+            inv[st.stage_of_send] = np.arange(len(st.stage_of_send))
+            assert np.array_equal(res[0].status | res[1].status, o["status"][st.stage_of_send])
+            seq_base = np.zeros(H, np.uint64)
+            for r, fr in zip(rels, res):
+                seq_base[r.lo:r.hi] = fr.seq_base[r.lo:r.hi]
+            assert np.array_equal(seq_base, nid_before)
+            ev = o["events"]
+            for r, fr in zip(rels, res):
+                s0, s1 = int(ev["off"][r.lo]), int(ev["off"][r.hi])
+                assert np.array_equal(fr.ev_off, (ev["off"][r.lo:r.hi + 1] - ev["off"][r.lo]).astype(np.uint32))
+                e = fr.events
+                assert len(e) == s1 - s0
+                assert np.array_equal(e[:, 0].astype(np.uint64), ev["deliver"][s0:s1] - np.uint64(start + ra))
+                assert np.array_equal(e[:, 1], ev["src"][s0:s1])
+                assert np.array_equal(e[:, 2].astype(np.uint64) + seq_base[e[:, 1]], ev["seq"][s0:s1])
+                assert np.array_equal(e[:, 3].astype(np.int64), inv[ev["pkt"][s0:s1].astype(np.int64)])
+                assert (fr.min_deliver, fr.min_latency, fr.n_sent) == (o["min_deliver"], o["min_latency"], o["n_sent"])
+            start += ra
+        for r in rels:
+            rng, nid = r.host_state()
+            assert np.array_equal(rng[r.lo:r.hi], rng0[r.lo:r.hi])   # the CPU drew
+            assert np.array_equal(nid[r.lo:r.hi], onid[r.lo:r.hi])
+    finally:
+        for e in engines:
+            e.close()
