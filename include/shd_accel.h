@@ -335,16 +335,25 @@ typedef struct shd_event16 {
     uint32_t send;          /* the send's index in stage order */
 } shd_event16;
 
+/* 12-byte form (shd_flush_out.event_bytes = 12): the source host is left out -- the caller's
+ * packet at index `send` already names it -- so 4 bytes less per event cross PCIe */
+typedef struct shd_event12 {
+    uint32_t deliver_off;
+    uint32_t seq_off;
+    uint32_t send;
+} shd_event12;
+
 typedef struct shd_flush_out {
     uint8_t* status2;
     uint32_t* ev_off;
-    shd_event16* events;
+    shd_event16* events;        /* shd_event12 records when event_bytes = 12 */
     uint64_t* seq_base;
     uint64_t min_deliver;   /* as shd_relay_out (under a communicator: over all ranks) */
     uint64_t min_latency;
     uint64_t n_sent;
     uint64_t n_events;      /* events returned (= n_sent on one context; the own destinations' events
                                under a communicator) */
+    uint32_t event_bytes;   /* in: 16 (or 0) = shd_event16 records, 12 = shd_event12 records */
 } shd_flush_out;
 
 shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_stages, uint64_t time_base,

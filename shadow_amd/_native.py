@@ -101,7 +101,7 @@ class Stage(C.Structure):
 class FlushOut(C.Structure):
     _fields_ = [("status2", C.c_void_p), ("ev_off", C.c_void_p), ("events", C.c_void_p), ("seq_base", C.c_void_p),
                 ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64),
-                ("n_events", C.c_uint64)]
+                ("n_events", C.c_uint64), ("event_bytes", C.c_uint32)]
 
 
 SEND_PAYLOAD = 0x80000000

@@ -103,6 +103,20 @@ __global__ __launch_bounds__(256) void fl_rebase(const uint32_t* __restrict__ go
     }
 }
 
+// an event record: 16 bytes {deliver - round_end, src, seq_off, send}, or (shd_flush_out.event_bytes
+// = 12) 12 bytes without the source host, which the caller's packet (send index) already names
+__device__ __forceinline__ void fl_put_event(void* out, bool b12, uint64_t e, uint32_t d, uint32_t s, uint32_t q,
+                                             uint32_t send) {
+    if (b12) {
+        uint32_t* o = static_cast<uint32_t*>(out) + 3 * e;
+        o[0] = d;
+        o[1] = q;
+        o[2] = send;
+    } else {
+        static_cast<uint4*>(out)[e] = make_uint4(d, s, q, send);
+    }
+}
+
 // 2-bit statuses in stage order: byte j holds sends 4j .. 4j+3 (send 4j + k in bits 2k, 2k+1);
 // sharded: the statuses of grouped positions [base, base + n_own) (this rank's hosts), 0 elsewhere
 __global__ __launch_bounds__(256) void fl_status2(uint64_t n, const uint32_t* __restrict__ inv,
@@ -126,22 +140,22 @@ __global__ __launch_bounds__(256) void fl_events16x(uint64_t n, uint64_t round_e
                                                     const uint32_t* __restrict__ src, const uint64_t* __restrict__ seq,
                                                     const uint32_t* __restrict__ pkt, const uint32_t* __restrict__ goff,
                                                     uint32_t per, const uint32_t* __restrict__ perm,
-                                                    uint4* __restrict__ out) {
+                                                    void* __restrict__ out, uint32_t b12) {
     const uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= n) return;
     const uint32_t s = src[e], first = (s / per) * per;
-    out[e] = make_uint4((uint32_t)(deliver[e] - round_end), s, (uint32_t)seq[e], perm[goff[first] + pkt[e]]);
+    fl_put_event(out, b12 != 0, e, (uint32_t)(deliver[e] - round_end), s, (uint32_t)seq[e], perm[goff[first] + pkt[e]]);
 }
 
-// 16-byte event records (already grouped by destination in EventQueue order)
+// event records (already grouped by destination in EventQueue order)
 __global__ __launch_bounds__(256) void fl_events16(uint64_t n, uint64_t round_end, const uint64_t* __restrict__ deliver,
                                                    const uint32_t* __restrict__ src, const uint64_t* __restrict__ seq,
                                                    const uint32_t* __restrict__ pkt, const uint64_t* __restrict__ seq_base,
-                                                   const uint32_t* __restrict__ perm, uint4* __restrict__ out) {
+                                                   const uint32_t* __restrict__ perm, void* __restrict__ out, uint32_t b12) {
     const uint64_t e = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= n) return;
     const uint32_t s = src[e];
-    out[e] = make_uint4((uint32_t)(deliver[e] - round_end), s, (uint32_t)(seq[e] - seq_base[s]), perm[pkt[e]]);
+    fl_put_event(out, b12 != 0, e, (uint32_t)(deliver[e] - round_end), s, (uint32_t)(seq[e] - seq_base[s]), perm[pkt[e]]);
 }
 
 }  // namespace shd
@@ -163,6 +177,8 @@ void shd_host_free(void* p) {
 shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_stages, uint64_t time_base,
                            const shd_round* round, shd_flush_out* out) {
     if (!ctx || !round || !out || (n_stages && !stages)) return SHD_ERR_INVALID;
+    if (out->event_bytes != 0 && out->event_bytes != 12 && out->event_bytes != 16) return SHD_ERR_INVALID;
+    const uint32_t eb = out->event_bytes == 12 ? 12u : 16u;
     RelayState& R = ctx->relay;
     if (!R.ready) return SHD_ERR_STATE;
     if (R.sharded && (!R.x_words.p || !R.xs_pin.p)) return SHD_ERR_STATE;   // set up before the communicator
@@ -282,17 +298,17 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
         fl_events16x<<<div_up(n_ev, 256), 256, 0, s>>>(n_ev, round->round_end, dout.ev_deliver, dout.ev_src,
                                                        dout.ev_seq, dout.ev_pkt, goff,
                                                        (uint32_t)div_up((uint64_t)H, (uint64_t)ctx->comm->size),
-                                                       R.fl_perm.as<uint32_t>(), R.fl_ev16.as<uint4>());
+                                                       R.fl_perm.as<uint32_t>(), R.fl_ev16.p, eb == 12 ? 1u : 0u);
     else if (n_ev)
         fl_events16<<<div_up(ns, 256), 256, 0, s>>>(ns, round->round_end, R.ev_deliver.as<uint64_t>(),
                                                     R.ev_src.as<uint32_t>(), R.ev_seq.as<uint64_t>(),
                                                     R.ev_pkt.as<uint32_t>(), seq_base, R.fl_perm.as<uint32_t>(),
-                                                    R.fl_ev16.as<uint4>());
+                                                    R.fl_ev16.p, eb == 12 ? 1u : 0u);
     SHD_HIP(hipGetLastError());
     if (out->status2 && n) SHD_HIP(hipMemcpyAsync(out->status2, R.fl_st2.p, (n + 3) / 4, hipMemcpyDeviceToHost, s));
     if (out->ev_off)
         SHD_HIP(hipMemcpyAsync(out->ev_off, dout.ev_off, (size_t)(hi - lo + 1) * 4, hipMemcpyDeviceToHost, s));
-    if (out->events && n_ev) SHD_HIP(hipMemcpyAsync(out->events, R.fl_ev16.p, n_ev * 16, hipMemcpyDeviceToHost, s));
+    if (out->events && n_ev) SHD_HIP(hipMemcpyAsync(out->events, R.fl_ev16.p, n_ev * eb, hipMemcpyDeviceToHost, s));
     if (out->seq_base && hi > lo)
         SHD_HIP(hipMemcpyAsync(out->seq_base + lo, seq_base + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost, s));
     SHD_TRY(wait_stream(ctx, s));

@@ -192,7 +192,7 @@ class Relay:
         return out
 
     def flush(self, run_host, run_count, sends, time_base: int, round_end: int, sim_end: int,
-              bootstrap_end: int = 0, pinned=None) -> "FlushResult":
+              bootstrap_end: int = 0, pinned=None, event_bytes: int = 16) -> "FlushResult":
         """``shd_relay_flush``: the worker threads' staging buffers as they stand (per stage: the
         runs' hosts and counts and the (n, 3) u32 send records {time_off, dst | SEND_PAYLOAD,
         draw_hi}).  ``pinned``: a PinnedStages holding them in pinned memory (the drop-in's path);
@@ -202,9 +202,10 @@ class Relay:
         n = pinned.n
         st2 = np.zeros((n + 3) // 4, np.uint8)
         ev_off = np.zeros(self.n_hosts + 1, np.uint32)
-        events = np.zeros((max(n, 1), 4), np.uint32)
+        events = np.zeros((max(n, 1), event_bytes // 4), np.uint32)   # 12 bytes: no source host column
         seq_base = np.zeros(self.n_hosts, np.uint64)
-        out = N.FlushOut(N.ptr(st2).value, N.ptr(ev_off).value, N.ptr(events).value, N.ptr(seq_base).value, 0, 0, 0, 0)
+        out = N.FlushOut(N.ptr(st2).value, N.ptr(ev_off).value, N.ptr(events).value, N.ptr(seq_base).value, 0, 0, 0, 0,
+                         event_bytes)
         rd = N.Round(round_end, sim_end, bootstrap_end)
         N.check(self.eng.lib.shd_relay_flush(self.eng.ctx, pinned.array, len(pinned.stages), int(time_base),
                                              C.byref(rd), C.byref(out)), "shd_relay_flush")

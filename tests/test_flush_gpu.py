@@ -19,6 +19,12 @@ def _case(H, NN, seed):
     return lat, loss, synth.c5_host_nodes(H, NN), synth.host_rng_states(H, 1)
 
 
+def _host_of_send(st):
+    """The staging's own knowledge: the source host of every send in stage order."""
+    return np.concatenate([np.repeat(np.asarray(h, np.uint32), np.asarray(c, np.int64))
+                           for h, c in zip(st.run_host, st.run_count)])
+
+
 def _check(fr, o, st, nid_before, round_end):
     inv = np.empty(len(st.stage_of_send), np.int64)
     inv[st.stage_of_send] = np.arange(len(st.stage_of_send))
@@ -27,6 +33,8 @@ def _check(fr, o, st, nid_before, round_end):
     assert np.array_equal(fr.ev_off, ev["off"])
     assert fr.n_sent == o["n_sent"] == len(fr.events)
     e = fr.events
+    if e.shape[1] == 3:   # 12-byte events {deliver_off, seq_off, send}: the source from the send's run
+        e = np.stack([e[:, 0], _host_of_send(st)[e[:, 2]], e[:, 1], e[:, 2]], axis=1)
     assert np.array_equal(e[:, 0].astype(np.uint64), ev["deliver"] - np.uint64(round_end))
     assert np.array_equal(e[:, 1], ev["src"])
     assert np.array_equal(e[:, 2].astype(np.uint64) + fr.seq_base[e[:, 1]], ev["seq"])
@@ -35,9 +43,9 @@ def _check(fr, o, st, nid_before, round_end):
     assert (fr.min_deliver, fr.min_latency) == (o["min_deliver"], o["min_latency"])
 
 
-@pytest.mark.parametrize("n_threads", [1, 16])
-@pytest.mark.parametrize("pinned", [False, True])
-def test_flush_rounds_vs_c_oracle(engine, n_threads, pinned):
+@pytest.mark.parametrize("n_threads,pinned,event_bytes", [(1, False, 16), (16, False, 16), (1, True, 16),
+                                                         (16, True, 16), (16, True, 12)])
+def test_flush_rounds_vs_c_oracle(engine, n_threads, pinned, event_bytes):
     from shadow_amd import synth
     from shadow_amd.relay import PinnedStages, Relay
     H, NN, P = 20_000, 200, 1_000_000
@@ -55,7 +63,8 @@ def test_flush_rounds_vs_c_oracle(engine, n_threads, pinned):
                              onid, start + ra, start + 100 * ra, boot, chance=chance)
         ps = PinnedStages.pinned(engine.lib, st.run_host, st.run_count, st.sends) if pinned else None
         try:
-            fr = rl.flush(st.run_host, st.run_count, st.sends, start, start + ra, start + 100 * ra, boot, pinned=ps)
+            fr = rl.flush(st.run_host, st.run_count, st.sends, start, start + ra, start + 100 * ra, boot, pinned=ps,
+                          event_bytes=event_bytes)
         finally:
             if ps is not None:
                 ps.free()
