@@ -175,6 +175,13 @@ struct RelayState {
     // first id of the round (a receiver does not hold the other ranks' hosts' ids)
     bool rel_ids = false;
     DevBuf fl_goff;   // the flush's grouped offsets over every host (sharded: all ranks' hosts)
+    // a one-context flush round: pipeline 7's bin sort writes the compact event records here
+    // (fl_direct says it did; the other pipelines leave the arrays for fl_events16)
+    DevBuf fl_tab, fl_rstg;   // zero-copy staging: the stage table, each run's stage
+    PinBuf fl_tab_pin;
+    void* fl_ev_out = nullptr;
+    uint32_t fl_b12 = 0;
+    bool fl_direct = false;
     DevBuf fl_runh, fl_runc, fl_runo, fl_hrun, fl_hcnt, fl_send, fl_perm, fl_inv, fl_st2, fl_ev16;
 };
 

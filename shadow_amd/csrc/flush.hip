@@ -49,6 +49,42 @@ __global__ __launch_bounds__(256) void fl_runs(uint32_t n_runs, const uint32_t* 
     if (atomicExch(&hrun[h], r + 1) != 0) atomicMin(&red[0], (unsigned long long)h);
 }
 
+// Zero-copy staging: when every staging buffer is pinned host memory the device reads it where it
+// lies (a device view of the pinned pages) instead of one copy per buffer -- at C5 three copies per
+// worker thread, each with ~11 us of launch gap, plus the re-read of the uploaded sends.
+struct FlStage {
+    const uint32_t* rh;    // device views of the stage's run_host / run_count / sends
+    const uint32_t* rc;
+    const Send12* sd;
+    uint64_t send_base;    // the stage's first send in stage order
+    uint32_t run_base, n_runs;
+};
+
+// fl_runs on the staged runs themselves: each run's host and count (copied to the device arrays
+// the scans read) and its stage
+__global__ __launch_bounds__(256) void fl_runs_zc(uint32_t n_runs, const FlStage* __restrict__ st, uint32_t n_stages,
+                                                  uint32_t n_hosts, uint32_t* __restrict__ runh,
+                                                  uint32_t* __restrict__ runc, uint32_t* __restrict__ rstage,
+                                                  uint32_t* __restrict__ hrun, unsigned long long* __restrict__ red) {
+    const uint32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= n_runs) return;
+    uint32_t lo = 0, hi = n_stages;   // the last stage whose first run is <= r (stages without runs skipped)
+    while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (st[m].run_base <= r) lo = m; else hi = m;
+    }
+    while (lo + 1 < n_stages && (st[lo].n_runs == 0 || r - st[lo].run_base >= st[lo].n_runs)) ++lo;
+    const uint32_t i = r - st[lo].run_base, h = st[lo].rh[i];
+    runh[r] = h;
+    runc[r] = st[lo].rc[i];
+    rstage[r] = lo;
+    if (h >= n_hosts) {
+        atomicMin(&red[1], (unsigned long long)r);
+        return;
+    }
+    if (atomicExch(&hrun[h], r + 1) != 0) atomicMin(&red[0], (unsigned long long)h);
+}
+
 // per host: its send count (0 without a run); entry n_hosts is 0 so one scan gives src_off[0..H]
 __global__ __launch_bounds__(256) void fl_host_counts(uint32_t n_hosts, const uint32_t* __restrict__ hrun,
                                                       const uint32_t* __restrict__ run_count,
@@ -69,7 +105,8 @@ __global__ __launch_bounds__(256) void fl_gather(uint32_t n_hosts, const uint32_
                                                  uint64_t time_base, uint64_t* __restrict__ send_time,
                                                  uint32_t* __restrict__ dst_host, uint32_t* __restrict__ payload,
                                                  uint32_t* __restrict__ draws, uint32_t* __restrict__ perm,
-                                                 uint32_t* __restrict__ inv, uint32_t lo, uint32_t hi) {
+                                                 uint32_t* __restrict__ inv, uint32_t lo, uint32_t hi,
+                                                 const FlStage* __restrict__ st, const uint32_t* __restrict__ rstage) {
     const uint32_t h = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (h >= n_hosts) return;
     const uint32_t r = hrun[h];
@@ -77,12 +114,18 @@ __global__ __launch_bounds__(256) void fl_gather(uint32_t n_hosts, const uint32_
     const uint32_t from = run_off[r - 1], to = src_off[h], cnt = src_off[h + 1] - to;
     const bool own = h >= lo && h < hi;
     const uint32_t base = src_off[lo];
+    // the run's sends: in the uploaded copy, or (zero-copy) in its stage's pinned buffer
+    const Send12* rs = in + from;
+    if (st) {
+        const FlStage& S = st[rstage[r - 1]];
+        rs = S.sd + (from - S.send_base);
+    }
     for (uint32_t k = lane; k < cnt; k += 64) {
         const uint32_t p = to + k;
         perm[p] = from + k;
         inv[from + k] = p;
         if (!own) continue;
-        const Send12 x = in[from + k];
+        const Send12 x = rs[k];
         const uint32_t q = p - base;
         send_time[q] = time_base + x.time_off;
         dst_host[q] = x.dst & ~SHD_SEND_PAYLOAD;
@@ -158,6 +201,18 @@ __global__ __launch_bounds__(256) void fl_events16(uint64_t n, uint64_t round_en
     fl_put_event(out, b12 != 0, e, (uint32_t)(deliver[e] - round_end), s, (uint32_t)(seq[e] - seq_base[s]), perm[pkt[e]]);
 }
 
+// a device view of host memory p when it is pinned (hipHostMalloc / registered), else nullptr
+static const void* dev_view(const void* p) {
+    if (!p) return nullptr;
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();   // pageable memory: not an error of the call
+        return nullptr;
+    }
+    if (at.type != hipMemoryTypeHost || !at.devicePointer || !at.hostPointer) return nullptr;
+    return static_cast<const char*>(at.devicePointer) + (static_cast<const char*>(p) - static_cast<const char*>(at.hostPointer));
+}
+
 }  // namespace shd
 
 using namespace shd;
@@ -225,9 +280,36 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
     // under a communicator: this rank's hosts [lo, hi) (the stages hold every rank's hosts)
     uint32_t lo = 0, hi = H;
     if (R.sharded) shard_range(H, ctx->comm->size, ctx->comm->rank, &lo, &hi);
-    // 1. the staging buffers, stage after stage (pinned host memory -- shd_host_alloc -- moves at
-    //    the link's rate; pageable memory is staged by the runtime)
+    // 1. the staging buffers: read where they lie when all are pinned (zero-copy), else copied stage
+    //    after stage (pinned host memory -- shd_host_alloc -- moves at the link's rate; pageable
+    //    memory is staged by the runtime)
+    std::vector<FlStage> tab(n_stages);
+    bool zc = n_stages > 0 && !ctx->knobs.on(K_FLUSH_COPY);
     {
+        uint64_t at = 0;
+        uint32_t ar = 0;
+        for (uint32_t k = 0; k < n_stages && zc; ++k) {
+            const shd_stage& S = stages[k];
+            FlStage& T = tab[k];
+            T.rh = static_cast<const uint32_t*>(S.n_runs ? dev_view(S.run_host) : nullptr);
+            T.rc = static_cast<const uint32_t*>(S.n_runs ? dev_view(S.run_count) : nullptr);
+            T.sd = static_cast<const Send12*>(S.n_sends ? dev_view(S.sends) : nullptr);
+            if ((S.n_runs && (!T.rh || !T.rc)) || (S.n_sends && !T.sd)) zc = false;
+            T.send_base = at;
+            T.run_base = ar;
+            T.n_runs = S.n_runs;
+            at += S.n_sends;
+            ar += S.n_runs;
+        }
+    }
+    if (zc) {
+        SHD_TRY(R.fl_tab.ensure((size_t)n_stages * sizeof(FlStage)));
+        SHD_TRY(R.fl_tab_pin.ensure((size_t)n_stages * sizeof(FlStage)));
+        SHD_TRY(R.fl_rstg.ensure(nr * 4));
+        std::memcpy(R.fl_tab_pin.p, tab.data(), (size_t)n_stages * sizeof(FlStage));
+        SHD_HIP(hipMemcpyAsync(R.fl_tab.p, R.fl_tab_pin.p, (size_t)n_stages * sizeof(FlStage), hipMemcpyHostToDevice, s));
+    }
+    if (!zc) {
         uint64_t at = 0, ar = 0;
         for (uint32_t k = 0; k < n_stages; ++k) {
             const shd_stage& S = stages[k];
@@ -248,8 +330,13 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
     SHD_HIP(hipMemsetAsync(R.fl_hrun.p, 0, (size_t)(H + 1) * 4, s));
     SHD_HIP(hipMemsetAsync(red, 0xFF, 16, s));
     if (n_runs) {
-        fl_runs<<<div_up(n_runs, 256), 256, 0, s>>>((uint32_t)n_runs, R.fl_runh.as<uint32_t>(), H,
-                                                     R.fl_hrun.as<uint32_t>(), red);
+        if (zc)
+            fl_runs_zc<<<div_up(n_runs, 256), 256, 0, s>>>((uint32_t)n_runs, R.fl_tab.as<FlStage>(), n_stages, H,
+                                                            R.fl_runh.as<uint32_t>(), R.fl_runc.as<uint32_t>(),
+                                                            R.fl_rstg.as<uint32_t>(), R.fl_hrun.as<uint32_t>(), red);
+        else
+            fl_runs<<<div_up(n_runs, 256), 256, 0, s>>>((uint32_t)n_runs, R.fl_runh.as<uint32_t>(), H,
+                                                         R.fl_hrun.as<uint32_t>(), red);
         SHD_TRY(scan_excl2(R.scan, R.fl_runc.as<uint32_t>(), R.fl_runo.as<uint32_t>(), nullptr, nullptr, n_runs, s));
     }
     fl_host_counts<<<div_up((uint64_t)H + 1, 256), 256, 0, s>>>(H, R.fl_hrun.as<uint32_t>(), R.fl_runc.as<uint32_t>(),
@@ -260,7 +347,9 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
         fl_gather<<<div_up(H, 4), 256, 0, s>>>(H, R.fl_hrun.as<uint32_t>(), R.fl_runo.as<uint32_t>(), goff,
                                                 R.fl_send.as<Send12>(), time_base, R.pk_time.as<uint64_t>(),
                                                 R.pk_dst.as<uint32_t>(), R.pk_pay.as<uint32_t>(), R.draws.as<uint32_t>(),
-                                                R.fl_perm.as<uint32_t>(), R.fl_inv.as<uint32_t>(), lo, hi);
+                                                R.fl_perm.as<uint32_t>(), R.fl_inv.as<uint32_t>(), lo, hi,
+                                                zc ? R.fl_tab.as<FlStage>() : nullptr,
+                                                zc ? R.fl_rstg.as<uint32_t>() : nullptr);
     if (R.sharded)
         fl_rebase<<<div_up((uint64_t)(hi - lo) + 1, 256), 256, 0, s>>>(goff, lo, hi - lo, R.pk_off.as<uint32_t>(), red);
     SHD_HIP(hipGetLastError());
@@ -282,33 +371,48 @@ shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_sta
     dout.ev_src = R.ev_src.as<uint32_t>();
     dout.ev_seq = R.ev_seq.as<uint64_t>();
     dout.ev_pkt = R.ev_pkt.as<uint32_t>();
+    // zero-copy outputs: the events and the 2-bit statuses written by the kernels straight into the
+    // caller's pinned buffers, so no copy follows the round (the writes cross the link as they go)
+    const bool zo = !ctx->knobs.on(K_FLUSH_COPY);
+    void* ev_host = zo && out->events ? const_cast<void*>(dev_view(out->events)) : nullptr;
+    uint8_t* st2_host = zo && out->status2 ? static_cast<uint8_t*>(const_cast<void*>(dev_view(out->status2))) : nullptr;
+    void* ev_dst = ev_host ? ev_host : R.fl_ev16.p;
+    uint8_t* st2_dst = st2_host ? st2_host : R.fl_st2.as<uint8_t>();
     R.cpu_draws = true;
-    R.rel_ids = R.sharded;
+    R.rel_ids = true;   // records carry ids relative to the source's first of the round
+    R.fl_ev_out = R.sharded ? nullptr : ev_dst;
+    R.fl_b12 = eb == 12 ? 1u : 0u;
+    R.fl_direct = false;
     const shd_status st = R.sharded ? relay_flush_round_sharded(ctx, &db, round, &dout)
                                     : relay_flush_round(ctx, &db, round, &dout);
     R.cpu_draws = false;
     R.rel_ids = false;
+    R.fl_ev_out = nullptr;
+    const bool direct = R.fl_direct && R.last_pipe == 7;   // (a rerun on pipeline 3 / 1 wrote the arrays)
+    R.fl_direct = false;
     SHD_TRY(st);
     // 4. compact outputs (the round committed: next_id2 holds every own host's first id of the round)
     const uint64_t ns = dout.n_sent, n_ev = R.sharded ? dout.n_events : ns;
     const uint64_t* seq_base = R.next_id2.as<uint64_t>();
     if (n) fl_status2<<<div_up((n + 3) / 4, 256), 256, 0, s>>>(n, R.fl_inv.as<uint32_t>(), R.st.as<uint8_t>(),
-                                                              R.fl_st2.as<uint8_t>(), (uint32_t)base, (uint32_t)n_own);
+                                                              st2_dst, (uint32_t)base, (uint32_t)n_own);
     if (n_ev && R.sharded)
         fl_events16x<<<div_up(n_ev, 256), 256, 0, s>>>(n_ev, round->round_end, dout.ev_deliver, dout.ev_src,
                                                        dout.ev_seq, dout.ev_pkt, goff,
                                                        (uint32_t)div_up((uint64_t)H, (uint64_t)ctx->comm->size),
-                                                       R.fl_perm.as<uint32_t>(), R.fl_ev16.p, eb == 12 ? 1u : 0u);
-    else if (n_ev)
+                                                       R.fl_perm.as<uint32_t>(), ev_dst, eb == 12 ? 1u : 0u);
+    else if (n_ev && !direct)
         fl_events16<<<div_up(ns, 256), 256, 0, s>>>(ns, round->round_end, R.ev_deliver.as<uint64_t>(),
                                                     R.ev_src.as<uint32_t>(), R.ev_seq.as<uint64_t>(),
                                                     R.ev_pkt.as<uint32_t>(), seq_base, R.fl_perm.as<uint32_t>(),
-                                                    R.fl_ev16.p, eb == 12 ? 1u : 0u);
+                                                    ev_dst, eb == 12 ? 1u : 0u);
     SHD_HIP(hipGetLastError());
-    if (out->status2 && n) SHD_HIP(hipMemcpyAsync(out->status2, R.fl_st2.p, (n + 3) / 4, hipMemcpyDeviceToHost, s));
+    if (out->status2 && n && !st2_host)
+        SHD_HIP(hipMemcpyAsync(out->status2, R.fl_st2.p, (n + 3) / 4, hipMemcpyDeviceToHost, s));
     if (out->ev_off)
         SHD_HIP(hipMemcpyAsync(out->ev_off, dout.ev_off, (size_t)(hi - lo + 1) * 4, hipMemcpyDeviceToHost, s));
-    if (out->events && n_ev) SHD_HIP(hipMemcpyAsync(out->events, R.fl_ev16.p, n_ev * eb, hipMemcpyDeviceToHost, s));
+    if (out->events && n_ev && !ev_host)
+        SHD_HIP(hipMemcpyAsync(out->events, R.fl_ev16.p, n_ev * eb, hipMemcpyDeviceToHost, s));
     if (out->seq_base && hi > lo)
         SHD_HIP(hipMemcpyAsync(out->seq_base + lo, seq_base + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost, s));
     SHD_TRY(wait_stream(ctx, s));

@@ -1599,10 +1599,28 @@ struct V7Out {
     uint32_t* pkt;
     const uint64_t* seq_base;
     uint64_t round_end;
+    // a flush round (shd_relay_flush, one context): the compact event records instead of the
+    // arrays -- {deliver - round_end, src, id relative to the source's first of the round (the
+    // records hold relative ids then), send index in stage order = perm[packet]}, 16 or 12 bytes
+    void* fl_out = nullptr;
+    const uint32_t* fl_perm = nullptr;
+    uint32_t fl_b12 = 0;
 };
 
 __device__ __forceinline__ void v7_emit(const V7Out& o, size_t at, const uint4& r) {
     const uint32_t src = r.y & (kV7MaxHosts - 1);
+    if (o.fl_out) {
+        const uint32_t send = o.fl_perm[r.w];
+        if (o.fl_b12) {
+            uint32_t* e = static_cast<uint32_t*>(o.fl_out) + 3 * at;
+            e[0] = r.x;
+            e[1] = r.z;
+            e[2] = send;
+        } else {
+            static_cast<uint4*>(o.fl_out)[at] = make_uint4(r.x, src, r.z, send);
+        }
+        return;
+    }
     o.deliver[at] = o.round_end + r.x;
     o.src[at] = src;
     o.seq[at] = o.seq_base ? o.seq_base[src] + r.z : r.z;
@@ -2066,6 +2084,12 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     }
     V7Out vo{o->ev_deliver, o->ev_src, o->ev_seq, o->ev_pkt,
              a.abs_seq ? nullptr : R.next_id.as<uint64_t>(), rd->round_end};
+    if (R.fl_ev_out && !a.abs_seq) {   // a flush round: compact records straight from the bin sort
+        vo.fl_out = R.fl_ev_out;
+        vo.fl_perm = R.fl_perm.as<uint32_t>();
+        vo.fl_b12 = R.fl_b12;
+        R.fl_direct = true;
+    }
     const uint32_t stop = ctx->knobs.get(K_B7_STOP, 0);   // tuning only: partial K4 (wrong output)
     bin_sort_v7<false><<<n_bins, kB7Threads, 0, s>>>(H, n_bins, R.bin_base.as<uint32_t>(), R.rec.as<uint4>(),
                                                     R.bin_lb.as<unsigned long long>(), o->ev_off, vo, a.red,

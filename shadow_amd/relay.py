@@ -192,7 +192,7 @@ class Relay:
         return out
 
     def flush(self, run_host, run_count, sends, time_base: int, round_end: int, sim_end: int,
-              bootstrap_end: int = 0, pinned=None, event_bytes: int = 16) -> "FlushResult":
+              bootstrap_end: int = 0, pinned=None, event_bytes: int = 16, pinned_out: bool = False) -> "FlushResult":
         """``shd_relay_flush``: the worker threads' staging buffers as they stand (per stage: the
         runs' hosts and counts and the (n, 3) u32 send records {time_off, dst | SEND_PAYLOAD,
         draw_hi}).  ``pinned``: a PinnedStages holding them in pinned memory (the drop-in's path);
@@ -204,11 +204,27 @@ class Relay:
         ev_off = np.zeros(self.n_hosts + 1, np.uint32)
         events = np.zeros((max(n, 1), event_bytes // 4), np.uint32)   # 12 bytes: no source host column
         seq_base = np.zeros(self.n_hosts, np.uint64)
-        out = N.FlushOut(N.ptr(st2).value, N.ptr(ev_off).value, N.ptr(events).value, N.ptr(seq_base).value, 0, 0, 0, 0,
-                         event_bytes)
-        rd = N.Round(round_end, sim_end, bootstrap_end)
-        N.check(self.eng.lib.shd_relay_flush(self.eng.ctx, pinned.array, len(pinned.stages), int(time_base),
-                                             C.byref(rd), C.byref(out)), "shd_relay_flush")
+        bufs, allocs = [st2, ev_off, events, seq_base], []
+        if pinned_out:   # the outputs in pinned memory too: the device writes them where they lie
+            lib = self.eng.lib
+            for i, a in enumerate(bufs):
+                ptr = lib.shd_host_alloc(max(a.nbytes, 1))
+                if not ptr:
+                    for q in allocs:
+                        lib.shd_host_free(q)
+                    raise MemoryError("shd_host_alloc")
+                allocs.append(ptr)
+                bufs[i] = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), (max(a.nbytes, 1),))[: a.nbytes] \
+                    .view(a.dtype).reshape(a.shape)
+        try:
+            out = N.FlushOut(*(N.ptr(a).value for a in bufs), 0, 0, 0, 0, event_bytes)
+            rd = N.Round(round_end, sim_end, bootstrap_end)
+            N.check(self.eng.lib.shd_relay_flush(self.eng.ctx, pinned.array, len(pinned.stages), int(time_base),
+                                                 C.byref(rd), C.byref(out)), "shd_relay_flush")
+            st2, ev_off, events, seq_base = (a.copy() for a in bufs)
+        finally:
+            for q in allocs:
+                self.eng.lib.shd_host_free(q)
         status = ((st2[:, None] >> (np.arange(4, dtype=np.uint8) * 2)) & 3).reshape(-1)[:n]
         return FlushResult(status, ev_off, events[:out.n_sent], seq_base, out.min_deliver, out.min_latency,
                            out.n_sent)

@@ -43,13 +43,18 @@ def _check(fr, o, st, nid_before, round_end):
     assert (fr.min_deliver, fr.min_latency) == (o["min_deliver"], o["min_latency"])
 
 
-@pytest.mark.parametrize("n_threads,pinned,event_bytes", [(1, False, 16), (16, False, 16), (1, True, 16),
-                                                         (16, True, 16), (16, True, 12)])
-def test_flush_rounds_vs_c_oracle(engine, n_threads, pinned, event_bytes):
+@pytest.mark.parametrize("n_threads,pinned,event_bytes,pinned_out,copy",
+                         [(1, False, 16, False, 0), (16, False, 16, False, 0), (1, True, 16, False, 0),
+                          (16, True, 16, False, 0), (16, True, 12, False, 0), (16, True, 16, True, 0),
+                          (16, True, 12, True, 0), (16, True, 16, True, 1)])
+def test_flush_rounds_vs_c_oracle(engine, knob, n_threads, pinned, event_bytes, pinned_out, copy):
+    """Pinned staging is read where it lies and pinned outputs are written where they lie (zero-copy)
+    unless the FLUSH_COPY knob asks for the copies; pageable buffers are always copied."""
     from shadow_amd import synth
     from shadow_amd.relay import PinnedStages, Relay
     H, NN, P = 20_000, 200, 1_000_000
     lat, loss, host_node, rng0 = _case(H, NN, 21)
+    knob("FLUSH_COPY", copy)
     rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
     onid = np.zeros(H, np.uint64)
     start, ra = 10**9, 10**6
@@ -64,7 +69,7 @@ def test_flush_rounds_vs_c_oracle(engine, n_threads, pinned, event_bytes):
         ps = PinnedStages.pinned(engine.lib, st.run_host, st.run_count, st.sends) if pinned else None
         try:
             fr = rl.flush(st.run_host, st.run_count, st.sends, start, start + ra, start + 100 * ra, boot, pinned=ps,
-                          event_bytes=event_bytes)
+                          event_bytes=event_bytes, pinned_out=pinned_out)
         finally:
             if ps is not None:
                 ps.free()
@@ -141,7 +146,7 @@ def test_flush_rejects_bad_staging(engine):
     _check(fr, o, st, np.zeros(H, np.uint64), 10**9 + 10**6)
 
 
-@pytest.mark.parametrize("path", ["bins", "x24"])
+@pytest.mark.parametrize("path", ["bins", "x24", "bins-pinned"])
 def test_flush_two_ranks_vs_c_oracle(engine, knob, path):
     """shd_relay_flush under a two-rank communicator: both ranks get the same 16 stages (every
     thread's buffer mixes both ranks' hosts); each keeps its own hosts' runs.  The OR of the ranks'
@@ -171,10 +176,13 @@ def test_flush_two_ranks_vs_c_oracle(engine, knob, path):
             o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(),
                                  onid, start + ra, start + 100 * ra, boot, chance=chance)
             res, errs = [None, None], []
+            from shadow_amd.relay import PinnedStages
+            ps = PinnedStages.pinned(engines[0].lib, st.run_host, st.run_count, st.sends) if path == "bins-pinned" else None
 
             def go(i):
-                try:
-                    res[i] = rels[i].flush(st.run_host, st.run_count, st.sends, start, start + ra, start + 100 * ra, boot)
+                try:   # (both ranks read the same pinned stages in place)
+                    res[i] = rels[i].flush(st.run_host, st.run_count, st.sends, start, start + ra, start + 100 * ra, boot,
+                                           pinned=ps)
                 except BaseException as ex:   # noqa: BLE001
                     errs.append(ex)
             ts = [threading.Thread(target=go, args=(i,)) for i in range(2)]
@@ -182,8 +190,10 @@ def test_flush_two_ranks_vs_c_oracle(engine, knob, path):
                 t.start()
             for t in ts:
                 t.join(timeout=300)
+            if ps is not None:
+                ps.free()
             assert not errs, errs
-            assert [r.last_pipeline() for r in rels] == ([8, 8] if path == "bins" else [7, 7])
+            assert [r.last_pipeline() for r in rels] == ([7, 7] if path == "x24" else [8, 8])
             inv = np.empty(len(st.stage_of_send), np.int64)
             inv[st.stage_of_send] = np.arange(len(st.stage_of_send))
             assert np.array_equal(res[0].status | res[1].status, o["status"][st.stage_of_send])
