@@ -52,17 +52,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# SHD_BENCH_REHEARSAL=1: every rank on GPU 0, torch.distributed over gloo and the engine's host
+# transport (shd_comm_init_host) instead of RCCL -- a rehearsal of the N > 1 code paths (sharding,
+# exchanges, checks) on a one-GPU box; its times are not scaling numbers (the ranks share one GPU).
+REHEARSAL = os.environ.get("SHD_BENCH_REHEARSAL", "") == "1"
+_DIST_DEV = "cuda"   # where the bench's own reductions live (cpu under gloo)
+
+
 def dist_setup(n_gpus):
+    global _DIST_DEV
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != n_gpus:
         raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    if REHEARSAL:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if REHEARSAL:
+            dist.init_process_group("gloo")
+            _DIST_DEV = "cpu"
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
@@ -80,7 +94,7 @@ def max_over_ranks(x, world):
         return x
     import torch
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=_DIST_DEV)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -91,7 +105,7 @@ def all_ranks_ok(ok, world):
         return bool(ok)
     import torch
     import torch.distributed as dist
-    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=_DIST_DEV)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return bool(t.item())
 
@@ -954,9 +968,13 @@ def main():
     world, rank, local = dist_setup(args.gpus)
     from shadow_amd.routing import Engine
     eng = Engine(local)
+    host_comm = None
     if world > 1:   # the engine's own communicator: RCCL over xGMI, one rank per GPU
         from shadow_amd import dist as D
-        D.comm_init_rccl(eng)
+        if REHEARSAL:
+            host_comm = D.HostComm(eng)   # (kept alive: it holds the transport callback)
+        else:
+            D.comm_init_rccl(eng)
     cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
 
     r = routing_leg(eng, world, rank, args.steps, args.warmup)
@@ -1055,6 +1073,7 @@ def main():
     if rank == 0:
         print(json.dumps(res), flush=True)
     eng.close()
+    del host_comm
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
