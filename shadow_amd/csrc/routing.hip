@@ -2242,7 +2242,7 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         }
         bool ovf = false;
         // delta-stepping bucket width (env override for tuning).  SHD_ALGO_DELTA: the mean arc
-        // latency.  AUTO on a pruned dense graph: the smallest arc latency (never pruned: every
+        // latency x 1.5 (below).  AUTO on a pruned dense graph: the smallest arc latency (never pruned: every
         // detour has two arcs), floored at mean/256 so that a stray tiny arc cannot make the
         // sweep count explode -- a bucket no wider than every arc settles in one sweep, so each
         // node is expanded once (Dial order); the sweep jumps to the smallest active label, so
@@ -2250,8 +2250,11 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
         // AUTO on a sparse graph: buckets of the mean arc latency (C3: 9.9 ms against 11.6 for
         // plain sweeps; 5 ms buckets 11.4, 2 ms 15.8)
         uint32_t delta = kLat32Inf;
+        // (LDS labels: 1.5 x mean_arc_lat.  C3 with the hub relaxation, round 5, tools/c3_delta_sweep.sh:
+        // 8 ms 7.85, 10 ms 7.38, 12.5 ms (1.0 x, the old default) 7.03, 16 ms 6.88, 20 ms 6.83-6.84,
+        // 25 ms 7.02, 30 ms 7.17, 40 ms 7.64)
         if (algo == SHD_ALGO_DELTA || (algo == SHD_ALGO_AUTO && !prune && ctx->knobs.get(K_SSSP_NO_DELTA, 0) != 1))
-            delta = ctx->knobs.get(K_SSSP_DELTA, P.mean_arc_lat);
+            delta = ctx->knobs.get(K_SSSP_DELTA, (uint32_t)std::min<uint64_t>(kLat32Inf - 1, (uint64_t)P.mean_arc_lat * 3 / 2));
         else if (algo == SHD_ALGO_AUTO && prune && ctx->knobs.get(K_SSSP_NO_DELTA, 0) != 1)
             delta = ctx->knobs.get(K_SSSP_DELTA, std::max(P.min_arc_lat, P.mean_arc_lat / 256));
         SHD_TRY(run_sssp(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
