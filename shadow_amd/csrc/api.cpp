@@ -80,6 +80,13 @@ shd_status readback_into(shd_ctx* ctx, hipStream_t s, const void* d_src, size_t 
     volatile unsigned long long* done = ctx->h_pin + kPinMarker;
     *done = 0;
     SHD_TRY(readback_launch(s, d_src, (uint32_t)(n_bytes / 8), h_dst, const_cast<unsigned long long*>(done)));
+    return wait_marker(ctx, s);
+}
+
+// the polled wait of readback_into, for kernels that write their words and the marker themselves
+// (the caller zeroes the marker before launching them)
+shd_status wait_marker(shd_ctx* ctx, hipStream_t s) {
+    volatile unsigned long long* done = ctx->h_pin + kPinMarker;
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 1; *done != 1; ++i) {
         __builtin_ia32_pause();

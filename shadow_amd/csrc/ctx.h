@@ -225,6 +225,9 @@ shd_status wait_stream(shd_ctx* ctx, hipStream_t s);
 shd_status readback(shd_ctx* ctx, hipStream_t s, int at, const void* d_src, size_t n_bytes);
 // the same into coherent pinned words of the caller's (PinBuf; n_bytes a multiple of 8, 8-aligned)
 shd_status readback_into(shd_ctx* ctx, hipStream_t s, const void* d_src, size_t n_bytes, unsigned long long* h_dst);
+// poll the pinned marker h_pin[kPinMarker] (zeroed by the caller) that a kernel sets after writing
+// its words into pinned memory; falls back to hipStreamSynchronize after 20 ms
+shd_status wait_marker(shd_ctx* ctx, hipStream_t s);
 // a committed relay round's (all-rank) reductions: the runahead update (runahead.rs:60-115) and
 // the earliest deliver time of the relay output that the queues have not merged yet (rounds.cpp)
 void round_note(shd_ctx* ctx, uint64_t min_deliver, uint64_t min_latency);

@@ -674,7 +674,8 @@ __global__ __launch_bounds__(256) void eqr_merge16(uint32_t n_hosts, EqSrcs S, c
 __global__ __launch_bounds__(1024) void eq_totals(uint32_t n_hosts, uint32_t n_part, const uint32_t* __restrict__ pop_off,
                                                   const uint32_t* __restrict__ keep_off,
                                                   const unsigned long long* __restrict__ part,
-                                                  unsigned long long* __restrict__ words) {
+                                                  unsigned long long* __restrict__ words,
+                                                  unsigned long long* host_words, unsigned long long* marker) {
     __shared__ unsigned long long s_v[16][kEqPart];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // a thread takes whole partial records (independent loads), then one reduction per word
@@ -697,16 +698,24 @@ __global__ __launch_bounds__(1024) void eq_totals(uint32_t n_hosts, uint32_t n_p
         if (lane == 0) s_v[w][j] = v[j];
     }
     __syncthreads();
+    // host_words (the read-back in the same launch): the words go straight to the pinned host
+    // words and the marker the host polls follows them (as rounds.hip readback_mark)
+    unsigned long long* out = host_words ? host_words : words;
     if (threadIdx.x < kEqPart) {
         const uint32_t j = threadIdx.x;
         unsigned long long t = s_v[0][j];
         for (int ww = 1; ww < 16; ++ww) t = j == 0 ? (s_v[ww][j] < t ? s_v[ww][j] : t) : t + s_v[ww][j];
-        if (j == 0) words[3] = t;
-        else words[3 + j] = t;   // words[4 + k] = left of source k
+        if (j == 0) out[3] = t;
+        else out[3 + j] = t;   // words[4 + k] = left of source k
     }
     if (threadIdx.x == 0) {
-        words[1] = pop_off[n_hosts];
-        words[2] = keep_off ? keep_off[n_hosts] : 0u;
+        out[1] = pop_off[n_hosts];
+        out[2] = keep_off ? keep_off[n_hosts] : 0u;
+    }
+    if (host_words) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // every thread's words reach the host first
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(marker, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -773,7 +782,16 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
     }
     SHD_HIP(hipGetLastError());
     if (!counts) return SHD_OK;   // (a compaction: what it moves is known on the host, nothing to wait for)
-    eq_totals<<<1, 1024, 0, s>>>(H, nb, out_off, nrun ? nrun->off.as<uint32_t>() : nullptr, part, words);
+    if (ctx->spin_wait && ctx->knobs.get(K_SYNC_KERNEL, 1) != 0) {   // totals + read-back in one launch
+        volatile unsigned long long* mark = ctx->h_pin + kPinMarker;
+        *mark = 0;
+        eq_totals<<<1, 1024, 0, s>>>(H, nb, out_off, nrun ? nrun->off.as<uint32_t>() : nullptr, part, words,
+                                     ctx->h_pin + kEqPinWord, const_cast<unsigned long long*>(mark));
+        SHD_HIP(hipGetLastError());
+        return wait_marker(ctx, s);
+    }
+    eq_totals<<<1, 1024, 0, s>>>(H, nb, out_off, nrun ? nrun->off.as<uint32_t>() : nullptr, part, words, nullptr,
+                                 nullptr);
     return readback(ctx, s, kEqPinWord, words, kEqWords * 8);
 }
 
