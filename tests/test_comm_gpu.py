@@ -303,3 +303,49 @@ def test_local_two_ranks_relay_into_queues_with_window(engine, dynamic):
 def _dev(a, dt):
     import torch
     return torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()
+
+
+@pytest.mark.parametrize("world,H,path", [(3, 5003, "bins"), (4, 4099, "bins"), (5, 3001, "bins"), (3, 5003, "x24"),
+                                          (8, 2000, "bins")])
+def test_local_many_ranks_relay_rounds(engine, knob, world, H, path):
+    """World sizes past two with host counts that split unevenly (the last rank's shard and last
+    bin are short; with 8 ranks on 2000 hosts every shard ends inside a bin of 32): two rounds,
+    every rank's statuses, events, reductions, streams and ids against the C restatement, and
+    the same round through the bin exchange and the packing form."""
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd.routing import Engine
+    NN, P = 40, 60 * H
+    _, lat, loss, host_node, rng0 = _case(H, NN, 7 + world)
+    engines = [Engine(0) for _ in range(world)]
+    try:
+        for e in engines:
+            knob("RELAY_SHARD_X24", 1 if path == "x24" else 0, eng=e)
+        D.comm_init_local(engines)
+        rels = [D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss) for e in engines]
+        bounds = [(r.lo, r.hi) for r in rels]
+        assert bounds[0][0] == 0 and bounds[-1][1] == H
+        orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+        start, ra = 10**9, 10**6
+        for rnd in range(2):
+            b = synth.packet_batch(H, P, start, start + ra, seed=300 + world + rnd)
+            rd = (start + ra, start + 10**12, start + ra // 2 if rnd == 0 else 0)
+            o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, orng, onid, *rd)
+            parts = [_slice_batch(b, r.lo, r.hi) for r in rels]
+            outs = _run_ranks([lambda r=r, p=p: r.round(*p[:4], rd) for r, p in zip(rels, parts)])
+            assert {r.last_pipeline() for r in rels} == ({8} if path == "bins" else {7})
+            bases = np.array([p[4] for p in parts], np.int64)
+            his = np.array([hi for _, hi in bounds], np.int64)
+
+            def a_of(src):
+                return bases[np.searchsorted(his, src.astype(np.int64), side="right")]
+            for r, out in zip(rels, outs):
+                _check_rank(out, o, r.lo, r.hi, a_of, b)
+            for r in rels:
+                st, nid = r.host_state()
+                assert np.array_equal(st[r.lo:r.hi], orng[r.lo:r.hi])
+                assert np.array_equal(nid[r.lo:r.hi], onid[r.lo:r.hi])
+            start += ra
+    finally:
+        for e in engines:
+            e.close()
