@@ -349,3 +349,47 @@ def test_local_many_ranks_relay_rounds(engine, knob, world, H, path):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.parametrize("world,chunk_rows", [(3, None), (4, 9), (8, 5), (8, None)])
+def test_local_many_ranks_routing_sharded(engine, world, chunk_rows):
+    """The sharded routing build past two ranks: uneven row shards (301 rows), one all-gather or
+    chunked exchanges with short last chunks; every rank's whole table against the C restatement."""
+    import ctypes as C
+
+    import torch
+    from shadow_amd import _native as N
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd.routing import Engine
+    from tests.graphs import engine_graph_from_edges
+    n = 301
+    el = synth.complete_graph(n, 20 + world)
+    used = np.arange(n, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(n, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    engines = [Engine(0) for _ in range(world)]
+    try:
+        for e in engines:
+            e.set_knob("SHARD_REPLICATE_MB", 0)
+            if chunk_rows:
+                e.set_knob("SHARD_CHUNK_ROWS", chunk_rows)
+        D.comm_init_local(engines)
+        g = engine_graph_from_edges(el)
+        per = (n + world - 1) // world
+        bufs = []
+        for e in engines:
+            cg = g._cgraph()
+            err = N.Error()
+            N.check(e.lib.shd_routing_prepare(e.ctx, C.byref(cg), N.ptr(used), n, N.ROUTE_SHORTEST, C.byref(err)),
+                    "prepare", err)
+            bufs.append((torch.empty((world * per, n), dtype=torch.int64, device="cuda"),
+                         torch.empty((world * per, n), dtype=torch.float32, device="cuda")))
+        torch.cuda.synchronize()
+        _run_ranks([lambda e=e, b=b: D.routing_run_sharded(e, N.ALGO_AUTO, b[0], b[1]) for e, b in zip(engines, bufs)])
+        for lt, ls in bufs:
+            assert np.array_equal(lt[:n].cpu().numpy().view(np.uint64), lat)
+            assert np.array_equal(ls[:n].cpu().numpy().view(np.uint32), loss.view(np.uint32))
+    finally:
+        for e in engines:
+            e.close()
