@@ -393,3 +393,44 @@ def test_local_many_ranks_routing_sharded(engine, world, chunk_rows):
     finally:
         for e in engines:
             e.close()
+
+
+@pytest.mark.parametrize("world,H", [(4, 3), (3, 7)])
+def test_local_ranks_without_hosts_or_sends(engine, world, H):
+    """More ranks than hosts (a rank owning no host) and ranks whose hosts send nothing: every
+    rank agrees on the round (the bin exchange needs every rank on pipeline 7, so the packing
+    form runs) and the results match the C restatement."""
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd.routing import Engine
+    NN = 3
+    _, lat, loss, host_node, rng0 = _case(H, NN, 31)
+    engines = [Engine(0) for _ in range(world)]
+    try:
+        D.comm_init_local(engines)
+        rels = [D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss) for e in engines]
+        bounds = [(r.lo, r.hi) for r in rels]
+        b = synth.packet_batch(H, 40, 10**9, 10**9 + 10**6, seed=5)
+        # the first host sends nothing
+        keep = np.ones(b.n, bool)
+        keep[: int(b.src_off[1])] = False
+        cnt = np.diff(b.src_off.astype(np.int64))
+        cnt[0] = 0
+        off = np.zeros(H + 1, np.uint32)
+        np.cumsum(cnt, out=off[1:])
+        b = synth.PacketBatch(off, b.send_time[keep], b.dst_host[keep], b.payload[keep])
+        rd = (10**9 + 10**6, 10**12, 0)
+        orng, onid = rng0.copy(), np.zeros(H, np.uint64)
+        o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, orng, onid, *rd)
+        parts = [_slice_batch(b, r.lo, r.hi) for r in rels]
+        outs = _run_ranks([lambda r=r, p=p: r.round(*p[:4], rd) for r, p in zip(rels, parts)])
+        bases = np.array([p[4] for p in parts], np.int64)
+        his = np.array([hi for _, hi in bounds], np.int64)
+
+        def a_of(src):
+            return bases[np.searchsorted(his, src.astype(np.int64), side="right")]
+        for r, out in zip(rels, outs):
+            _check_rank(out, o, r.lo, r.hi, a_of, b)
+    finally:
+        for e in engines:
+            e.close()
