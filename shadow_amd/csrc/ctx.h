@@ -193,6 +193,7 @@ struct PreparedGraph {
     uint64_t arcs = 0, max_arc_lat = 0, pruned_arcs = 0, tight_arcs = 0;
     uint32_t mean_arc_lat = 1, min_arc_lat = 1;
     bool reordered = false;   // g_offr / g_usedr / g_arc8r / g_aqr hold the locality order
+    bool used_ident = false;  // used[j] == j for every node (the LDS kernels then skip that gather)
     uint32_t lds_labels = 0;  // how many of the first (highest-degree) nodes keep LDS labels
     std::vector<uint32_t> used, node_ids, es, ed;
     std::vector<uint64_t> el;

@@ -422,8 +422,14 @@ __device__ __forceinline__ void expand_flat8(const uint32_t* q, uint32_t qn, uin
 __device__ unsigned long long g_sssp_prof[8];
 #define SS_MARK(slot) do { if (true) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
     ss_acc[slot] += t_ - ss_t; ss_t = t_; } } while (0)
+// prune_rows: shader clocks per phase summed over workgroups (thread 0): row load + max, histogram,
+// boundary bin, detour selection, 2-hop tests, list write; [6] first start, [7] last end (100 MHz)
+__device__ unsigned long long g_prune_prof[4096 * 8];   // per workgroup (row u < 4096)
+#define PR_MARK(slot) do { if (threadIdx.x == 0) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    pr_acc[slot] += t_ - pr_t; pr_t = t_; } } while (0)
 #else
 #define SS_MARK(slot) do { } while (0)
+#define PR_MARK(slot) do { } while (0)
 #endif
 
 // One source row: init, sweeps until nothing improves, emit the used columns.
@@ -449,7 +455,7 @@ __device__ __forceinline__ void sssp_row(
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t grp = lane / G, gl = lane % G;
     uint32_t* q = wq + wave * kQStride;
-    const uint32_t src = used[row];
+    const uint32_t src = used ? used[row] : row;   // (nullptr: every node used, in index order)
 #ifdef SHD_SSSP_PROF
     uint64_t ss_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ss_t = __builtin_amdgcn_s_memtime();
 #endif
@@ -810,7 +816,7 @@ __device__ __forceinline__ void sssp_row(
         if (GLAB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         for (uint32_t j = tid; j < n_used; j += BLOCK) {
-            const uint32_t v = used[j];
+            const uint32_t v = used ? used[j] : j;
             uint32_t nh = 0xFFFFFFFFu;
             if (v == src) {
                 nh = src;
@@ -836,7 +842,7 @@ __device__ __forceinline__ void sssp_row(
 #pragma unroll
         for (uint32_t i = 0; i < kOut; ++i) {
             const uint32_t j = j0 + i * BLOCK;
-            uj[i] = j < n_used ? used[j] : 0u;
+            uj[i] = j < n_used ? (used ? used[j] : j) : 0u;
         }
 #pragma unroll
         for (uint32_t i = 0; i < kOut; ++i) {
@@ -1049,16 +1055,23 @@ __device__ __forceinline__ uint32_t dense_lat(const uint32_t* __restrict__ Wl, u
     else return Wl[(size_t)x * V + v];
 }
 
-template <int BLOCK, int K, bool DCSR = false>
+template <int BLOCK, int K, bool DCSR = false, int VB = 4, int KB = 8, bool CMP = false, int PB = 8>
 __global__ __launch_bounds__(BLOCK) void prune_rows(
     const uint32_t* __restrict__ Wl, const float* __restrict__ Wp, uint32_t V,
     uint32_t* __restrict__ pbeg, uint32_t* __restrict__ pend, uint4* __restrict__ parcs,
-    uint32_t* __restrict__ cursor, uint32_t* __restrict__ flags) {
+    uint32_t* __restrict__ cursor, uint32_t* __restrict__ flags, uint32_t shg = 0xFFFFFFFFu) {
     // Detour nodes x: ~K of u's lowest-latency neighbours, chosen by a 256-bin latency histogram
     // (every node in the bins below the K-th smallest latency's bin, then nodes of that bin in
     // index order up to K).  Any set of detour nodes is sound -- it only decides how many arcs
     // are dropped -- so this replaces a full bitonic sort of the row (55 barrier stages) by
     // three passes over it.
+    // CMP (round 5, the K = 32 default; C2 prune 24.4 -> 15.6 us): the detours are the K
+    // smallest (latency, index) pairs in ascending order, ranked in LDS by all waves; the first
+    // batch tests every arc against the KB nearest, skipping detours no shorter than the arc; its
+    // survivors (~11 % of a C2 row) are packed and tested one lane each against the rest, PB at a
+    // time, stopping at the first detour no shorter than the arc -- instead of every wave
+    // carrying a few live lanes through every batch.  The row's losses come in with its
+    // latencies, so the kept arcs read them from LDS.
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint4* kept = reinterpret_cast<uint4*>(smem);      // V staged arcs
     uint32_t* cnt = reinterpret_cast<uint32_t*>(kept + V);   // [0] kept [1] base [2] max [3] below-bin
@@ -1067,28 +1080,48 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
     uint32_t* sela = selx + K;                         // their latencies
     uint32_t* row = sela + K;                          // u's exact arc latencies
     uint16_t* binv = reinterpret_cast<uint16_t*>(row + V);   // bin per node (0xFFFF: no arc)
+    uint2* live2 = reinterpret_cast<uint2*>((reinterpret_cast<uintptr_t>(binv + V) + 7) & ~(uintptr_t)7);   // CMP: first-batch survivors
+    uint64_t* cand = reinterpret_cast<uint64_t*>(live2 + V);   // CMP: <= 64 detour candidates
+    uint32_t* rk = reinterpret_cast<uint32_t*>(cand + 64);        // and their ranks
+    float* prow = reinterpret_cast<float*>(rk + 64);              // CMP: u's arc losses
     const uint32_t u = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+#ifdef SHD_SSSP_PROF
+    uint64_t pr_acc[6] = {0, 0, 0, 0, 0, 0}, pr_t = __builtin_amdgcn_s_memtime();
+    const uint64_t pr_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (DCSR && u == 0 && tid < 16) flags[tid] = (tid == 4 || tid == 5) ? 0xFFFFFFFFu : 0u;   // as flags_init
-    for (uint32_t v = tid; v < V; v += BLOCK) row[v] = dense_lat<DCSR>(Wl, V, u, v);
-    for (uint32_t i = tid; i < 256; i += BLOCK) hist[i] = 0;
-    if (tid < 8) cnt[tid] = 0;
     uint32_t mx = 0;
     for (uint32_t v = tid; v < V; v += BLOCK) {
-        const uint32_t w = row[v];
+        const uint32_t w = dense_lat<DCSR>(Wl, V, u, v);
+        row[v] = w;
         if (w != kLat32Inf) mx = max(mx, w);
+        if constexpr (CMP) {   // the row's losses ride the same memory trip (kept arcs read them)
+            if (w != kLat32Inf) prow[v] = Wp[DCSR ? (size_t)u * (V - 1) + v - (v > u ? 1u : 0u) : (size_t)u * V + v];
+        }
     }
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-    __syncthreads();
-    if (lane == 0) atomicMax(&cnt[2], mx);
-    __syncthreads();
-    const uint32_t bits = 32u - (uint32_t)__clz((int)max(cnt[2], 1u));
-    const uint32_t sh = bits > 8 ? bits - 8 : 0;
+    for (uint32_t i = tid; i < 256; i += BLOCK) hist[i] = 0;
+    if (tid < 8) cnt[tid] = 0;
+    if (CMP && tid < 64) rk[tid] = 0;
+    uint32_t sh;
+    if (CMP && shg != 0xFFFFFFFFu) {   // bins from the graph's largest arc latency (host): one barrier
+        __syncthreads();
+        sh = shg;
+    } else {
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        __syncthreads();
+        if (lane == 0) atomicMax(&cnt[2], mx);
+        __syncthreads();
+        const uint32_t bits = 32u - (uint32_t)__clz((int)max(cnt[2], 1u));
+        sh = bits > 8 ? bits - 8 : 0;
+    }
+    PR_MARK(0);
     for (uint32_t v = tid; v < V; v += BLOCK) {
         const uint32_t w = row[v];
         binv[v] = w != kLat32Inf ? (uint16_t)(w >> sh) : (uint16_t)0xFFFF;
         if (w != kLat32Inf) atomicAdd(&hist[w >> sh], 1u);
     }
     __syncthreads();
+    PR_MARK(1);
     if (tid < 64) {   // wave 0: the bin holding the K-th smallest latency
         uint32_t c[4], sum = 0;
 #pragma unroll
@@ -1128,7 +1161,56 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
         }
     }
     __syncthreads();
-    {   // every node of the bins below; then wave 0 takes the boundary bin in index order, so
+    PR_MARK(2);
+    // CMP: the detours are the K smallest (latency, index) pairs in ascending order.  Fast path:
+    // the bins below and the boundary bin hold at most 64 candidates -- collect them, and wave 0
+    // sorts them in registers; otherwise the index-order boundary scan below, then a rank sort.
+    bool sel_done = false;
+    if constexpr (CMP && K <= 64) {
+        const uint32_t bsel = cnt[4];
+        const uint32_t ncand = bsel < 256 ? cnt[3] + hist[bsel] : (uint32_t)K;
+        if (ncand <= 64) {
+            // rank sort: wave p compares every candidate with its share of the others
+            for (uint32_t v = tid; v < V; v += BLOCK) {
+                if (binv[v] <= bsel) {   // (no arc: 0xFFFF, above every bin)
+                    const uint32_t sl = atomicAdd(&cnt[5], 1u);
+                    cand[sl] = (uint64_t)row[v] << 32 | v;
+                }
+            }
+            __syncthreads();
+            const uint32_t n = cnt[5];
+            constexpr uint32_t per = 64 / (BLOCK / 64);
+            if (lane < n) {
+                const uint64_t ki = cand[lane];
+                const uint32_t j0 = (tid >> 6) * per;
+                uint32_t r = 0;
+#pragma unroll
+                for (uint32_t jj = 0; jj < per; ++jj)
+                    r += j0 + jj < n && cand[j0 + jj] < ki ? 1u : 0u;
+                if (r) atomicAdd(&rk[lane], r);
+            }
+            __syncthreads();
+            if (tid < 64) {
+                if (lane < n) {
+                    const uint32_t r = rk[lane];
+                    if (r < (uint32_t)K) {
+                        const uint64_t k = cand[lane];
+                        selx[r] = (uint32_t)k;
+                        sela[r] = (uint32_t)(k >> 32);
+                    }
+                } else if (lane < (uint32_t)K) {   // unused slots: no detour
+                    selx[lane] = 0u;
+                    sela[lane] = kLat32Inf;
+                }
+                if (tid == 0) {
+                    cnt[0] = 0;
+                    cnt[7] = 0;
+                }
+            }
+            sel_done = true;
+        }
+    }
+    if (!sel_done) {   // every node of the bins below; then wave 0 takes the boundary bin in index order, so
         // the detour set (and with it the kept-arc count) is the same on every run
         const uint32_t bsel = cnt[4], below = cnt[3];
         for (uint32_t v = tid; v < V; v += BLOCK) {
@@ -1153,19 +1235,42 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
             }
             if (tid == 0) cnt[6] = taken;
         }
+      __syncthreads();
+      const uint32_t nsel = min((uint32_t)K, cnt[5] + cnt[6]);
+      for (uint32_t j = nsel + tid; j < (uint32_t)K; j += BLOCK) {   // unused slots: no detour
+          selx[j] = 0u;
+          sela[j] = kLat32Inf;
+      }
+      if (tid == 0) cnt[0] = 0;
+      if constexpr (CMP) {   // detours in ascending latency (ties by index): wave 0 ranks them
+        __syncthreads();
+        uint32_t* tx = hist;   // the histogram is spent; K <= 128 pairs fit its 256 words
+        uint32_t* ta = hist + K;
+        if (tid < 64) {
+            for (uint32_t i = lane; i < (uint32_t)K; i += 64) {
+                const uint32_t ai = sela[i], xi = selx[i];
+                uint32_t r = 0;
+                for (uint32_t j = 0; j < (uint32_t)K; ++j) {
+                    const uint32_t aj = sela[j], xj = selx[j];
+                    r += aj < ai || (aj == ai && (xj < xi || (xj == xi && j < i))) ? 1u : 0u;
+                }
+                tx[r] = xi;
+                ta[r] = ai;
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = tid; j < (uint32_t)K; j += BLOCK) {
+            selx[j] = tx[j];
+            sela[j] = ta[j];
+        }
+        if (tid == 0) cnt[7] = 0;   // survivors of the first batch
+      }
     }
     __syncthreads();
-    const uint32_t nsel = min((uint32_t)K, cnt[5] + cnt[6]);
-    for (uint32_t j = nsel + tid; j < (uint32_t)K; j += BLOCK) {   // unused slots: no detour
-        selx[j] = 0u;
-        sela[j] = kLat32Inf;
-    }
-    if (tid == 0) cnt[0] = 0;
-    __syncthreads();
+    PR_MARK(3);
     // 2-hop test of every arc of u: each thread tests VB arcs at once against batches of KB
     // detours (VB x KB loads in flight), and a lane stops loading for an arc as soon as a
     // strictly shorter detour is found -- most arcs of a dense row fall to the first batch
-    constexpr int VB = 4, KB = 8;
     for (uint32_t v0 = tid; v0 < V; v0 += BLOCK * VB) {
         uint32_t w[VB], z[VB];
 #pragma unroll
@@ -1174,7 +1279,7 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
             w[i] = v < V ? row[v] : kLat32Inf;
             z[i] = kLat32Inf;
         }
-        for (int j0 = 0; j0 < K; j0 += KB) {
+        for (int j0 = 0; j0 < (CMP ? KB : K); j0 += KB) {
             bool any = false;
 #pragma unroll
             for (int i = 0; i < VB; ++i) any |= w[i] != kLat32Inf && w[i] <= z[i];
@@ -1193,7 +1298,11 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
                 const bool live = w[i] != kLat32Inf && w[i] <= z[i];
 #pragma unroll
                 for (int j = 0; j < KB; ++j) {
-                    if constexpr (DCSR)   // (x, x) has no arc; past the diagonal the row is shifted by one
+                    if constexpr (CMP)   // sorted detours: one no shorter than the arc cannot beat it
+                        bv[i][j] = live && as[j] < w[i] && v != xs[j]
+                                       ? Wl[xb[j] + v - (DCSR && v > xs[j] ? 1u : 0u)]
+                                       : kLat32Inf;
+                    else if constexpr (DCSR)   // (x, x) has no arc; past the diagonal the row is shifted by one
                         bv[i][j] = live && as[j] != kLat32Inf && v != xs[j] ? Wl[xb[j] + v - (v > xs[j] ? 1u : 0u)]
                                                                             : kLat32Inf;
                     else
@@ -1212,12 +1321,50 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
         for (int i = 0; i < VB; ++i) {
             if (w[i] == kLat32Inf || w[i] > z[i]) continue;
             const uint32_t v = v0 + i * BLOCK;
+            if constexpr (CMP) {   // survivors of the first batch: the rest of the detours below
+                if (K > KB && w[i] > sela[KB]) {
+                    const uint32_t li = atomicAdd(&cnt[7], 1u);
+                    live2[li] = make_uint2(v, w[i]);
+                    continue;
+                }
+            }
             const uint32_t slot = atomicAdd(&cnt[0], 1u);
             const size_t at = DCSR ? (size_t)u * (V - 1) + v - (v > u ? 1u : 0u) : (size_t)u * V + v;
-            kept[slot] = make_uint4(v, w[i], __float_as_uint(one_minus(Wp[at])), 0u);
+            kept[slot] = make_uint4(v, w[i], __float_as_uint(one_minus(CMP ? prow[v] : Wp[at])), 0u);
+        }
+    }
+    if constexpr (CMP && K > KB) {
+        // the first batch's survivors, packed: one lane per arc over the remaining detours in
+        // batches of 8 (a wave's loads are all live instead of a few lanes of every wave)
+        __syncthreads();
+        const uint32_t nl = cnt[7];
+        for (uint32_t i = tid; i < nl; i += BLOCK) {
+            const uint2 e = live2[i];
+            const uint32_t v = e.x, wv = e.y;
+            uint32_t z = kLat32Inf;
+            for (int j0 = KB; j0 < K && wv <= z && sela[j0] < wv; j0 += PB) {
+                uint32_t as[PB], bq[PB];
+#pragma unroll
+                for (int j = 0; j < PB; ++j) {
+                    as[j] = j0 + j < K ? sela[j0 + j] : kLat32Inf;
+                    const uint32_t x = j0 + j < K ? selx[j0 + j] : 0u;
+                    bq[j] = as[j] < wv && v != x
+                                ? Wl[(size_t)x * (DCSR ? V - 1 : V) + v - (DCSR && v > x ? 1u : 0u)]
+                                : kLat32Inf;
+                }
+#pragma unroll
+                for (int j = 0; j < PB; ++j) {
+                    const uint32_t t = as[j] + bq[j];
+                    if (as[j] != kLat32Inf && bq[j] != kLat32Inf && t >= as[j]) z = min(z, t);
+                }
+            }
+            if (wv > z) continue;
+            const uint32_t slot = atomicAdd(&cnt[0], 1u);
+            kept[slot] = make_uint4(v, wv, __float_as_uint(one_minus(prow[v])), 0u);
         }
     }
     __syncthreads();
+    PR_MARK(4);
     // each list is padded to kArcPad slots with no-op arcs for relax_node_pad (scratch label
     // V + i, lat 0, q 0: candidate (lu, 1.0f) against a scratch label holding 0).  Row u's list
     // starts at u * roundup(V, kArcPad): the 1000 workgroups of C2 finish together, and one
@@ -1237,6 +1384,14 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
         pbeg[u] = at;
         pend[u] = at + n;
     }
+#ifdef SHD_SSSP_PROF
+    PR_MARK(5);
+    if (tid == 0 && u < 4096) {
+        for (int k = 0; k < 6; ++k) g_prune_prof[u * 8 + k] = pr_acc[k];
+        g_prune_prof[u * 8 + 6] = pr_t0;
+        g_prune_prof[u * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1666,6 +1821,8 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
     P.n_used = n_used;
     P.directed = g->directed != 0;
     P.used.assign(used, used + n_used);
+    P.used_ident = n_used == g->n_nodes;
+    for (uint32_t j = 0; j < n_used && P.used_ident; j++) P.used_ident = used[j] == j;
     P.node_ids.resize(g->n_nodes);
     for (uint32_t v = 0; v < g->n_nodes; v++) P.node_ids[v] = gml_id(g, v);
     P.es.assign(g->edge_src, g->edge_src + g->n_edges);
@@ -1783,11 +1940,11 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
     auto* unreach = reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16);
     auto* stats = ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr;
     hipEvent_t e0 = ctx->time_now ? ctx->ev[2] : nullptr, e1 = ctx->time_now ? ctx->ev[3] : nullptr;
+    const uint32_t* usedp = P.used_ident ? nullptr : (const uint32_t*)ctx->g_used.as<uint32_t>();
     if constexpr (kArcPad % (G * 8) == 0) {
         if (lat_guard) {
             hipExtLaunchKernelGGL(sssp_lds_group<BLOCK, G, R, CACHE, 8>, dim3(re - rb), dim3(BLOCK), (uint32_t)lds,
-                                  ctx->stream, e0, e1, 0u, A.beg, A.end, A.arcs, P.V,
-                                  (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
+                                  ctx->stream, e0, e1, 0u, A.beg, A.end, A.arcs, P.V, usedp, P.n_used, rb,
                                   (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(),
                                   (const float*)ctx->g_diag_loss.as<float>(), d_lat, d_loss, flags, unreach, delta,
                                   stats, seed, seed_stride, ctx->nh_out, lat_guard, use_offl, 0u, 0u);
@@ -1801,8 +1958,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
                        flat_off + flat_bytes <= ctx->max_lds;
     auto kern = flatl ? sssp_lds_group<BLOCK, G, R, CACHE, 0, true> : sssp_lds_group<BLOCK, G, R, CACHE, 0, false>;
     hipExtLaunchKernelGGL(kern, dim3(re - rb), dim3(BLOCK), (uint32_t)(flatl ? flat_off + flat_bytes : lds),
-                          ctx->stream, e0, e1, 0u, A.beg, A.end, A.arcs, P.V,
-                          (const uint32_t*)ctx->g_used.as<uint32_t>(), P.n_used, rb,
+                          ctx->stream, e0, e1, 0u, A.beg, A.end, A.arcs, P.V, usedp, P.n_used, rb,
                           (const uint64_t*)ctx->g_diag_lat.as<uint64_t>(), (const float*)ctx->g_diag_loss.as<float>(),
                           d_lat, d_loss, flags, unreach, delta, stats, seed, seed_stride, ctx->nh_out, 0u,
                           use_offl, (uint32_t)flat_off, flatl ? 0u : ctx->knobs.get(K_SSSP_HUB, kHubDeg));
@@ -2038,13 +2194,21 @@ static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
     const uint32_t Kr = ctx->knobs.get(K_PRUNE_K, kPruneK);   // tuning: detour nodes per row (same output tables)
     const uint32_t K = Kr >= 128 ? 128u : Kr >= 64 ? 64u : 32u;
     const size_t plds = (size_t)V * 22 + (8 + 256 + 2 * (size_t)K) * 4;
+    // K = 32 (the default): the sorted-detour kernel (CMP) with the first batch's survivors
+    // packed; SHD_PRUNE_SHAPE=0 keeps the round-4 kernel for A/B (same tables)
+    const size_t plds_c = plds + 8 + (size_t)V * 12 + 64 * 12;   // + survivors (uint2 each), sort scratch, losses
+    const bool legacy = ctx->knobs.get(K_PRUNE_SHAPE, 1) == 0;
+    // bins from the graph's largest arc latency instead of each row's (SHD_PRUNE_SHAPE_SH=0: per row)
+    const uint32_t gbits = 64u - (uint32_t)__builtin_clzll(std::max<uint64_t>(std::min<uint64_t>(P.max_arc_lat, kLat32Inf - 1), 1));
+    const uint32_t shg = ctx->knobs.get(K_PRUNE_SHAPE_SH, 1) ? (gbits > 8 ? gbits - 8 : 0) : 0xFFFFFFFFu;
     if (P.dense_rows && !ctx->knobs.on(K_PRUNE_DENSE_BUILD)) {
         // the CSR is the dense matrix (complete graph, arcs in index order): prune straight from it
         const uint32_t* Wl = ctx->g_lat.as<uint32_t>();
         const float* Wp = ctx->g_aux.as<float>();
         if (K >= 128) prune_rows<256, 128, true><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
         else if (K >= 64) prune_rows<256, 64, true><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
-        else prune_rows<256, 32, true><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+        else if (legacy) prune_rows<256, 32, true><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+        else prune_rows<512, 32, true, 2, 8, true, 12><<<V, 512, plds_c, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags, shg);
     } else {
         SHD_TRY(ctx->g_dense.ensure(nn * 8));
         SHD_TRY(ctx->g_labels.ensure(nn * 4));
@@ -2055,7 +2219,8 @@ static shd_status run_prune(shd_ctx* ctx, ArcView* out) {
                                                   flags);
         if (K >= 128) prune_rows<256, 128><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
         else if (K >= 64) prune_rows<256, 64><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
-        else prune_rows<256, 32><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+        else if (legacy) prune_rows<256, 32><<<V, 256, plds, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags);
+        else prune_rows<512, 32, false, 2, 8, true, 12><<<V, 512, plds_c, s>>>(Wl, Wp, V, pbeg, pend, pa, cursor, flags, shg);
     }
     SHD_HIP(hipGetLastError());
     *out = ArcView{pbeg, pend, ctx->g_prune_dst.as<uint4>(), 0, true};
@@ -2311,5 +2476,9 @@ extern "C" int shd_debug_sssp_prof(unsigned long long* out, int reset) {
         if (hipMemcpyToSymbol(HIP_SYMBOL(shd::g_sssp_prof), z, sizeof(z)) != hipSuccess) return 1;
     }
     return 0;
+}
+extern "C" int shd_debug_prune_prof(unsigned long long* out, int reset) {   // 4096 x 8 words
+    (void)reset;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(shd::g_prune_prof), sizeof(unsigned long long) * 4096 * 8) != hipSuccess;
 }
 #endif

@@ -326,3 +326,37 @@ def test_global_label_kernel_forced(engine, seed, knob):
         t = NetworkGraph(ids, s, d, l, p, directed).compute_shortest_paths(used, engine, algo=algo)
         _assert_table(t, lat, loss.view(np.uint32))
 
+
+
+def _complete(n, mode, seed):
+    from shadow_amd import synth
+    el = synth.complete_graph(n, seed)
+    rng = np.random.default_rng(seed)
+    arcs = el.src != el.dst
+    if mode == "const":      # every arc ties: each row's boundary bin holds all of it (slow selection)
+        el.latency_ns[arcs] = np.uint64(5 * synth.MS)
+    elif mode == "few":      # three latencies: heavy ties, > 64 candidates in the boundary bin
+        el.latency_ns[arcs] = rng.integers(1, 4, size=int(arcs.sum())).astype(np.uint64) * np.uint64(synth.MS)
+    elif mode == "wide":     # ns-granular latencies over four decades (bins from the global max)
+        el.latency_ns[arcs] = rng.integers(1_000, 10_000_000, size=int(arcs.sum())).astype(np.uint64)
+    return el
+
+
+@pytest.mark.parametrize("n,mode", [(2, "rand"), (5, "rand"), (33, "rand"), (63, "const"), (64, "few"),
+                                    (65, "rand"), (130, "few"), (257, "wide"), (513, "rand"), (777, "few")])
+@pytest.mark.parametrize("dense_build", [0, 1])
+@pytest.mark.parametrize("shape", [None, 0])
+def test_prune_complete_graphs(engine, knob, n, mode, dense_build, shape):
+    """The k-nearest 2-hop prune on complete graphs (the dense-CSR and the dense_build inputs)
+    against the C restatement: the sorted-detour kernel (default; its fast and slow detour
+    selections -- ties put > 64 candidates in the boundary bin) and the round-4 kernel
+    (SHD_PRUNE_SHAPE=0); odd sizes exercise the LDS layout's alignment."""
+    knob("PRUNE_SHAPE", shape)
+    knob("PRUNE_DENSE_BUILD", dense_build)
+    el = _complete(n, mode, 11 + n)
+    used = np.arange(n, dtype=np.uint32)
+    code, lat, loss, _ = corc.routing(n, el.src, el.dst, el.latency_ns, el.packet_loss, False, used)
+    assert code == "OK"
+    t = engine_graph_from_edges(el).compute_shortest_paths(used, engine, algo=2)
+    _assert_table(t, lat, loss.view(np.uint32))
+    assert engine.last_info()["algo_used"] == 2
