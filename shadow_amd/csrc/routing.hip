@@ -465,6 +465,12 @@ __device__ __forceinline__ void sssp_row(
     const float inv_delta = use_delta ? (float)kBktSub / (float)delta : 0.0f;
     // the ordering key of an active node: its bucket byte, or its label's latency
     auto act_key = [&](uint32_t v) -> uint32_t {
+        // LDS labels: the latency half only, a 4-byte read (C3 DELTA 6.86 -> 6.79 ms; the 64-bit
+        // atomics write both halves at once, so the half read is always one label's latency)
+        if constexpr (!GLAB && !FASTG)
+            if (!bkt)
+                return __hip_atomic_load(reinterpret_cast<const uint32_t*>(&lab[v]) + 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
         return FASTG || bkt ? (uint32_t)(bkt[v] >> kBktShift) : key_lat(ld_lab<GLAB>(&lab[v]));
     };
 
