@@ -1363,9 +1363,12 @@ static shd_status relay_device_v1(shd_ctx* ctx, const shd_batch* b, const shd_ro
 // ==========================================================================================
 constexpr uint32_t kV7MaxHosts = 1u << 18;      // src host bits in the record
 constexpr uint32_t kV7MaxPackets = 1u << 24;    // packet-index bits in bin_sort_v7's key
-constexpr uint32_t kB7Threads = 512;
+#ifndef SHD_B7_THREADS
+#define SHD_B7_THREADS 512
+#endif
+constexpr uint32_t kB7Threads = SHD_B7_THREADS;
 constexpr uint32_t kB7Cap = 3584;               // records per bin staged in LDS (C5: ~3200)
-constexpr uint32_t kB7Per = kB7Cap / kB7Threads;
+constexpr uint32_t kB7Per = (kB7Cap + kB7Threads - 1) / kB7Threads;
 constexpr unsigned long long kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbMask = (1ull << 62) - 1;
 
 // Histogram row r = g * kHistSplit + k counts, per destination bin, the packets of the host

@@ -155,6 +155,8 @@ __device__ __forceinline__ void relax_node_pad(uint32_t u, uint32_t gl, uint64_t
         uint64_t cand[R], old[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) cand[i] = pack_key(lu + a[i].y, fold_q(qu, __uint_as_float(a[i].z)));
+        // (a plain read first and the atomic only for a better candidate measured slower: C2 SSSP
+        // 61 -> 66 us)
 #pragma unroll
         for (int i = 0; i < R; ++i)
             old[i] = atomicMin(reinterpret_cast<unsigned long long*>(&lab[a[i].x]), (unsigned long long)cand[i]);
