@@ -97,6 +97,7 @@ struct EqRunBuf {   // one stored run of the event queues: a CSR of per-host sor
 struct EqState {   // destination event queues (equeue.hip): a list of sorted runs (one per batch)
     EqRunBuf run[kEqSlots];         // slots
     int lend = -1;                  // the slot handed out by shd_equeue_batch_buffers (not live yet)
+    bool fold_next = false;         // the next pass folds a compaction in (the run limit was reached)
     uint64_t lend_cap = 0;          // events the lent slot holds
     DevBuf curs[2];                 // [kEqSlots][n_hosts] u32 cursors (first unpopped), double-buffered
     DevBuf bcut;                    // [n_hosts] the batch's first kept event per host

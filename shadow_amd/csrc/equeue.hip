@@ -49,6 +49,9 @@ struct EqSrcs {
     EqSrc s[kEqSrcMax];
     uint32_t n;
     int32_t b;   // index of the batch source, -1 without one
+    // sources whose remainders [cut, end) are merged into the new run together with the batch's
+    // (a compaction folded into the advance: those runs are dropped after it)
+    uint32_t fold = 0;
 };
 
 __device__ __forceinline__ bool eq_less(uint64_t ta, uint32_t sa, uint64_t qa, uint64_t tb, uint32_t sb,
@@ -121,10 +124,17 @@ __global__ __launch_bounds__(256) void eqr_count(uint32_t n_hosts, EqSrcs S, uin
             np = m - lo;
             rem = hi - m;
             if (m < hi) head = q.deliver[m] < head ? q.deliver[m] : head;
-            if ((int32_t)k == S.b) keep[h] = (uint32_t)rem;
         }
-        for (uint32_t o = kEqLanes / 2; o > 0; o >>= 1) np += __shfl_xor(np, o);
-        if (h < n_hosts && k == 0) pop[h] = np;
+        // the new run's events of this host: the batch's remainder and the folded runs'
+        uint32_t kp = h < n_hosts && k < S.n && ((int32_t)k == S.b || ((S.fold >> k) & 1u)) ? (uint32_t)rem : 0u;
+        for (uint32_t o = kEqLanes / 2; o > 0; o >>= 1) {
+            np += __shfl_xor(np, o);
+            kp += __shfl_xor(kp, o);
+        }
+        if (h < n_hosts && k == 0) {
+            pop[h] = np;
+            keep[h] = kp;
+        }
         if (h == n_hosts && k == 0) {
             pop[n_hosts] = 0;
             keep[n_hosts] = 0;
@@ -444,11 +454,13 @@ __device__ __forceinline__ void eq_merge_host(uint32_t h, uint32_t w, uint32_t l
 // STAGE: staged events per host -- kEqStage on the normal passes (8 workgroups per CU), 256 on a
 // compaction's (whole runs: ~100-250 pending per host on C5, sorted rather than searched in
 // global memory)
+// keep (a folded compaction's second launch): the sources in S.fold merge their remainders
+// [cut, end) into `popped` = the new run at pop_off = its offsets, whose cursor starts there.
 template <uint32_t STAGE>
 __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, const uint32_t* __restrict__ pop_off,
                                                  EqOut popped, EqOut nrun, const uint32_t* __restrict__ nrun_off,
                                                  uint32_t* __restrict__ nrun_cur, const uint2* __restrict__ ranges,
-                                                 uint32_t sort_rank) {
+                                                 uint32_t sort_rank, uint32_t keep = 0) {
     __shared__ uint64_t s_t[4][STAGE], s_q[4][STAGE], s_g[4][STAGE];
     __shared__ uint32_t s_s[4][STAGE];
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -456,6 +468,16 @@ __global__ __launch_bounds__(256) void eqr_merge(uint32_t n_hosts, EqSrcs S, con
     if (h >= n_hosts) return;   // wave-uniform; the kernel has no workgroup barrier
     // lane k < S.n holds source k's popped range and its place in the LDS stage
     uint32_t my_lo = 0, my_m = 0;
+    if (keep) {
+        if (lane < S.n && ((S.fold >> lane) & 1u)) {
+            my_lo = S.s[lane].cut[h];
+            my_m = S.s[lane].off[h + 1];
+        }
+        eq_merge_host<STAGE>(h, w, lane, S, my_lo, my_m, pop_off[h], popped, EqOut{}, 0u, nullptr, s_t, s_q, s_g,
+                             s_s, sort_rank != 0);
+        if (lane == 0) nrun_cur[h] = pop_off[h];
+        return;
+    }
     if (lane < S.n) {   // eqr_count's (cursor, cut) pairs of this host: one line
         const uint2 r = ranges[(size_t)h * kEqSrcMax + lane];
         my_lo = r.x;
@@ -754,6 +776,8 @@ static_assert(kEqPinWord + (int)kEqWords <= kPinMarker, "queue counts below the 
 // nrun_cur.  Returns with the counts in ctx->h_pin + kEqPinWord.
 static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, uint32_t* out_off, EqOut out,
                           EqRunBuf* nrun, uint32_t* nrun_cur, uint64_t n_in, bool counts = true) {
+    // S.fold: the batch's remainder (when there is one) and the folded runs' are merged into the
+    // new run by a second merge launch; the first one then only pops
     EqState& Q = ctx->eq;
     hipStream_t s = ctx->stream;
     const uint32_t H = Q.n_hosts;
@@ -770,11 +794,22 @@ static shd_status eq_pass(shd_ctx* ctx, const EqSrcs& S, uint64_t window_end, ui
     // the popped offsets and the new run's offsets: one hand-written look-back scan launch (scan.h)
     SHD_TRY(scan_excl2(Q.scan, Q.pop_cnt.as<uint32_t>(), out_off, nrun ? Q.keep_cnt.as<uint32_t>() : nullptr,
                        nrun ? nrun->off.as<uint32_t>() : nullptr, H + 1, s));
-    if (n_in) {
+    if (n_in && S.fold) {
+        EqSrcs SP = S, SK = S;
+        SP.b = -1;   // no remainder copy: the keep launch merges the batch's with the folded runs'
+        SP.fold = 0;
+        SK.fold = S.fold | (S.b >= 0 ? 1u << S.b : 0u);
+        SK.b = -1;
+        const uint32_t srt = ctx->knobs.get(K_EQ_SEARCH_ONLY, 0) == 1 ? 0u : 1u;
+        (window_end == ~0ull ? eqr_merge<256> : eqr_merge<kEqStage>)<<<div_up(H, 4), 256, 0, s>>>(
+            H, SP, out_off, out, EqOut{}, nullptr, nullptr, Q.ranges.as<uint2>(), srt, 0u);
+        eqr_merge<256><<<div_up(H, 4), 256, 0, s>>>(H, SK, nrun->off.as<uint32_t>(), nr, EqOut{}, nullptr, nrun_cur,
+                                                     Q.ranges.as<uint2>(), srt, 1u);
+    } else if (n_in) {
         if (ctx->knobs.get(K_EQ_WAVE_MERGE, 1) != 0)   // default: a wave a host (faster on C5, see eqr_merge16)
             (window_end == ~0ull ? eqr_merge<256> : eqr_merge<kEqStage>)<<<div_up(H, 4), 256, 0, s>>>(
                 H, S, out_off, out, nr, nrun ? nrun->off.as<uint32_t>() : nullptr, nrun_cur, Q.ranges.as<uint2>(),
-                ctx->knobs.get(K_EQ_SEARCH_ONLY, 0) == 1 ? 0u : 1u);
+                ctx->knobs.get(K_EQ_SEARCH_ONLY, 0) == 1 ? 0u : 1u, 0u);
         else
             eqr_merge16<<<div_up(H, 16), 256, 0, s>>>(H, S, out_off, out, nr,
                                                       nrun ? nrun->off.as<uint32_t>() : nullptr, nrun_cur,
@@ -970,7 +1005,12 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     for (int r = 0; r < kEqSlots; ++r) live += Q.run[r].live ? 1 : 0;
     const int max_runs = (int)std::min<int64_t>(std::max<int64_t>(ctx->knobs.get(K_EQ_MAX_RUNS, kEqMaxRuns), 2),
                                                 kEqMaxRuns);
-    if (has_b && n_b && live >= max_runs) SHD_TRY(eq_compact(ctx, false));   // room for the batch's run
+    if (has_b && n_b && live >= max_runs) {   // room for the batch's run
+        // default: the compaction rides this advance's pass (the picked runs' remainders merge into
+        // the new run, no pass of its own); SHD_EQ_FOLD=0: a compaction pass first (round 4)
+        if (ctx->knobs.get(K_EQ_FOLD, 1) != 0) Q.fold_next = true;
+        else SHD_TRY(eq_compact(ctx, false));
+    }
     if (adopt) {
         const int t = Q.lend;
         EqRunBuf& R = Q.run[t];
@@ -996,24 +1036,44 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     int slots[kEqSrcMax];
     EqSrcs S = eq_sources(Q, slots);
     const uint32_t n_runs = S.n;
+    // a folded compaction: the half of the runs holding the fewest pending events (as eq_compact)
+    uint64_t n_fold = 0;
+    if (Q.fold_next && n_runs >= 2) {
+        int ord[kEqSrcMax];
+        for (uint32_t k = 0; k < n_runs; ++k) ord[k] = (int)k;
+        std::sort(ord, ord + n_runs, [&](int a, int b) { return Q.run[slots[a]].left < Q.run[slots[b]].left; });
+        const uint32_t tk = ctx->knobs.get(K_EQ_FOLD_TAKE, 0);   // (tuning: runs folded; 0 = half)
+        const uint32_t take = std::min<uint32_t>(n_runs, std::max<uint32_t>(2, tk ? tk : (n_runs + 1) / 2));
+        for (uint32_t i = 0; i < take; ++i) {
+            S.fold |= 1u << ord[i];
+            n_fold += Q.run[slots[ord[i]]].left;
+        }
+    }
+    Q.fold_next = false;
     EqRunBuf* nrun = nullptr;
     int t = -1;
     if (has_b) {
         S.b = (int32_t)S.n;
         S.s[S.n++] = EqSrc{d_batch->ev_off, nullptr, Q.bcut.as<uint32_t>(), d_batch->ev_deliver, d_batch->ev_src,
                            d_batch->ev_seq, nullptr, d_batch->ev_pkt, Q.batches};
+    }
+    if (has_b || S.fold) {   // the new run: the batch's remainder and / or the folded runs'
         t = eq_free_slot(Q);
+        if (t < 0) return SHD_ERR_STATE;
         nrun = &Q.run[t];
-        SHD_TRY(eq_run_alloc(*nrun, H, n_b));
+        SHD_TRY(eq_run_alloc(*nrun, H, n_b + n_fold));
     }
     const EqOut popped{Q.pd.as<uint64_t>(), Q.ps.as<uint32_t>(), Q.pq.as<uint64_t>(), Q.pt.as<uint64_t>()};
     SHD_TRY(eq_pass(ctx, S, window_end, Q.pop_off.as<uint32_t>(), popped, nrun,
-                    has_b ? eq_cursor(Q, 1 - Q.ccur, t) : nullptr, n_in));
+                    nrun ? eq_cursor(Q, 1 - Q.ccur, t) : nullptr, n_in));
     const unsigned long long* wd = ctx->h_pin + kEqPinWord;
     const uint64_t n_pop = wd[1], n_keep = wd[2];
-    uint64_t left = 0;
-    for (uint32_t k = 0; k < S.n; ++k) left += wd[4 + k];
-    if (n_pop + left != n_in || (has_b && wd[4 + S.b] != n_keep)) {   // batch ev_off / n_events disagree
+    uint64_t left = 0, into_new = 0;
+    for (uint32_t k = 0; k < S.n; ++k) {
+        left += wd[4 + k];
+        if ((int32_t)k == S.b || ((S.fold >> k) & 1u)) into_new += wd[4 + k];
+    }
+    if (n_pop + left != n_in || (nrun && into_new != n_keep)) {   // batch ev_off / n_events disagree
         std::fprintf(stderr, "shd_equeue_advance: counts disagree: popped %llu + left %llu != in %llu "
                      "(pending %llu, batch %llu, runs %u, batch kept %llu vs %llu)\n",
                      (unsigned long long)n_pop, (unsigned long long)left, (unsigned long long)n_in,
@@ -1024,15 +1084,16 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
     // commit: cursors moved to the cut buffer; drained runs dropped; the batch's remainder is a run
     for (uint32_t k = 0; k < n_runs; ++k) {
         EqRunBuf& R = Q.run[slots[k]];
-        R.left = wd[4 + k];
+        const bool folded = (S.fold >> k) & 1u;   // its remainder moved into the new run
+        R.left = folded ? 0 : wd[4 + k];
         R.live = R.left > 0;
         R.fresh = false;   // its cursor is in the cut buffer now
     }
-    if (has_b) {
+    if (nrun) {
         nrun->n = nrun->left = n_keep;
         nrun->live = n_keep > 0;
-        ++Q.batches;
     }
+    if (has_b) ++Q.batches;
     Q.ccur = 1 - Q.ccur;
     Q.n_pending = left;
     Q.n_popped = n_pop;
