@@ -99,6 +99,7 @@ struct EqState {   // destination event queues (equeue.hip): a list of sorted ru
     int lend = -1;                  // the slot handed out by shd_equeue_batch_buffers (not live yet)
     bool fold_next = false;         // the next pass folds a compaction in (the run limit was reached)
     uint64_t lend_cap = 0;          // events the lent slot holds
+    uint64_t cap_hint = 0;          // the largest run capacity grown so far (every later growth takes it)
     DevBuf curs[2];                 // [kEqSlots][n_hosts] u32 cursors (first unpopped), double-buffered
     DevBuf bcut;                    // [n_hosts] the batch's first kept event per host
     DevBuf pd, ps, pq, pt;          // the last call's popped events

@@ -743,12 +743,16 @@ __global__ __launch_bounds__(1024) void eq_totals(uint32_t n_hosts, uint32_t n_p
 
 // a stored run's event arrays for n events (the ensure keeps growth headroom: slots are reused
 // round after round)
-static shd_status eq_run_alloc(EqRunBuf& r, uint32_t n_hosts, uint64_t n) {
+static shd_status eq_run_alloc(EqState& Q, EqRunBuf& r, uint32_t n_hosts, uint64_t n) {
     // room for half as many again: the runs' sizes wander from round to round, and a regrowth
-    // (hipFree + hipMalloc of ~0.5 GB of arrays) inside an advance cost ~0.3 ms (C5: 0.78 ms rounds)
+    // (hipFree + hipMalloc of ~0.5 GB of arrays) inside an advance cost ~0.3 ms (C5: 0.78 ms rounds);
+    // and at least the largest capacity any slot has grown to, so the slots reach their steady
+    // size in one growth each instead of several (the slots take turns as batch, remainder and
+    // compaction runs of different sizes)
     const size_t m = std::max<uint64_t>(n, 1);
-    if (r.deliver.bytes < m * 8) {
-        const size_t g = m + m / 2;
+    if (r.deliver.bytes < m * 8 || r.src.bytes < m * 4 || r.seq.bytes < m * 8 || r.tag.bytes < m * 8) {
+        const size_t g = std::max<size_t>(m + m / 2, Q.cap_hint);
+        Q.cap_hint = g;
         SHD_TRY(r.deliver.ensure(g * 8));
         SHD_TRY(r.src.ensure(g * 4));
         SHD_TRY(r.seq.ensure(g * 8));
@@ -882,7 +886,7 @@ static shd_status eq_compact(shd_ctx* ctx, bool all) {
     if (S.n == 0) return SHD_OK;
     const int t = eq_free_slot(Q);
     EqRunBuf& T = Q.run[t];
-    SHD_TRY(eq_run_alloc(T, Q.n_hosts, n));
+    SHD_TRY(eq_run_alloc(Q, T, Q.n_hosts, n));
     // every pending event of the picked runs moves (window ~0): n, known here, so the pass runs
     // without its totals and read-back -- the advance's own pass follows on the stream
     SHD_TRY(eq_pass(ctx, S, ~0ull, T.off.as<uint32_t>(), eq_run_out(T), nullptr, nullptr, n, false));
@@ -956,10 +960,14 @@ shd_status shd_equeue_batch_buffers(shd_ctx* ctx, uint64_t max_events, shd_relay
     EqRunBuf& R = Q.run[t];
     const size_t m = std::max<uint64_t>(max_events, 1);
     SHD_TRY(R.off.ensure((size_t)(Q.n_hosts + 1) * 4));
-    SHD_TRY(R.deliver.ensure(m * 8));
-    SHD_TRY(R.src.ensure(m * 4));
-    SHD_TRY(R.seq.ensure(m * 8));
-    SHD_TRY(R.pkt.ensure(m * 4));
+    if (R.deliver.bytes < m * 8) {   // a growth takes the slots' largest capacity (eq_run_alloc)
+        const size_t g = std::max<size_t>(m, Q.cap_hint);
+        Q.cap_hint = g;
+        SHD_TRY(R.deliver.ensure(g * 8));
+        SHD_TRY(R.src.ensure(g * 4));
+        SHD_TRY(R.seq.ensure(g * 8));
+    }
+    SHD_TRY(R.pkt.ensure(std::max<size_t>(m, R.deliver.bytes / 8) * 4));
     Q.lend = t;
     Q.lend_cap = m;   // the relay refuses a round of more events than this into the slot
     out->ev_off = R.off.as<uint32_t>();
@@ -1061,7 +1069,7 @@ shd_status shd_equeue_advance(shd_ctx* ctx, const shd_relay_out* d_batch, uint64
         t = eq_free_slot(Q);
         if (t < 0) return SHD_ERR_STATE;
         nrun = &Q.run[t];
-        SHD_TRY(eq_run_alloc(*nrun, H, n_b + n_fold));
+        SHD_TRY(eq_run_alloc(Q, *nrun, H, n_b + n_fold));
     }
     const EqOut popped{Q.pd.as<uint64_t>(), Q.ps.as<uint32_t>(), Q.pq.as<uint64_t>(), Q.pt.as<uint64_t>()};
     SHD_TRY(eq_pass(ctx, S, window_end, Q.pop_off.as<uint32_t>(), popped, nrun,
