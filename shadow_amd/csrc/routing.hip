@@ -457,7 +457,12 @@ __device__ __forceinline__ void sssp_row(
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t grp = lane / G, gl = lane % G;
     uint32_t* q = wq + wave * kQStride;
-    const uint32_t src = used ? used[row] : row;   // (nullptr: every node used, in index order)
+    // (LDS kernels: nullptr = every node used, in index order; the global-label kernel always
+    // passes the array -- a runtime check there cost the one VGPR above 128 that halves its
+    // residency: C4 rows 0-4095 17.3 -> 27.2 ms)
+    uint32_t src;
+    if constexpr (GLAB) src = used[row];
+    else src = used ? used[row] : row;
 #ifdef SHD_SSSP_PROF
     uint64_t ss_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ss_t = __builtin_amdgcn_s_memtime();
 #endif
@@ -824,7 +829,7 @@ __device__ __forceinline__ void sssp_row(
         if (GLAB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         for (uint32_t j = tid; j < n_used; j += BLOCK) {
-            const uint32_t v = used ? used[j] : j;
+            const uint32_t v = GLAB || used ? used[j] : j;
             uint32_t nh = 0xFFFFFFFFu;
             if (v == src) {
                 nh = src;
@@ -850,7 +855,7 @@ __device__ __forceinline__ void sssp_row(
 #pragma unroll
         for (uint32_t i = 0; i < kOut; ++i) {
             const uint32_t j = j0 + i * BLOCK;
-            uj[i] = j < n_used ? (used ? used[j] : j) : 0u;
+            uj[i] = j < n_used ? (GLAB || used ? used[j] : j) : 0u;
         }
 #pragma unroll
         for (uint32_t i = 0; i < kOut; ++i) {
@@ -932,6 +937,9 @@ __global__ __launch_bounds__(BLOCK) void sssp_lds_group(
 // nodes = 400 KB per source).  A persistent grid of slots: slot b owns the label array
 // glab[b*V, (b+1)*V) and walks rows row_begin + b, + gridDim.x, ...; the bitmap and the queues
 // stay in LDS (V/8 bytes).
+// (Two slots per CU need <= 128 VGPRs at BLOCK = 512; the kernel sits at exactly 128, so any
+// added live value halves its residency -- check .vgpr_count after changes to sssp_row.  A
+// waves-per-EU launch bound keeps the count but schedules worse: C4 rows 0-4095 17.4 -> 18.5 ms.)
 template <int BLOCK, int G, int R, bool FASTG>
 __global__ __launch_bounds__(BLOCK) void sssp_global_group(
     const uint32_t* __restrict__ abeg, const uint32_t* __restrict__ aend,
@@ -2475,6 +2483,18 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
 }
 
 }  // namespace shd
+
+// Test hook (not part of the ABI header): the vector registers of the shipped SSSP kernels,
+// which sit at the budgets their residency needs (tests/test_routing_gpu.py): 0 = C4's global-
+// label kernel (two 512-thread slots per CU: <= 128), 1 = C2's padded-list kernel (four 256-thread
+// workgroups per CU: <= 128), 2 = C3's 1024-thread kernel (<= 128)
+extern "C" int shd_debug_kernel_vgprs(int which) {
+    hipFuncAttributes at{};
+    const void* f = which == 0   ? reinterpret_cast<const void*>(&shd::sssp_global_group<512, 4, 4, true>)
+                    : which == 1 ? reinterpret_cast<const void*>(&shd::sssp_lds_group<256, 8, 4, true, 8, false>)
+                                 : reinterpret_cast<const void*>(&shd::sssp_lds_group<1024, 4, 2, false, 0, false>);
+    return hipFuncGetAttributes(&at, f) == hipSuccess ? at.numRegs : -1;
+}
 
 #ifdef SHD_SSSP_PROF
 extern "C" int shd_debug_sssp_prof(unsigned long long* out, int reset) {

@@ -360,3 +360,16 @@ def test_prune_complete_graphs(engine, knob, n, mode, dense_build, shape):
     t = engine_graph_from_edges(el).compute_shortest_paths(used, engine, algo=2)
     _assert_table(t, lat, loss.view(np.uint32))
     assert engine.last_info()["algo_used"] == 2
+
+
+@pytest.mark.parametrize("which", [0, 1, 2])
+def test_sssp_kernels_within_register_budget(engine, which):
+    """The SSSP kernels sit at the register budgets their residency needs (two 512-thread slots
+    per CU for C4's global-label kernel, four 256-thread workgroups for C2's, one 1024-thread
+    workgroup for C3's: <= 128 VGPRs each); one register more halves C4's residency (round 5: a
+    null check in the shared row code did, C4 rows 0-4095 17.3 -> 27.2 ms)."""
+    import ctypes as C
+    lib = engine.lib
+    lib.shd_debug_kernel_vgprs.restype = C.c_int
+    n = lib.shd_debug_kernel_vgprs(which)
+    assert 0 < n <= 128, n
