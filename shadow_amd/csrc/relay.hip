@@ -394,6 +394,22 @@ __global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint32_t* __rest
     s_nd[lane] = nd;
     uint32_t mx = nd;
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the store pattern below: kDrawSlice lanes per host write its kDrawSlice consecutive draws
+    // (4 B each), 64 / kDrawSlice hosts per step.  The hosts' (count, start) a lane stores for
+    // are the same every slice: read once into registers (read per store, each store waited on
+    // two dependent LDS round trips: C5 K0 alone 34.6 -> 30.1 us)
+    constexpr uint32_t kG = kDrawSlice, kHpg = 64 / kDrawSlice;
+    const uint32_t kl = lane % kDrawSlice;
+    uint32_t g_nd[kG], g_beg[kG];
+#pragma unroll
+    for (uint32_t g = 0; g < kG; ++g) {
+        const uint32_t hl = g * kHpg + lane / kDrawSlice;
+        g_nd[g] = s_nd[hl];
+        g_beg[g] = s_beg[hl];
+    }
     for (uint32_t j0 = 0; j0 < mx; j0 += kDrawSlice) {
 #pragma unroll
         for (uint32_t k = 0; k < kDrawSlice; ++k)
@@ -401,12 +417,12 @@ __global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint32_t* __rest
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // kDrawSlice lanes per host write its kDrawSlice consecutive draws (4 B each)
+        uint32_t v[kG];
 #pragma unroll
-        for (uint32_t g = 0; g < 64 * kDrawSlice / 64; ++g) {
-            const uint32_t hl = g * (64 / kDrawSlice) + lane / kDrawSlice, k = lane % kDrawSlice;
-            if (j0 + k < s_nd[hl]) draw[s_beg[hl] + j0 + k] = s[k][hl];
-        }
+        for (uint32_t g = 0; g < kG; ++g) v[g] = s[kl][g * kHpg + lane / kDrawSlice];
+#pragma unroll
+        for (uint32_t g = 0; g < kG; ++g)
+            if (j0 + kl < g_nd[g]) draw[g_beg[g] + j0 + kl] = v[g];
         __builtin_amdgcn_wave_barrier();
     }
     if (hl < a.n_src) {
@@ -2071,12 +2087,18 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     a.n_bins = n_bins;
     uint32_t* seg = R.bin_cnt.as<uint32_t>() + (size_t)G * kHistSplit * n_bins;
     a.seg_pre = seg;
-    // K0 goes first: with the draws kept as 4 bytes and the histogram at 30 us, K0 plus the
-    // stream join (~12 us from its end to the stamp's start) was the longer of the two chains, so
-    // its fork is issued before anything else.  The fork event follows the caller's work on the
-    // stream (e.g. the kernels that wrote the batch).
+    // (side-stream form: K0 goes first -- with the draws kept as 4 bytes and the histogram at 30
+    // us, K0 plus the stream join (~12 us from its end to the stamp's start) was the longer of the
+    // two chains, so its fork is issued before anything else.  The fork event follows the
+    // caller's work on the stream, e.g. the kernels that wrote the batch.)
     const bool k0 = !b->chance && !R.cpu_draws;   // (shd_relay_flush filled the draws from the CPU's)
-    if (k0) {   // K0: the per-host generator streams, on the side stream next to the bins
+    // K0 in line before the histogram (default, round 5): K0 30 us + histogram 21 us back to back
+    // beat K0 beside the histogram (39 ‖ 41 us, each slowed by the other taking wave slots) plus
+    // the fork / join events: C5 round 0.467-0.476 -> 0.457 ms.  SHD_RELAY_K0_INLINE=0: the side stream.
+    const bool k0_inline = k0 && ctx->knobs.get(K_RELAY_K0_INLINE, 1) != 0;
+    if (k0_inline) {
+        relay_draws<<<div_up(R.n_src, 64), 64, 0, s>>>(a, R.draws.as<uint32_t>());
+    } else if (k0) {   // K0: the per-host generator streams, on the side stream next to the bins
         SHD_HIP(hipEventRecord(ctx->sev[0], s));
         SHD_HIP(hipStreamWaitEvent(ctx->side, ctx->sev[0], 0));
         relay_draws<<<div_up(R.n_src, 64), 64, 0, ctx->side>>>(a, R.draws.as<uint32_t>());
@@ -2089,10 +2111,10 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
                                                                              R.bin_cnt.as<uint32_t>());
     else
         relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
-    if (k0) SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));   // after the histogram's launch
+    if (k0 && !k0_inline) SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));   // after the histogram's launch
     bin_col_scan<<<div_up(n_bins, 64), 1024, 0, s>>>(G, n_bins, R.bin_cnt.as<uint32_t>(), seg, tot, a.red);
     bin_base_scan<<<1, 1024, 0, s>>>(n_bins, tot, R.bin_base.as<uint32_t>(), R.bin_lb.as<unsigned long long>(), a.red);
-    if (k0) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
+    if (k0 && !k0_inline) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
     relay_stamp_v6<true><<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4, s>>>(
         a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     if (xsh) {
