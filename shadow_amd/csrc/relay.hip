@@ -368,10 +368,18 @@ constexpr uint32_t kDrawSlice = SHD_DRAW_SLICE;   // draws per host per LDS tran
 // draws iff now < sim_end (worker.rs:334-341); send times are non-decreasing within a host (a
 // host's sends happen in simulated-time order; the stamp checks it), so the drawing sends are a
 // prefix of the host's range, found from its last send (binary search when it is skipped).
-__global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint32_t* __restrict__ draw) {
-    __shared__ uint32_t s[kDrawSlice][65];   // the draws' top 32 bits (draw_drops)
-    __shared__ uint32_t s_beg[64], s_nd[64];
-    const uint32_t lane = threadIdx.x, hl = blockIdx.x * 64 + lane, h = a.src_lo + hl;
+#ifndef SHD_K0_WAVES
+#define SHD_K0_WAVES 1
+#endif
+constexpr uint32_t kK0Waves = SHD_K0_WAVES;   // waves (64 hosts each) per K0 workgroup
+__global__ __launch_bounds__(64 * kK0Waves) void relay_draws(RelayArgs3 a, uint32_t* __restrict__ draw) {
+    __shared__ uint32_t s_all[kK0Waves][kDrawSlice][65];   // the draws' top 32 bits (draw_drops)
+    __shared__ uint32_t s_beg_all[kK0Waves][64], s_nd_all[kK0Waves][64];
+    const uint32_t wv = threadIdx.x >> 6;
+    auto& s = s_all[wv];
+    uint32_t* s_beg = s_beg_all[wv];
+    uint32_t* s_nd = s_nd_all[wv];
+    const uint32_t lane = threadIdx.x & 63, hl = (blockIdx.x * kK0Waves + wv) * 64 + lane, h = a.src_lo + hl;
     uint32_t nd = 0;
     Xoshiro r{0, 0, 0, 0};
     if (hl < a.n_src) {
@@ -411,9 +419,17 @@ __global__ __launch_bounds__(64) void relay_draws(RelayArgs3 a, uint32_t* __rest
         g_beg[g] = s_beg[hl];
     }
     for (uint32_t j0 = 0; j0 < mx; j0 += kDrawSlice) {
+        // the slice's draws in registers first, then to LDS together: a draw written to LDS as it
+        // came made the next draw wait for that write (its registers were reused), an LDS round
+        // trip per draw on the generator's chain
+        uint32_t dv[kDrawSlice];
 #pragma unroll
-        for (uint32_t k = 0; k < kDrawSlice; ++k)
-            if (j0 + k < nd) s[k][lane] = (uint32_t)(r.next() >> 32);
+        for (uint32_t k = 0; k < kDrawSlice; ++k) {
+            dv[k] = 0u;
+            if (j0 + k < nd) dv[k] = (uint32_t)(r.next() >> 32);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kDrawSlice; ++k) s[k][lane] = dv[k];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1973,7 +1989,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     RelayArgs3 a = relay_args3(ctx, b, rd, o);
     const uint64_t* seq_base = a.abs_seq ? nullptr : R.next_id.as<uint64_t>();
     if (!b->chance && !R.cpu_draws && R.n_src)   // K0: the per-host generator streams
-        relay_draws<<<div_up(R.n_src, 64), 64, 0, s>>>(a, R.draws.as<uint32_t>());
+        relay_draws<<<div_up(R.n_src, 64 * kK0Waves), 64 * kK0Waves, 0, s>>>(a, R.draws.as<uint32_t>());
     if (R.n_src == 0) {
     } else if (R.hn_bits) {   // host -> node map fits the LDS: persistent stamp, no node gathers
         const uint32_t groups = div_up(R.n_src, kS5Hosts);
@@ -2097,11 +2113,11 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     // the fork / join events: C5 round 0.467-0.476 -> 0.457 ms.  SHD_RELAY_K0_INLINE=0: the side stream.
     const bool k0_inline = k0 && ctx->knobs.get(K_RELAY_K0_INLINE, 1) != 0;
     if (k0_inline) {
-        relay_draws<<<div_up(R.n_src, 64), 64, 0, s>>>(a, R.draws.as<uint32_t>());
+        relay_draws<<<div_up(R.n_src, 64 * kK0Waves), 64 * kK0Waves, 0, s>>>(a, R.draws.as<uint32_t>());
     } else if (k0) {   // K0: the per-host generator streams, on the side stream next to the bins
         SHD_HIP(hipEventRecord(ctx->sev[0], s));
         SHD_HIP(hipStreamWaitEvent(ctx->side, ctx->sev[0], 0));
-        relay_draws<<<div_up(R.n_src, 64), 64, 0, ctx->side>>>(a, R.draws.as<uint32_t>());
+        relay_draws<<<div_up(R.n_src, 64 * kK0Waves), 64 * kK0Waves, 0, ctx->side>>>(a, R.draws.as<uint32_t>());
     }
     // the histogram's first block also resets the round's reductions (red_init's job: one
     // launch less; only the scans and the stamp read them, all after the histogram)
