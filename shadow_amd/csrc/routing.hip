@@ -1251,36 +1251,36 @@ __global__ __launch_bounds__(BLOCK) void prune_rows(
             }
             if (tid == 0) cnt[6] = taken;
         }
-      __syncthreads();
-      const uint32_t nsel = min((uint32_t)K, cnt[5] + cnt[6]);
-      for (uint32_t j = nsel + tid; j < (uint32_t)K; j += BLOCK) {   // unused slots: no detour
-          selx[j] = 0u;
-          sela[j] = kLat32Inf;
-      }
-      if (tid == 0) cnt[0] = 0;
-      if constexpr (CMP) {   // detours in ascending latency (ties by index): wave 0 ranks them
         __syncthreads();
-        uint32_t* tx = hist;   // the histogram is spent; K <= 128 pairs fit its 256 words
-        uint32_t* ta = hist + K;
-        if (tid < 64) {
-            for (uint32_t i = lane; i < (uint32_t)K; i += 64) {
-                const uint32_t ai = sela[i], xi = selx[i];
-                uint32_t r = 0;
-                for (uint32_t j = 0; j < (uint32_t)K; ++j) {
-                    const uint32_t aj = sela[j], xj = selx[j];
-                    r += aj < ai || (aj == ai && (xj < xi || (xj == xi && j < i))) ? 1u : 0u;
+        const uint32_t nsel = min((uint32_t)K, cnt[5] + cnt[6]);
+        for (uint32_t j = nsel + tid; j < (uint32_t)K; j += BLOCK) {   // unused slots: no detour
+            selx[j] = 0u;
+            sela[j] = kLat32Inf;
+        }
+        if (tid == 0) cnt[0] = 0;
+        if constexpr (CMP) {   // detours in ascending latency (ties by index): wave 0 ranks them
+            __syncthreads();
+            uint32_t* tx = hist;   // the histogram is spent; K <= 128 pairs fit its 256 words
+            uint32_t* ta = hist + K;
+            if (tid < 64) {
+                for (uint32_t i = lane; i < (uint32_t)K; i += 64) {
+                    const uint32_t ai = sela[i], xi = selx[i];
+                    uint32_t r = 0;
+                    for (uint32_t j = 0; j < (uint32_t)K; ++j) {
+                        const uint32_t aj = sela[j], xj = selx[j];
+                        r += aj < ai || (aj == ai && (xj < xi || (xj == xi && j < i))) ? 1u : 0u;
+                    }
+                    tx[r] = xi;
+                    ta[r] = ai;
                 }
-                tx[r] = xi;
-                ta[r] = ai;
             }
+            __syncthreads();
+            for (uint32_t j = tid; j < (uint32_t)K; j += BLOCK) {
+                selx[j] = tx[j];
+                sela[j] = ta[j];
+            }
+            if (tid == 0) cnt[7] = 0;   // survivors of the first batch
         }
-        __syncthreads();
-        for (uint32_t j = tid; j < (uint32_t)K; j += BLOCK) {
-            selx[j] = tx[j];
-            sela[j] = ta[j];
-        }
-        if (tid == 0) cnt[7] = 0;   // survivors of the first batch
-      }
     }
     __syncthreads();
     PR_MARK(3);
