@@ -371,6 +371,11 @@ constexpr uint32_t kDrawSlice = SHD_DRAW_SLICE;   // draws per host per LDS tran
 #ifndef SHD_K0_WAVES
 #define SHD_K0_WAVES 1
 #endif
+#ifdef SHD_STAMP_PROF
+// K0 (relay_draws, tuning builds): per wave, shader clocks of setup / draws / stores and its
+// 100 MHz start / end (tools/k0_prof.py)
+__device__ unsigned long long g_k0_prof[4096][5];
+#endif
 constexpr uint32_t kK0Waves = SHD_K0_WAVES;   // waves (64 hosts each) per K0 workgroup
 __global__ __launch_bounds__(64 * kK0Waves) void relay_draws(RelayArgs3 a, uint32_t* __restrict__ draw) {
     __shared__ uint32_t s_all[kK0Waves][kDrawSlice][65];   // the draws' top 32 bits (draw_drops)
@@ -380,6 +385,13 @@ __global__ __launch_bounds__(64 * kK0Waves) void relay_draws(RelayArgs3 a, uint3
     uint32_t* s_beg = s_beg_all[wv];
     uint32_t* s_nd = s_nd_all[wv];
     const uint32_t lane = threadIdx.x & 63, hl = (blockIdx.x * kK0Waves + wv) * 64 + lane, h = a.src_lo + hl;
+#ifdef SHD_STAMP_PROF
+    const uint64_t k0_t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t k0_c = __builtin_amdgcn_s_memtime(), k0_acc[3] = {0, 0, 0};
+#define K0_MARK(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); k0_acc[i] += t_ - k0_c; k0_c = t_; } while (0)
+#else
+#define K0_MARK(i) do { } while (0)
+#endif
     uint32_t nd = 0;
     Xoshiro r{0, 0, 0, 0};
     if (hl < a.n_src) {
@@ -409,6 +421,7 @@ __global__ __launch_bounds__(64 * kK0Waves) void relay_draws(RelayArgs3 a, uint3
     // (4 B each), 64 / kDrawSlice hosts per step.  The hosts' (count, start) a lane stores for
     // are the same every slice: read once into registers (read per store, each store waited on
     // two dependent LDS round trips: C5 K0 alone 34.6 -> 30.1 us)
+    K0_MARK(0);
     constexpr uint32_t kG = kDrawSlice, kHpg = 64 / kDrawSlice;
     const uint32_t kl = lane % kDrawSlice;
     uint32_t g_nd[kG], g_beg[kG];
@@ -428,6 +441,7 @@ __global__ __launch_bounds__(64 * kK0Waves) void relay_draws(RelayArgs3 a, uint3
             dv[k] = 0u;
             if (j0 + k < nd) dv[k] = (uint32_t)(r.next() >> 32);
         }
+        K0_MARK(1);
 #pragma unroll
         for (uint32_t k = 0; k < kDrawSlice; ++k) s[k][lane] = dv[k];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -440,6 +454,7 @@ __global__ __launch_bounds__(64 * kK0Waves) void relay_draws(RelayArgs3 a, uint3
         for (uint32_t g = 0; g < kG; ++g)
             if (j0 + kl < g_nd[g]) draw[g_beg[g] + j0 + kl] = v[g];
         __builtin_amdgcn_wave_barrier();
+        K0_MARK(2);
     }
     if (hl < a.n_src) {
         a.rng_out[4 * (size_t)h] = r.s0;
@@ -447,6 +462,19 @@ __global__ __launch_bounds__(64 * kK0Waves) void relay_draws(RelayArgs3 a, uint3
         a.rng_out[4 * (size_t)h + 2] = r.s2;
         a.rng_out[4 * (size_t)h + 3] = r.s3;
     }
+#ifdef SHD_STAMP_PROF
+    {
+        const uint32_t wid = blockIdx.x * kK0Waves + wv;
+        if (lane == 0 && wid < 4096) {
+            g_k0_prof[wid][0] = k0_acc[0];
+            g_k0_prof[wid][1] = k0_acc[1];
+            g_k0_prof[wid][2] = k0_acc[2];
+            g_k0_prof[wid][3] = k0_t0;
+            g_k0_prof[wid][4] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+#endif
+#undef K0_MARK
 }
 
 // A path-table entry from global memory through an explicit global (addrspace 1) pointer.  Next
@@ -3187,6 +3215,9 @@ shd_status shd_path_packet_counts(shd_ctx* ctx, uint64_t* counts) {
 }  // extern "C"
 
 #ifdef SHD_STAMP_PROF
+extern "C" int shd_debug_k0_prof(unsigned long long* out) {   // 4096 x 5 words
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(shd::g_k0_prof), sizeof(unsigned long long) * 4096 * 5) != hipSuccess;
+}
 extern "C" int shd_debug_stamp_prof(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(shd::g_stamp_prof), sizeof(unsigned long long) * 12) != hipSuccess) return 1;
     if (reset) {
