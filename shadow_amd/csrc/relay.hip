@@ -395,6 +395,9 @@ __global__ __launch_bounds__(64 * kK0Waves) void relay_draws(RelayArgs3 a, uint3
     uint32_t nd = 0;
     Xoshiro r{0, 0, 0, 0};
     if (hl < a.n_src) {
+        // the stream's state first: its loads need nothing below, so they share the first trip
+        r = Xoshiro{a.rng[4 * (size_t)h], a.rng[4 * (size_t)h + 1], a.rng[4 * (size_t)h + 2],
+                    a.rng[4 * (size_t)h + 3]};
         const uint32_t b = a.src_off[hl], e = a.src_off[hl + 1];
         nd = e - b;
         if (nd && !(a.send_time[e - 1] < a.sim_end)) {   // first send with now >= sim_end
@@ -406,8 +409,6 @@ __global__ __launch_bounds__(64 * kK0Waves) void relay_draws(RelayArgs3 a, uint3
             nd = lo - b;
         }
         s_beg[lane] = b;
-        r = Xoshiro{a.rng[4 * (size_t)h], a.rng[4 * (size_t)h + 1], a.rng[4 * (size_t)h + 2],
-                    a.rng[4 * (size_t)h + 3]};
     } else {
         s_beg[lane] = 0;
     }
