@@ -159,6 +159,7 @@ struct RelayState {
         ev_deliver, ev_seq, ev_src, ev_pkt, ev_off, dst_cnt, red, rec, brec, tmp, draws,
         bin_cnt, bin_base, bin_lb;
     ScanScratch scan;     // pipeline 1's destination offsets (scan.h)
+    ScanScratch col_scan; // pipeline 7's bin bases (bin_col_scan's look-back states)
     DevBuf rs_counts;     // pipeline 3's radix sort: per-tile digit counts
     ScanScratch rs_scan;
     // sharded rounds: packed outgoing events, exchange words, per-peer offset blocks, what was

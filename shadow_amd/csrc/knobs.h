@@ -18,7 +18,7 @@ namespace shd {
     X(PRUNE_DENSE_BUILD) X(SSSP_HUB) X(SYNC_KERNEL)                                               \
     X(EQ_COUNT_BLOCKS) X(EQ_WAVE_MERGE) X(EQ_SEARCH_ONLY) X(EQ_MAX_RUNS) X(RELAY_GROUP_SENDS) X(HIST_SCALAR) X(B7_STOP) X(RELAY_FORCE_V1)         \
     X(RELAY_FORCE_V3) X(RELAY_NO_LDS_MAP) X(MERGE_BY_EVENT) X(SHARD_CHUNK_ROWS) X(SHARD_REPLICATE_MB)             \
-    X(SHARD_RESERVE_SLOTS) X(RELAY_SHARD_X24) X(FLUSH_COPY) X(PRUNE_SHAPE) X(PRUNE_SHAPE_SH) X(EQ_FOLD) X(EQ_FOLD_TAKE) X(RELAY_K0_INLINE)
+    X(SHARD_RESERVE_SLOTS) X(RELAY_SHARD_X24) X(FLUSH_COPY) X(PRUNE_SHAPE) X(PRUNE_SHAPE_SH) X(EQ_FOLD) X(EQ_FOLD_TAKE) X(RELAY_K0_INLINE) X(RELAY_SCAN2)
 
 enum Knob : int {
 #define SHD_KNOB_ENUM(n) K_##n,

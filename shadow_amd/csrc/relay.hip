@@ -1560,9 +1560,17 @@ __global__ __launch_bounds__(kHist4Threads) void relay_bin_hist4(RelayArgs3 a, u
 // that does not fit the stamp's 8-bit slot counters flags red[6].
 constexpr uint32_t kColMaxG = 256;   // stamp workgroups (one per CU)
 
+// (base != nullptr: bin_base_scan folded in -- each block's 64 bin totals, a wave scan, and a
+// decoupled look-back over the earlier blocks (blockIdx order: at most 128 blocks, all resident)
+// give the bins' record bases; the look-back states carry an epoch (scan.h layout), so they are
+// never cleared.  One launch and one queue gap less per round.)
 __global__ __launch_bounds__(1024) void bin_col_scan(uint32_t G, uint32_t n_bins, const uint32_t* __restrict__ cnt,
                                                      uint32_t* __restrict__ seg, uint32_t* __restrict__ tot,
-                                                     unsigned long long* __restrict__ red) {
+                                                     unsigned long long* __restrict__ red,
+                                                     uint32_t* __restrict__ base = nullptr,
+                                                     unsigned long long* __restrict__ lb = nullptr,
+                                                     unsigned long long* __restrict__ state = nullptr,
+                                                     uint32_t epoch = 0) {
     __shared__ uint32_t s[16][64];
     constexpr uint32_t kPer = kColMaxG / 16;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6, b = blockIdx.x * 64 + lane;
@@ -1599,6 +1607,51 @@ __global__ __launch_bounds__(1024) void bin_col_scan(uint32_t G, uint32_t n_bins
             run += c[i];
         }
         if (w == 15) tot[b] = run;
+    }
+    if (base && w == 15) {   // wave 15 holds the 64 bin totals of this block
+        const uint32_t t = b < n_bins ? run : 0u;
+        if (t > kB7Cap) atomicOr(&red[6], 1ull);
+        uint32_t incl = t;
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        const uint32_t agg = __shfl(incl, 63);
+        const unsigned long long tag = (unsigned long long)epoch << 34;
+        unsigned long long* st = state + 2 + (size_t)blockIdx.x * 2;
+        uint32_t excl = 0;
+        if (blockIdx.x != 0) {
+            if (lane == 0) __hip_atomic_store(st, tag | (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t hi = (int64_t)blockIdx.x - 1;;) {   // 64 earlier blocks a step
+                const int64_t j = hi - (int64_t)lane;
+                const unsigned long long v =
+                    j >= 0 ? __hip_atomic_load(&state[2 + (size_t)j * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                           : tag | (2ull << 32);   // before block 0: an inclusive 0
+                const uint32_t f = (uint32_t)(v >> 32) & 3u;
+                const bool ok = (uint32_t)(v >> 34) == epoch && f != 0;
+                const uint64_t incl_m = __ballot(ok && f == 2), bad_m = __ballot(!ok);
+                const uint32_t fi = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;
+                const uint64_t upto = fi == 64 ? ~0ull : ((2ull << fi) - 1ull);
+                if (bad_m & upto) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                uint32_t add = lane <= fi ? (uint32_t)v : 0u;
+                for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o);
+                excl += add;
+                if (fi < 64) break;
+                hi -= 64;
+            }
+        }
+        if (lane == 0) __hip_atomic_store(st, tag | (2ull << 32) | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (b < n_bins) {
+            base[b] = excl + incl - t;
+            lb[b] = 0;   // bin_sort_v7's look-back states
+        }
+        if (b == n_bins - 1) {
+            base[n_bins] = excl + incl;
+            lb[n_bins] = 0;   // its ticket
+        }
     }
 }
 
@@ -2157,8 +2210,25 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
     else
         relay_bin_hist<<<G * kHistSplit, 256, (size_t)n_bins * 4, s>>>(a, G, R.bin_cnt.as<uint32_t>());
     if (k0 && !k0_inline) SHD_HIP(hipEventRecord(ctx->sev[1], ctx->side));   // after the histogram's launch
-    bin_col_scan<<<div_up(n_bins, 64), 1024, 0, s>>>(G, n_bins, R.bin_cnt.as<uint32_t>(), seg, tot, a.red);
-    bin_base_scan<<<1, 1024, 0, s>>>(n_bins, tot, R.bin_base.as<uint32_t>(), R.bin_lb.as<unsigned long long>(), a.red);
+    if (ctx->knobs.get(K_RELAY_SCAN2, 0) != 0 || div_up(n_bins, 64) > 128) {   // (A/B: two launches)
+        bin_col_scan<<<div_up(n_bins, 64), 1024, 0, s>>>(G, n_bins, R.bin_cnt.as<uint32_t>(), seg, tot, a.red);
+        bin_base_scan<<<1, 1024, 0, s>>>(n_bins, tot, R.bin_base.as<uint32_t>(), R.bin_lb.as<unsigned long long>(), a.red);
+    } else {   // the bases from the column scan's own look-back (bin_col_scan)
+        ScanScratch& SS = R.col_scan;
+        const uint64_t blocks = div_up(n_bins, 64);
+        if (blocks * 16 + 16 > SS.state.bytes) {
+            SHD_TRY(SS.state.ensure(blocks * 16 + 16));
+            SHD_HIP(hipMemsetAsync(SS.state.p, 0, SS.state.bytes, s));
+            SS.epoch = 0;
+        }
+        if (++SS.epoch >= (1u << 30)) {
+            SHD_HIP(hipMemsetAsync(SS.state.p, 0, SS.state.bytes, s));
+            SS.epoch = 1;
+        }
+        bin_col_scan<<<(uint32_t)blocks, 1024, 0, s>>>(G, n_bins, R.bin_cnt.as<uint32_t>(), seg, tot, a.red,
+                                                       R.bin_base.as<uint32_t>(), R.bin_lb.as<unsigned long long>(),
+                                                       SS.state.as<unsigned long long>(), SS.epoch);
+    }
     if (k0 && !k0_inline) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
     relay_stamp_v6<true><<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4, s>>>(
         a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
