@@ -373,3 +373,18 @@ def test_sssp_kernels_within_register_budget(engine, which):
     lib.shd_debug_kernel_vgprs.restype = C.c_int
     n = lib.shd_debug_kernel_vgprs(which)
     assert 0 < n <= 128, n
+
+
+def test_prune_large_complete_graph_matches_unpruned(engine, knob):
+    """The sorted-detour prune at a size whose LDS stage is ~100 KB (3000 nodes): its tables
+    against the unpruned LDS engine's (algo 1) on the same graph -- exact either way."""
+    from shadow_amd import synth
+    el = synth.complete_graph(3000, 5)
+    used = np.arange(3000, dtype=np.uint32)
+    g = engine_graph_from_edges(el)
+    ref = g.compute_shortest_paths(used, engine, algo=1)
+    knob("PRUNE_SHAPE", None)
+    t = g.compute_shortest_paths(used, engine, algo=2)
+    assert engine.last_info()["algo_used"] == 2
+    assert np.array_equal(t.lat, ref.lat)
+    assert np.array_equal(t.loss.view(np.uint32), ref.loss.view(np.uint32))
