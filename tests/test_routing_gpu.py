@@ -375,12 +375,14 @@ def test_sssp_kernels_within_register_budget(engine, which):
     assert 0 < n <= 128, n
 
 
-def test_prune_large_complete_graph_matches_unpruned(engine, knob):
-    """The sorted-detour prune at a size whose LDS stage is ~100 KB (3000 nodes): its tables
-    against the unpruned LDS engine's (algo 1) on the same graph -- exact either way."""
+@pytest.mark.parametrize("n", [3000, 4096])
+def test_prune_large_complete_graph_matches_unpruned(engine, knob, n):
+    """The sorted-detour prune at sizes whose LDS stage is ~100-140 KB (3000 nodes, and 4096 =
+    kPruneMaxV): its tables against the unpruned LDS engine's (algo 1) on the same graph --
+    exact either way."""
     from shadow_amd import synth
-    el = synth.complete_graph(3000, 5)
-    used = np.arange(3000, dtype=np.uint32)
+    el = synth.complete_graph(n, 5)
+    used = np.arange(n, dtype=np.uint32)
     g = engine_graph_from_edges(el)
     ref = g.compute_shortest_paths(used, engine, algo=1)
     knob("PRUNE_SHAPE", None)
