@@ -252,21 +252,58 @@ def sssp_roofline(n, arcs, V, ms):
                     "(SURVEY 8(d))", "bytes": b}
 
 
+def cpu_info():
+    """The host the CPU baselines ran on (CPU model, nproc, threads used)."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff}
+
+
+TIDY_WHAT = "tidy: the same Dijkstra, used-node bitmap instead of Vec::contains, dense table written directly"
+FAITHFUL_WHAT = "faithful: heap Dijkstra + Vec::contains filter + HashMap materialisation (graph/mod.rs:192-230)"
+
+
 def cpu_rows_baseline(el, rows, n_total, what):
-    """Faithful C restatement (per-source heap Dijkstra + Vec::contains filter + HashMap) on a
-    contiguous sample of source rows, all host cores; extrapolated to the whole build."""
+    """The C restatement on a contiguous sample of source rows, all host cores, extrapolated to
+    the whole build: the faithful variant (value) and the tidy one beside it."""
     from oracle import corc
     used = np.arange(el.n_nodes, dtype=np.uint32)
     threads = corc.max_threads()
-    t0 = time.perf_counter()
-    code, lat, loss, _ = corc.routing(el.n_nodes, el.src, el.dst, el.latency_ns, el.packet_loss, el.directed,
-                                      used, variant=corc.FAITHFUL, threads=threads, rows=rows)
-    dt = time.perf_counter() - t0
     k = rows[1] - rows[0]
-    full_s = dt * n_total / k
-    return dict(value=n_total * n_total / full_s, unit="node-pairs/s", cores=threads, kind="port",
-                sample=f"{what}: source rows {rows[0]}-{rows[1] - 1} ({k} of {n_total}) in {dt:.2f} s, "
-                       f"extrapolated x{n_total / k:.0f} (faithful: heap Dijkstra + Vec::contains + HashMap)"), lat, loss
+    out = {}
+    for name, variant in (("faithful", corc.FAITHFUL), ("tidy", corc.TIDY)):
+        t0 = time.perf_counter()
+        code, lat, loss, _ = corc.routing(el.n_nodes, el.src, el.dst, el.latency_ns, el.packet_loss, el.directed,
+                                          used, variant=variant, threads=threads, rows=rows)
+        dt = time.perf_counter() - t0
+        out[name] = (n_total * n_total / (dt * n_total / k), dt, lat, loss)
+    v, dt, lat, loss = out["faithful"]
+    tv, tdt, tlat, tloss = out["tidy"]
+    cb = dict(value=v, unit="node-pairs/s", cores=threads, kind="port", variant="faithful",
+              sample=f"{what}: source rows {rows[0]}-{rows[1] - 1} ({k} of {n_total}) in {dt:.2f} s, "
+                     f"extrapolated x{n_total / k:.0f} ({FAITHFUL_WHAT})",
+              tidy=dict(value=tv, unit="node-pairs/s", cores=threads, kind="port",
+                        sample=f"the same rows in {tdt:.2f} s ({TIDY_WHAT})"), **cpu_info())
+    return cb, (lat, loss), (tlat, tloss)
+
+
+def cpu_bit_exact(cb, faithful, tidy, glat, gloss):
+    """bit_exact_vs_gpu of both CPU variants against the GPU rows (latency and loss bits)."""
+    def same(t):
+        return bool(np.array_equal(t[0], glat) and np.array_equal(t[1].view(np.uint32), gloss.view(np.uint32)))
+    cb["bit_exact_vs_gpu"] = same(faithful)
+    cb["tidy"]["bit_exact_vs_gpu"] = same(tidy)
 
 
 def c2_engines(eng, el, reps=5):
@@ -332,9 +369,8 @@ def c3_leg(eng, reps=2, cpu=True):
     out = dict(workload="C3: 10k-node Barabasi-Albert m=3 + self-loops, all 10k rows",
                nodes=n, arcs=arcs, node_pairs_per_s=n * n / (best * 1e-3), algorithms=res)
     if cpu:
-        cb, clat, closs = cpu_rows_baseline(el, (0, 256), n, "C3")
-        cb["bit_exact_vs_gpu"] = bool(np.array_equal(clat, lat[:256].cpu().numpy().view(np.uint64)) and
-                                      np.array_equal(closs.view(np.uint32), loss[:256].cpu().numpy().view(np.uint32)))
+        cb, fa, ti = cpu_rows_baseline(el, (0, 256), n, "C3")
+        cpu_bit_exact(cb, fa, ti, lat[:256].cpu().numpy().view(np.uint64), loss[:256].cpu().numpy())
         out["cpu_baseline"] = cb
     del lat, loss
     torch.cuda.empty_cache()
@@ -381,10 +417,9 @@ def c4_leg(eng, world, rank, steps, gather=True, cpu=True):
         # the LAST 64 rows: the persistent kernel's slots take every row past the grid (the first
         # 2 x n_cu rows) from the row counter, so these are claimed rows, not a slot's first row
         lo = n - 64
-        cb, clat, closs = cpu_rows_baseline(el, (lo, n), n, "C4")
+        cb, fa, ti = cpu_rows_baseline(el, (lo, n), n, "C4")
         lat, loss = r["lat_dev"], r["loss_dev"]
-        cb["bit_exact_vs_gpu"] = bool(np.array_equal(clat, lat[lo:].cpu().numpy().view(np.uint64)) and
-                                      np.array_equal(closs.view(np.uint32), loss[lo:].cpu().numpy().view(np.uint32)))
+        cpu_bit_exact(cb, fa, ti, lat[lo:].cpu().numpy().view(np.uint64), loss[lo:].cpu().numpy())
         cb["rows_checked"] = [lo, n]
         out["cpu_baseline"] = cb
     del r
@@ -620,12 +655,14 @@ def flush_e2e(eng, rl, lat_table, loss_table, setup, reps=3, n_threads=16):
             flush()
         ms12 = (time.perf_counter() - t0) / reps * 1e3
         out.event_bytes = 16
+        same12 = bool(len(e12) == len(e16) and np.array_equal(e12, e16[:, [0, 2, 3]]) and
+                      np.array_equal(host_of_send[e12[:, 2]], e16[:, 1]))
+        ok = bool(ok) and same12   # a wrong 12-byte event form fails the bench (advisor, round 5)
         return ({"ms_per_round": ms, "packets_per_s": P / (ms * 1e-3), "pcie_bytes": moved, "first_call_ms": first_ms,
                  "stages": n_threads, "bit_exact_vs_cpu_chance": bool(ok),
                  "events12": {"ms_per_round": ms12, "packets_per_s": P / (ms12 * 1e-3),
                               "pcie_bytes": moved - ns12 * 4,
-                              "same_as_16_byte_events": bool(len(e12) == len(e16) and np.array_equal(
-                                  e12, e16[:, [0, 2, 3]]) and np.array_equal(host_of_send[e12[:, 2]], e16[:, 1])),
+                              "same_as_16_byte_events": same12,
                               "what": "event_bytes = 12: {deliver_off, seq_off, send} (the source host is the "
                                       "send's run's)"},
                  "what": "shd_relay_flush: 16 worker threads' pinned staging buffers (runs + 12-byte sends with the "
@@ -640,21 +677,29 @@ def torch_pinned_u8(n):
     return torch.empty(max(int(n), 1), dtype=torch.uint8).pin_memory()
 
 
-def cpu_baseline_routing(el, budget_s=8.0):
+def cpu_baseline_routing(el, budget_s=6.0):
+    """Full C2 builds by the C restatement, OpenMP over sources, all host cores: the faithful
+    variant (value) and the tidy one beside it; each variant's last table returned."""
     from oracle import corc
     used = np.arange(el.n_nodes, dtype=np.uint32)
     threads = corc.max_threads()
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        code, lat, loss, _ = corc.routing(el.n_nodes, el.src, el.dst, el.latency_ns, el.packet_loss,
-                                          el.directed, used, variant=corc.FAITHFUL, threads=threads)
-        reps += 1
-        if time.perf_counter() - t0 > budget_s or reps >= 20:
-            break
-    dt = (time.perf_counter() - t0) / reps
-    return dict(value=el.n_nodes ** 2 / dt, unit="node-pairs/s", cores=threads, kind="port",
-                sample=f"{reps} full C2 builds (faithful variant: per-source heap Dijkstra + "
-                       f"Vec::contains filter + HashMap materialisation, OpenMP over sources)"), lat
+    out = {}
+    for name, variant in (("faithful", corc.FAITHFUL), ("tidy", corc.TIDY)):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            code, lat, loss, _ = corc.routing(el.n_nodes, el.src, el.dst, el.latency_ns, el.packet_loss,
+                                              el.directed, used, variant=variant, threads=threads)
+            reps += 1
+            if time.perf_counter() - t0 > budget_s or reps >= 20:
+                break
+        out[name] = ((time.perf_counter() - t0) / reps, reps, lat, loss)
+    dt, reps, lat, loss = out["faithful"]
+    tdt, treps, tlat, tloss = out["tidy"]
+    cb = dict(value=el.n_nodes ** 2 / dt, unit="node-pairs/s", cores=threads, kind="port", variant="faithful",
+              sample=f"{reps} full C2 builds ({FAITHFUL_WHAT}; OpenMP over sources)",
+              tidy=dict(value=el.n_nodes ** 2 / tdt, unit="node-pairs/s", cores=threads, kind="port",
+                        sample=f"{treps} full C2 builds ({TIDY_WHAT})"), **cpu_info())
+    return cb, (lat, loss), (tlat, tloss)
 
 
 def cpu_baseline_relay(rl, lat_table, loss_table, budget_s=8.0):
@@ -1000,8 +1045,8 @@ def main():
                              "(A = arcs before pruning: the reference's Dijkstra work)"},
     }
     if cpu:
-        cb, lat_cpu = cpu_baseline_routing(r["el"])
-        cb["bit_exact_vs_gpu"] = bool(np.array_equal(lat_cpu, r["lat"]))
+        cb, fa, ti = cpu_baseline_routing(r["el"])
+        cpu_bit_exact(cb, fa, ti, r["lat"], r["loss"])
         res["cpu_baseline"] = cb
     checks = {}
     if world > 1:   # the multi-GPU run checks itself: every rank's whole table against the C restatement

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define SHD_ABI_VERSION 2
+#define SHD_ABI_VERSION 3
 
 typedef enum shd_status {
     SHD_OK = 0,
@@ -343,7 +343,12 @@ typedef struct shd_event12 {
     uint32_t send;
 } shd_event12;
 
+/* Versioned: struct_size must be sizeof(shd_flush_out) as the caller's header declares it (round
+ * 5 added n_events and event_bytes at the end; a caller built against that older layout has a
+ * pointer here and is refused with SHD_ERR_INVALID instead of having fields read past its object). */
 typedef struct shd_flush_out {
+    uint32_t struct_size;   /* in: sizeof(shd_flush_out) */
+    uint32_t event_bytes;   /* in: 16 (or 0) = shd_event16 records, 12 = shd_event12 records */
     uint8_t* status2;
     uint32_t* ev_off;
     shd_event16* events;        /* shd_event12 records when event_bytes = 12 */
@@ -353,7 +358,6 @@ typedef struct shd_flush_out {
     uint64_t n_sent;
     uint64_t n_events;      /* events returned (= n_sent on one context; the own destinations' events
                                under a communicator) */
-    uint32_t event_bytes;   /* in: 16 (or 0) = shd_event16 records, 12 = shd_event12 records */
 } shd_flush_out;
 
 shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_stages, uint64_t time_base,

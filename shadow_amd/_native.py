@@ -99,9 +99,18 @@ class Stage(C.Structure):
 
 
 class FlushOut(C.Structure):
-    _fields_ = [("status2", C.c_void_p), ("ev_off", C.c_void_p), ("events", C.c_void_p), ("seq_base", C.c_void_p),
+    """shd_flush_out; versioned by its leading struct_size, which the constructor fills in.
+    FlushOut(status2, ev_off, events, seq_base, min_deliver, min_latency, n_sent, n_events,
+    event_bytes): the fields' order before round 6, kept for the callers."""
+    _fields_ = [("struct_size", C.c_uint32), ("event_bytes", C.c_uint32),
+                ("status2", C.c_void_p), ("ev_off", C.c_void_p), ("events", C.c_void_p), ("seq_base", C.c_void_p),
                 ("min_deliver", C.c_uint64), ("min_latency", C.c_uint64), ("n_sent", C.c_uint64),
-                ("n_events", C.c_uint64), ("event_bytes", C.c_uint32)]
+                ("n_events", C.c_uint64)]
+
+    def __init__(self, status2=0, ev_off=0, events=0, seq_base=0, min_deliver=0, min_latency=0, n_sent=0,
+                 n_events=0, event_bytes=16):
+        super().__init__(C.sizeof(FlushOut), event_bytes, status2, ev_off, events, seq_base, min_deliver,
+                         min_latency, n_sent, n_events)
 
 
 SEND_PAYLOAD = 0x80000000

@@ -743,7 +743,10 @@ __global__ __launch_bounds__(1024) void eq_totals(uint32_t n_hosts, uint32_t n_p
 
 // a stored run's event arrays for n events (the ensure keeps growth headroom: slots are reused
 // round after round)
-static shd_status eq_run_alloc(EqState& Q, EqRunBuf& r, uint32_t n_hosts, uint64_t n) {
+// hint = false (shd_equeue_pending's full compaction, the whole pending set in one run): the
+// growth neither takes nor raises the slots' shared capacity -- a hint raised to 1.5x every pending
+// event would make every later slot growth that large (advisor, round 5: ~14x the largest run)
+static shd_status eq_run_alloc(EqState& Q, EqRunBuf& r, uint32_t n_hosts, uint64_t n, bool hint = true) {
     // room for half as many again: the runs' sizes wander from round to round, and a regrowth
     // (hipFree + hipMalloc of ~0.5 GB of arrays) inside an advance cost ~0.3 ms (C5: 0.78 ms rounds);
     // and at least the largest capacity any slot has grown to, so the slots reach their steady
@@ -751,8 +754,8 @@ static shd_status eq_run_alloc(EqState& Q, EqRunBuf& r, uint32_t n_hosts, uint64
     // compaction runs of different sizes)
     const size_t m = std::max<uint64_t>(n, 1);
     if (r.deliver.bytes < m * 8 || r.src.bytes < m * 4 || r.seq.bytes < m * 8 || r.tag.bytes < m * 8) {
-        const size_t g = std::max<size_t>(m + m / 2, Q.cap_hint);
-        Q.cap_hint = g;
+        const size_t g = hint ? std::max<size_t>(m + m / 2, Q.cap_hint) : m + m / 2;
+        if (hint) Q.cap_hint = g;
         SHD_TRY(r.deliver.ensure(g * 8));
         SHD_TRY(r.src.ensure(g * 4));
         SHD_TRY(r.seq.ensure(g * 8));
@@ -886,10 +889,13 @@ static shd_status eq_compact(shd_ctx* ctx, bool all) {
     if (S.n == 0) return SHD_OK;
     const int t = eq_free_slot(Q);
     EqRunBuf& T = Q.run[t];
-    SHD_TRY(eq_run_alloc(Q, T, Q.n_hosts, n));
-    // every pending event of the picked runs moves (window ~0): n, known here, so the pass runs
-    // without its totals and read-back -- the advance's own pass follows on the stream
-    SHD_TRY(eq_pass(ctx, S, ~0ull, T.off.as<uint32_t>(), eq_run_out(T), nullptr, nullptr, n, false));
+    SHD_TRY(eq_run_alloc(Q, T, Q.n_hosts, n, !all));
+    // every pending event of the picked runs moves (window ~0): n, known here, so inside an advance
+    // the pass runs without its totals and read-back (the advance's own pass follows on the
+    // stream).  The full compaction of shd_equeue_pending is not hot: it reads the totals back and
+    // checks that exactly the n events the runs' counts promise were moved.
+    SHD_TRY(eq_pass(ctx, S, ~0ull, T.off.as<uint32_t>(), eq_run_out(T), nullptr, nullptr, n, all));
+    if (all && ctx->h_pin[kEqPinWord + 1] != n) return SHD_ERR_STATE;
     // the new run's cursor goes to the CURRENT cursor buffer: the runs left out keep theirs there
     SHD_HIP(hipMemcpyAsync(eq_cursor(Q, Q.ccur, t), T.off.p, (size_t)Q.n_hosts * 4, hipMemcpyDeviceToDevice,
                            ctx->stream));

@@ -232,6 +232,7 @@ void shd_host_free(void* p) {
 shd_status shd_relay_flush(shd_ctx* ctx, const shd_stage* stages, uint32_t n_stages, uint64_t time_base,
                            const shd_round* round, shd_flush_out* out) {
     if (!ctx || !round || !out || (n_stages && !stages)) return SHD_ERR_INVALID;
+    if (out->struct_size != sizeof(shd_flush_out)) return SHD_ERR_INVALID;   // another header's layout
     if (out->event_bytes != 0 && out->event_bytes != 12 && out->event_bytes != 16) return SHD_ERR_INVALID;
     const uint32_t eb = out->event_bytes == 12 ? 12u : 16u;
     RelayState& R = ctx->relay;
