@@ -38,10 +38,10 @@ struct RcclComm final : Comm {
         return SHD_OK;
     }
     shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes, void* const* recv,
-                        const size_t* recv_bytes, hipStream_t s) override {
+                        const size_t* recv_bytes, hipStream_t s, shd_status local) override {
         // the group is posted whatever happens to the own part: the peers' sends and receives
         // must meet theirs
-        shd_status st = SHD_OK;
+        shd_status st = local;
         for (int k = 0; k < n_parts; ++k) {   // own part: a device copy
             const size_t i = (size_t)rank * n_parts + k;
             if (send_bytes[i] != recv_bytes[i]) st = SHD_ERR_INVALID;
@@ -134,8 +134,9 @@ struct LocalComm final : Comm {
         return leave(st, s);
     }
     shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes, void* const* recv,
-                        const size_t* recv_bytes, hipStream_t s) override {
-        shd_status st = n_parts < 1 || n_parts > 4 ? SHD_ERR_INVALID : SHD_OK;   // the group's pointer slots
+                        const size_t* recv_bytes, hipStream_t s, shd_status local) override {
+        // (a caller's own failure enters as this rank's status: the peers skip its parts)
+        shd_status st = n_parts < 1 || n_parts > 4 ? SHD_ERR_INVALID : local;   // the group's pointer slots
         const shd_status e0 = enter(s);
         if (st == SHD_OK) st = e0;
         else g->pre[rank] = (int)st;
@@ -186,6 +187,8 @@ struct HostComm final : Comm {
     unsigned char* hs = nullptr;   // pinned staging: the blocks sent
     unsigned char* hr = nullptr;   // and received
     size_t hs_cap = 0, hr_cap = 0;
+    std::vector<uint64_t> st_s, st_r, st_b, st_o;   // the staging status round (sized at init)
+    const Knobs* kn = nullptr;                     // its context's knobs (fault injection)
     ~HostComm() override {
         if (hs) (void)hipHostFree(hs);
         if (hr) (void)hipHostFree(hr);
@@ -225,17 +228,34 @@ struct HostComm final : Comm {
         }
         // Every rank enters the transport, whatever happens locally: its peers are already
         // blocked in the caller's collective.  Pinned staging that cannot grow falls back to
-        // pageable memory for this call; only when that fails too is the rank unable to take part.
+        // pageable memory for this call.  A rank left with no staging at all cannot send blocks
+        // of the agreed sizes, so the allocation's outcome is agreed first, in a status round of
+        // its own (8 bytes per rank, buffers allocated when the communicator was made): every
+        // rank then either moves the blocks or returns the lowest failing rank's status.
         std::vector<unsigned char> hs_tmp, hr_tmp;
         unsigned char* S = hs;
         unsigned char* Rv = hr;
+        shd_status st_mem = SHD_OK;
         try {
+            if (kn && kn->get(K_TEST_FAIL, 0) == 3) throw std::bad_alloc();   // (fault injection, tests)
             if (grow(hs, hs_cap, s_end) == SHD_OK) S = hs;
             else { hs_tmp.resize(s_end); S = hs_tmp.data(); }
             if (grow(hr, hr_cap, r_end) == SHD_OK) Rv = hr;
             else { hr_tmp.resize(r_end); Rv = hr_tmp.data(); }
         } catch (...) {
-            return SHD_ERR_NOMEM;
+            st_mem = SHD_ERR_NOMEM;
+        }
+        {
+            for (int r = 0; r < n; ++r) {
+                st_s[r] = (uint64_t)st_mem;
+                st_b[r] = 8;
+                st_o[r] = (uint64_t)r * 8;
+            }
+            if (ops.all_to_allv(ops.user, st_s.data(), st_b.data(), st_o.data(), st_r.data(), st_b.data(),
+                                st_o.data()) != 0)
+                return SHD_ERR_HIP;
+            for (int q = 0; q < n; ++q)
+                if ((shd_status)st_r[q] != SHD_OK) return (shd_status)st_r[q];
         }
         for (int r = 0; r < n; ++r) {
             size_t at = so[r] + 8;
@@ -294,7 +314,7 @@ struct HostComm final : Comm {
         return run(1, src, sb, so, dst, rb, s, SHD_OK);
     }
     shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes, void* const* recv,
-                        const size_t* recv_bytes, hipStream_t s) override {
+                        const size_t* recv_bytes, hipStream_t s, shd_status local) override {
         if (n_parts < 1) return SHD_ERR_INVALID;
         const size_t m = (size_t)size * n_parts;
         std::vector<const void*> src(send, send + m);
@@ -307,7 +327,7 @@ struct HostComm final : Comm {
             if (r != rank)
                 for (int k = 0; k < n_parts; ++k) off += sb[(size_t)r * n_parts + k];
         }
-        return run(n_parts, src, sb, so, dst, rb, s, SHD_OK);
+        return run(n_parts, src, sb, so, dst, rb, s, local);
     }
     shd_status all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
         // one staged block (status + bytes) sent to every peer: every send offset is 0
@@ -395,6 +415,12 @@ shd_status shd_comm_init_host(shd_ctx* ctx, int32_t n_ranks, int32_t rank, const
     c->ops = *ops;
     c->rank = rank;
     c->size = n_ranks;
+    c->kn = &ctx->knobs;
+    try {
+        for (auto* v : {&c->st_s, &c->st_r, &c->st_b, &c->st_o}) v->resize((size_t)n_ranks);
+    } catch (...) {
+        return SHD_ERR_NOMEM;
+    }
     ctx->comm = std::move(c);
     ctx->relay.ready = false;
     ctx->eq.ready = false;

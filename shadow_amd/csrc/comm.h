@@ -27,9 +27,13 @@ struct Comm {
     // point to point with every rank in one group: part k of the message to rank r is
     // send[r * n_parts + k] (send_bytes[..]); part k of the message from rank q lands in
     // recv[q * n_parts + k] (recv_bytes[..]).  Sizes were agreed before (zero parts are skipped
-    // on both sides).
+    // on both sides).  local: the caller's own status on entry, a failure it carries into this
+    // collective instead of returning before it -- LocalComm and HostComm agree it (every rank
+    // returns the lowest failing rank's status); RCCL cannot, so a caller that needs the agreement
+    // there sends the status in-band as a part of its own (relay_round_sharded_v7).
     virtual shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes,
-                                void* const* recv, const size_t* recv_bytes, hipStream_t s) = 0;
+                                void* const* recv, const size_t* recv_bytes, hipStream_t s,
+                                shd_status local = SHD_OK) = 0;
     // recv holds size * bytes; rank q's send lands at recv + q * bytes (in place allowed:
     // send == recv + rank * bytes)
     virtual shd_status all_gather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;

@@ -170,6 +170,10 @@ struct RelayState {
     // the per-sender receive / packet bases
     DevBuf xs_sc, xs_out, xs_b;
     PinBuf xs_pin;
+    // the exchange's status part: [0] this rank's status after the sizing gather (0 unless a local
+    // failure is carried), [1 + q] the one rank q sent (its own slot stays 0)
+    DevBuf xs_st;
+    bool xs_st_dirty = false;
     // shd_relay_flush (flush.hip): the round's draws came from the CPU (top 32 bits in `draws`), the
     // staged runs and records as uploaded, the send permutation (grouped <-> stage order) and the
     // packed outputs

@@ -1,5 +1,7 @@
 // Tuning and testing knobs of one context.  None changes a result: they pick grids, kernel
-// variants or an equivalent fallback pipeline.  Each starts from the environment variable
+// variants or an equivalent fallback pipeline -- except TEST_FAIL, fault injection for the
+// failure-agreement tests (1: a sharded relay round fails on this rank after its sizing summary
+// is read; 3: the host transport's staging cannot be allocated).  Each starts from the environment variable
 // SHD_<name>, read ONCE by shd_open, so a caller's environment cannot change grids between two
 // builds; shd_set_knob / shd_get_knob (api.cpp) change or inspect them per context afterwards.
 #pragma once
@@ -18,7 +20,8 @@ namespace shd {
     X(PRUNE_DENSE_BUILD) X(SSSP_HUB) X(SYNC_KERNEL)                                               \
     X(EQ_COUNT_BLOCKS) X(EQ_WAVE_MERGE) X(EQ_SEARCH_ONLY) X(EQ_MAX_RUNS) X(RELAY_GROUP_SENDS) X(HIST_SCALAR) X(B7_STOP) X(RELAY_FORCE_V1)         \
     X(RELAY_FORCE_V3) X(RELAY_NO_LDS_MAP) X(MERGE_BY_EVENT) X(SHARD_CHUNK_ROWS) X(SHARD_REPLICATE_MB)             \
-    X(SHARD_RESERVE_SLOTS) X(RELAY_SHARD_X24) X(FLUSH_COPY) X(PRUNE_SHAPE) X(PRUNE_SHAPE_SH) X(EQ_FOLD) X(EQ_FOLD_TAKE) X(RELAY_K0_INLINE) X(RELAY_SCAN2)
+    X(SHARD_RESERVE_SLOTS) X(RELAY_SHARD_X24) X(FLUSH_COPY) X(PRUNE_SHAPE) X(PRUNE_SHAPE_SH) X(EQ_FOLD) X(EQ_FOLD_TAKE) X(RELAY_K0_INLINE) X(RELAY_SCAN2)   \
+    X(TEST_FAIL)
 
 enum Knob : int {
 #define SHD_KNOB_ENUM(n) K_##n,

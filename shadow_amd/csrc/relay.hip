@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 
 #include <vector>
@@ -702,7 +703,7 @@ __device__ unsigned long long g_stamp_prof[12];
 // BIN (pipeline v7): every packet with a valid destination is also placed, sent or not, into
 // its destination bin (kBinDst consecutive destinations): the workgroup's slots of bin b are
 // the segment bin_base[b] + seg_pre[g][b] counted by relay_bin_hist; the slot inside the
-// segment comes from an LDS counter (four 8-bit counters per word).  The records carry the
+// segment comes from an LDS counter (one u32 per bin holding the absolute next slot).  The records carry the
 // status and the destination's low bits so bin_sort_v7 can filter and split them.
 constexpr uint32_t kBinShift = 5;
 constexpr uint32_t kBinDst = 1u << kBinShift;
@@ -722,18 +723,27 @@ __device__ __forceinline__ uint32_t dst_bin(const RelayArgs3& a, uint32_t dst, u
 }
 constexpr uint32_t kHistSplit = 2;   // histogram rows per stamp workgroup (relay_bin_hist)
 
-template <bool BIN>
+// CH: the batch carries f64 chances (a.chance) instead of K0's draws.  A template parameter, not
+// a run-time select: `a.chance ? chance64[i] : draw[i]` compiled to a branch whose join moved the
+// loaded value with an s_waitcnt vmcnt(0), so each of a thread's kS6Per load sets waited for the
+// one before it (four memory round trips per chunk instead of one).
+template <bool BIN, bool CH>
 __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const uint32_t* __restrict__ draw,
                                                              const uint32_t* __restrict__ packed,
                                                              uint32_t n_words, uint32_t bits) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_tbl[];   // packed host -> node
-    uint32_t* s_cur = s_tbl + n_words;                                 // BIN: slot counters
-    if (BIN && a.red[6]) return;   // a bin overflowed its 8-bit counters or LDS stage: the host reruns v3
+    // BIN: per bin, the next record slot of this workgroup's segment (absolute: bin base + segment
+    // start + records placed), so placing a record is one LDS atomic -- no per-record loads of
+    // the bases (a scattered load costs ~64 TA cycles per wave instruction: ~30 us of the stamp)
+    uint32_t* s_slot = s_tbl + n_words;
+    if (BIN && a.red[6]) return;   // a bin overflowed bin_sort_v7's LDS stage: the host reruns v3
+    constexpr uint32_t kW = kS6Threads / 64;
+    static_assert(kS6Per * kW <= 64, "one wave scans the chunk's (i, wave) sent totals");
     __shared__ uint2 s_rows[kS5RowLds];
-    __shared__ uint16_t s_scan[kS6Cap + 1];
     __shared__ uint32_t s_host[kS5Hosts], s_beg[kS5Hosts], s_pre[kS5Hosts + 1], s_node[kS5Hosts];
     __shared__ uint32_t s_rowof[kS5Hosts], s_rownode[kS5Hosts], s_run[kS5Hosts], s_base[kS5Hosts];
-    __shared__ uint32_t s_wsum[kS6Threads / 64], s_nrows;
+    __shared__ uint32_t s_off[kS5Hosts];    // a host's event id = s_off + the chunk's sent prefix
+    __shared__ uint32_t s_wt[64], s_nrows;  // sent sends per (i, wave) of the chunk
     __shared__ uint8_t s_own[kS6Cap];   // chunk position -> host slot in the group
     // next group's distinct source nodes: up to one per host of the group (a group of kS5Hosts
     // hosts spans at most kS5Hosts nodes; the prefetch stages pn * n_nodes <= kS5RowLds entries)
@@ -748,7 +758,8 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
 #endif
     for (uint32_t i = tid; i < n_words; i += kS6Threads) s_tbl[i] = packed[i];
     if (BIN)
-        for (uint32_t i = tid; i < (a.n_bins + 3) / 4; i += kS6Threads) s_cur[i] = 0;
+        for (uint32_t b = tid; b < a.n_bins; b += kS6Threads)
+            s_slot[b] = a.bin_base[b] + a.seg_pre[(size_t)blockIdx.x * a.n_bins + b];
     const uint32_t n_groups = (a.n_src + a.gs - 1) / a.gs;
     uint64_t min_d = ~0ull, min_l = ~0ull, ns_total = 0;
     bool wide = false, disorder = false;
@@ -852,27 +863,33 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
             }
             // (a) positions -> packet indices through the owner map (positions past the chunk end
             // are clamped onto its last packet so every load below is in bounds and unconditional)
-            uint32_t idx[kS6Per], hl[kS6Per], kk[kS6Per];
+            // hl: the host slot, plus kFirst / kLast when the position is the host's first / last send
+            // (the position inside the host is needed only for those and the load below: one
+            // register per position less)
+            constexpr uint32_t kFirst = 0x100, kLast = 0x200, kSlot = 0xFF;
+            uint32_t idx[kS6Per], hl[kS6Per];
 #pragma unroll
             for (uint32_t i = 0; i < kS6Per; ++i) {
                 const uint32_t q = min(tid + kS6Threads * i, cn - 1);
                 const uint32_t gp = c0 + q;
                 const uint32_t lo = s_own[q];       // s_pre[lo] <= gp < s_pre[lo + 1]
-                hl[i] = lo;
-                kk[i] = gp - s_pre[lo];
-                idx[i] = s_beg[lo] + kk[i];
+                const uint32_t k = gp - s_pre[lo];
+                hl[i] = lo | (k == 0 ? kFirst : 0u) | (gp + 1 == s_pre[lo + 1] ? kLast : 0u);
+                idx[i] = s_beg[lo] + k;
             }
             SP_MARK(8);
             // (b) all loads of the chunk in flight together
-            uint64_t now[kS6Per], prv[kS6Per], rv[kS6Per];
+            uint64_t now[kS6Per], prv[kS6Per];
+            std::conditional_t<CH, uint64_t, uint32_t> rv[kS6Per];
             uint32_t dst[kS6Per], pay[kS6Per];
 #pragma unroll
             for (uint32_t i = 0; i < kS6Per; ++i) {
                 now[i] = a.send_time[idx[i]];
-                prv[i] = a.send_time[idx[i] - (kk[i] > 0 ? 1u : 0u)];
+                prv[i] = a.send_time[idx[i] - ((hl[i] & kFirst) ? 0u : 1u)];
                 dst[i] = a.dst_host[idx[i]];
                 pay[i] = a.payload[idx[i]];
-                rv[i] = a.chance ? chance64[idx[i]] : (uint64_t)draw[idx[i]];
+                if constexpr (CH) rv[i] = chance64[idx[i]];
+                else rv[i] = draw[idx[i]];
             }
             SP_MARK(9);
             // (c) decisions
@@ -885,17 +902,19 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 doff[i] = dn[i] = 0;
                 if (pos < cn) {
                     // a drawing send after a skipped one breaks K0's prefix rule
-                    if (kk[i] > 0 && now[i] < a.sim_end && !(prv[i] < a.sim_end)) disorder = true;
+                    // (bitwise, not short-circuit: a `&&` chain let the compiler sink prv's load
+                    // under the now[i] test -- a second, dependent memory round trip)
+                    disorder |= !(hl[i] & kFirst) & (now[i] < a.sim_end) & !(prv[i] < a.sim_end);
                     if (dst[i] >= a.n_hosts) {      // "No host ID for dest address" (worker.rs:350-355)
                         atomicMin(&a.red[3], (unsigned long long)idx[i]);
                     } else if (now[i] < a.sim_end) {
                         dn[i] = packed_get(s_tbl, dst[i], bits);
-                        const uint2 pp = staged ? s_rows[s_rowof[hl[i]] * a.n_nodes + dn[i]]
-                                                : path_global(a.path, (size_t)s_node[hl[i]] * a.n_nodes + dn[i]);
+                        const uint2 pp = staged ? s_rows[s_rowof[hl[i] & kSlot] * a.n_nodes + dn[i]]
+                                                : path_global(a.path, (size_t)s_node[hl[i] & kSlot] * a.n_nodes + dn[i]);
                         const double reliability = (double)one_minus(__uint_as_float(pp.y));
                         bool tie = false;
-                        const bool ge = a.chance ? __longlong_as_double((long long)rv[i]) >= reliability
-                                                 : draw_drops((uint32_t)rv[i], reliability, tie);
+                        const bool ge = CH ? __longlong_as_double((long long)rv[i]) >= reliability
+                                           : draw_drops((uint32_t)rv[i], reliability, tie);
                         wide |= tie;   // a draw whose low bits would decide: redo the round on pipeline 1
                         if (!(now[i] < a.bootstrap_end) && ge && pay[i] > 0) {
                             st[i] = kStDropped;
@@ -911,9 +930,18 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                         }
                     }
                 }
-                s_scan[pos] = st[i] == kStSent ? 1 : 0;
             }
             SP_MARK(10);
+            // the chunk's event ids without a block scan: sent flags -> one ballot per (i, wave),
+            // the 64 wave totals through LDS, and every wave scans those itself (one barrier).
+            // Position order is pos = tid + kS6Threads * i: i-major, then wave, then lane.
+            uint64_t sm[kS6Per];
+#pragma unroll
+            for (uint32_t i = 0; i < kS6Per; ++i) sm[i] = __ballot(st[i] == kStSent);
+            if (lane == 0) {
+#pragma unroll
+                for (uint32_t i = 0; i < kS6Per; ++i) s_wt[i * kW + w] = (uint32_t)__popcll(sm[i]);
+            }
             __syncthreads();
             SP_MARK(3);
             if (c0 == 0) {   // prefetch the next group's rows; they land while this group runs
@@ -930,68 +958,80 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                     have_pf = true;
                 }
             }
-            {   // block-wide exclusive scan of the sent flags (kS6Per consecutive entries per thread)
-                uint32_t v[kS6Per], sum = 0;
-#pragma unroll
-                for (uint32_t i = 0; i < kS6Per; ++i) {
-                    v[i] = s_scan[tid * kS6Per + i];
-                    sum += v[i];
-                }
-                uint32_t incl = sum;
+            uint32_t pre[kS6Per];   // sent sends of the chunk before each own position
+            {
+                const uint32_t v = lane < kS6Per * kW ? s_wt[lane] : 0u;
+                uint32_t incl = v;
 #pragma unroll
                 for (uint32_t o = 1; o < 64; o <<= 1) {
                     const uint32_t y = __shfl_up(incl, o);
                     if (lane >= o) incl += y;
                 }
-                if (lane == 63) s_wsum[w] = incl;
-                __syncthreads();
-                uint32_t run = incl - sum;
-                for (uint32_t ww = 0; ww < w; ++ww) run += s_wsum[ww];
+                const uint32_t ex = incl - v;
 #pragma unroll
-                for (uint32_t i = 0; i < kS6Per; ++i) {
-                    s_scan[tid * kS6Per + i] = (uint16_t)run;
-                    run += v[i];
-                }
-                if (tid == kS6Threads - 1) s_scan[kS6Cap] = (uint16_t)run;
+                for (uint32_t i = 0; i < kS6Per; ++i)
+                    pre[i] = (uint32_t)__shfl((int)ex, (int)(i * kW + w)) +
+                             __builtin_amdgcn_mbcnt_hi((uint32_t)(sm[i] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm[i], 0u));
+            }
+            // a host's first position in the chunk (its first send, or the chunk's start) fixes the
+            // offset of its ids in this chunk: id = s_off + pre
+#pragma unroll
+            for (uint32_t i = 0; i < kS6Per; ++i) {
+                const uint32_t pos = tid + kS6Threads * i;
+                const uint32_t h = hl[i] & kSlot;
+                if (pos < cn && ((hl[i] & kFirst) || pos == 0)) s_off[h] = s_base[h] + s_run[h] - pre[i];
             }
             __syncthreads();
             SP_MARK(4);
+            // stores: the ids, each record's slot in its bin (one LDS atomic), then every store; a
+            // host's last position in the chunk carries its sent count into s_run
+            uint32_t local[kS6Per], slot[kS6Per];
+#pragma unroll
+            for (uint32_t i = 0; i < kS6Per; ++i) {
+                const uint32_t pos = tid + kS6Threads * i;
+                local[i] = 0;
+                slot[i] = 0;
+                if (pos < cn) {
+                    const uint32_t h = hl[i] & kSlot, so = s_off[h];
+                    if (st[i] == kStSent) local[i] = so + pre[i];
+                    if (BIN && dst[i] < a.n_hosts) {
+                        uint32_t dl;
+                        slot[i] = atomicAdd(&s_slot[dst_bin(a, dst[i], dl)], 1u);
+                    }
+                    if (pos == cn - 1 || (hl[i] & kLast))
+                        s_run[h] = so + pre[i] + (st[i] == kStSent ? 1u : 0u) - s_base[h];
+                }
+            }
 #pragma unroll
             for (uint32_t i = 0; i < kS6Per; ++i) {
                 const uint32_t pos = tid + kS6Threads * i;
                 if (pos < cn) {
+#ifndef SHD_PRICE_STATUS   // (tuning builds: price the stamp's stores away; wrong output)
                     a.status[idx[i]] = st[i];
-                    uint32_t local = 0;
-                    if (st[i] == kStSent) {
-                        const uint32_t first = max(s_pre[hl[i]], c0) - c0;
-                        local = s_base[hl[i]] + s_run[hl[i]] + s_scan[pos] - s_scan[first];
-                        if (a.counts) atomicAdd(&a.counts[(size_t)s_node[hl[i]] * a.n_nodes + dn[i]], 1ull);
-                    }
+#endif
                     if (!BIN) {
                         a.key[idx[i]] = st[i] == kStSent ? dst[i] : a.n_hosts;
-                        if (st[i] == kStSent) a.rec[idx[i]] = make_uint4(doff[i], s_host[hl[i]], local, idx[i]);
+                        if (st[i] == kStSent) a.rec[idx[i]] = make_uint4(doff[i], s_host[hl[i] & kSlot], local[i], idx[i]);
                     } else if (dst[i] < a.n_hosts) {
                         uint32_t dl;
-                        const uint32_t bin = dst_bin(a, dst[i], dl), sh = (bin & 3u) * 8u;
-                        const uint32_t old = atomicAdd(&s_cur[bin >> 2], 1u << sh);
-                        const uint32_t slot = a.bin_base[bin] + a.seg_pre[(size_t)blockIdx.x * a.n_bins + bin] +
-                                              ((old >> sh) & 0xFFu);
-                        a.rec[slot] = make_uint4(doff[i],
-                                                 s_host[hl[i]] | (dl << 18) |
-                                                     ((uint32_t)st[i] << 24),
-                                                 local, idx[i]);
+                        dst_bin(a, dst[i], dl);
+#if defined(SHD_PRICE_REC) && SHD_PRICE_REC == 2
+                        if (slot[i] == 0xFFFFFFFFu)   // never: the record store priced away
+#elif defined(SHD_PRICE_REC)
+                        slot[i] = idx[i];             // coalesced by packet index instead of the bin slot
+#endif
+                        a.rec[slot[i]] = make_uint4(doff[i],
+                                                    s_host[hl[i] & kSlot] | (dl << 18) |
+                                                        ((uint32_t)st[i] << 24),
+                                                    local[i], idx[i]);
                     }
+                    if (st[i] == kStSent && a.counts)
+                        atomicAdd(&a.counts[(size_t)s_node[hl[i] & kSlot] * a.n_nodes + dn[i]], 1ull);
                 }
             }
             if (c0 + kS6Cap < T) fill_owner(c0 + kS6Cap, nh);   // s_own of this chunk is consumed
             __syncthreads();
             SP_MARK(5);
-            if (tid < nh) {
-                const uint32_t pb = max(s_pre[tid], c0), pe = min(s_pre[tid + 1], c0 + cn);
-                if (pe > pb) s_run[tid] += s_scan[pe - c0] - s_scan[pb - c0];
-            }
-            __syncthreads();
-            SP_MARK(6);
         }
         if (tid < nh) {
             const size_t h = s_host[tid];
@@ -1557,7 +1597,7 @@ __global__ __launch_bounds__(kHist4Threads) void relay_bin_hist4(RelayArgs3 a, u
 // seg[g][b] = number of bin-b slots of stamp workgroups before g (the sum of kHistSplit
 // histogram rows per workgroup, exclusive prefix over g); tot[b] = all of bin b.  Lane = bin,
 // wave = a slice of workgroups; every row load of a slice is independent.  A workgroup count
-// that does not fit the stamp's 8-bit slot counters flags red[6].
+// (the stamp's slot counters are 32-bit since round 6: no workgroup count overflows them).
 constexpr uint32_t kColMaxG = 256;   // stamp workgroups (one per CU)
 
 // (base != nullptr: bin_base_scan folded in -- each block's 64 bin totals, a wave scan, and a
@@ -1577,7 +1617,6 @@ __global__ __launch_bounds__(1024) void bin_col_scan(uint32_t G, uint32_t n_bins
     const uint32_t g0 = min(G, w * kPer), g1 = min(G, g0 + kPer);
     uint32_t c[kPer];
     uint32_t sum = 0;
-    bool over = false;
     // every row load unconditional (indices clamped, values masked) so all of them are in flight
     // together instead of one guarded load at a time
     const uint32_t bc = min(b, n_bins - 1);
@@ -1591,10 +1630,8 @@ __global__ __launch_bounds__(1024) void bin_col_scan(uint32_t G, uint32_t n_bins
 #pragma unroll
     for (uint32_t i = 0; i < kPer; ++i) {
         if (!(g0 + i < g1 && b < n_bins)) c[i] = 0;
-        over |= c[i] > 0xFFu;
         sum += c[i];
     }
-    if (over) atomicOr(&red[6], 1ull);
     s[w][lane] = sum;
     __syncthreads();
     uint32_t run = 0;
@@ -1843,7 +1880,26 @@ struct XSrc {
     const uint32_t* rbase;   // sender q's slice in the received records (q != me)
     const uint32_t* pbase;
     const uint4* own;        // this rank's own records stay where its stamp put them (never exchanged)
+    const uint64_t* rst;     // [world] the status each sender carried into the exchange (own: own_st)
+    uint32_t own_st;
 };
+
+// the round's agreed status from the exchange's status part: the lowest failing rank's
+__device__ __forceinline__ uint32_t xs_status(const XSrc& xs) {
+    for (uint32_t q = 0; q < xs.world; ++q) {
+        const uint32_t v = q == xs.me ? xs.own_st : (uint32_t)xs.rst[q];
+        if (v) return v;
+    }
+    return 0u;
+}
+
+// a rank without bins: no bin sort writes its event count and the agreed status
+__global__ __launch_bounds__(64) void xs_fin_empty(XSrc xs, uint32_t* __restrict__ ev_off) {
+    if (threadIdx.x == 0) {
+        ev_off[0] = 0;
+        ev_off[1] = xs_status(xs);
+    }
+}
 
 // K4 (v7): one workgroup per bin, bins taken in ticket order so the event offsets can use a
 // decoupled look-back (publish the bin's sent count, add the predecessors' counts).  The bin's
@@ -1966,7 +2022,10 @@ __global__ __launch_bounds__(kB7Threads) void bin_sort_v7(uint32_t n_hosts, uint
     __syncthreads();
     const uint32_t excl = s_excl, d0 = bin * kBinDst, S = s_off[kBinDst];
     if (tid < kBinDst && d0 + tid < n_hosts) ev_off[d0 + tid] = excl + s_off[tid];
-    if (tid == 0 && bin == n_bins - 1) ev_off[n_hosts] = excl + S;
+    if (tid == 0 && bin == n_bins - 1) {
+        ev_off[n_hosts] = excl + S;
+        if constexpr (X) ev_off[n_hosts + 1] = xs_status(xs);   // (read back with the count)
+    }
     if (stop == 2) return;
     for (uint32_t i = tid; i < N; i += kB7Threads) {
         const uint32_t y = x[i].y;
@@ -2075,9 +2134,9 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
     if (R.n_src == 0) {
     } else if (R.hn_bits) {   // host -> node map fits the LDS: persistent stamp, no node gathers
         const uint32_t groups = div_up(R.n_src, kS5Hosts);
-        relay_stamp_v6<false><<<std::min<uint32_t>(groups, (uint32_t)ctx->n_cu), kS6Threads,
-                         (size_t)R.hn_words * 4, s>>>(a, R.draws.as<uint32_t>(),
-                                                      R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
+        auto* k = a.chance ? &relay_stamp_v6<false, true> : &relay_stamp_v6<false, false>;
+        k<<<std::min<uint32_t>(groups, (uint32_t)ctx->n_cu), kS6Threads, (size_t)R.hn_words * 4, s>>>(
+            a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     } else {
         relay_stamp_v5<<<div_up(R.n_src, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint32_t>());
     }
@@ -2115,12 +2174,14 @@ static bool relay_v7_ok(shd_ctx* ctx, uint64_t n, uint32_t n_bins) {
     // two in-process ranks call the relay from two threads)
     static const size_t stat_lds = [] {
         hipFuncAttributes at{};
-        return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&relay_stamp_v6<true>)) == hipSuccess
-                   ? (size_t)at.sharedSizeBytes
+        hipFuncAttributes at2{};   // (the two chance forms' static LDS: the larger)
+        return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&relay_stamp_v6<true, false>)) == hipSuccess &&
+                       hipFuncGetAttributes(&at2, reinterpret_cast<const void*>(&relay_stamp_v6<true, true>)) == hipSuccess
+                   ? std::max((size_t)at.sharedSizeBytes, (size_t)at2.sharedSizeBytes)
                    : (size_t)0;
     }();
     if (!stat_lds) return false;
-    return stat_lds + (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4 <= 160 * 1024;
+    return stat_lds + (size_t)R.hn_words * 4 + (size_t)n_bins * 4 <= 160 * 1024;
 }
 
 // Hosts per stamp group: about S sends per group (SHD_RELAY_GROUP_SENDS, 0 = fixed kS5Hosts),
@@ -2230,7 +2291,8 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
                                                        SS.state.as<unsigned long long>(), SS.epoch);
     }
     if (k0 && !k0_inline) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
-    relay_stamp_v6<true><<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)(n_bins + 3) / 4 * 4, s>>>(
+    auto* stamp = a.chance ? &relay_stamp_v6<true, true> : &relay_stamp_v6<true, false>;
+    stamp<<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)n_bins * 4, s>>>(
         a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     if (xsh) {
         SHD_HIP(hipGetLastError());
@@ -2735,7 +2797,10 @@ static shd_status relay_shard_alloc(shd_ctx* ctx) {
     SHD_TRY(R.xs_b.ensure((size_t)world * 8 + 64));
     SHD_TRY(R.x_off.ensure(((size_t)H + world) * 4));
     SHD_TRY(R.x_roff.ensure((size_t)world * (n_own + 1) * 4 + (size_t)(world + 1) * 4));
-    SHD_TRY(R.m_off.ensure((n_own + 1) * 4));
+    SHD_TRY(R.m_off.ensure((n_own + 4) * 4));   // + the received statuses' word (bin_sort_v7<true>)
+    SHD_TRY(R.xs_st.ensure(((size_t)world + 1) * 8));
+    SHD_HIP(hipMemsetAsync(R.xs_st.p, 0, ((size_t)world + 1) * 8, ctx->stream));
+    R.xs_st_dirty = false;
     SHD_TRY(R.ev_off.ensure(((size_t)H + 1) * 4));
     R.x_cap = 0;
     return SHD_OK;
@@ -2888,7 +2953,7 @@ static shd_status relay_round_sharded_x24(shd_ctx* ctx, const shd_batch* b, cons
 
 // One sharded round without the merge (see xs_row above).  *fallback = true (the same on every
 // rank: the decision reads only the gathered rows) when any rank cannot take this path -- not
-// pipeline 7, a bin over its LDS stage or an 8-bit slot counter, a deliver offset or event ids
+// pipeline 7, a bin over its LDS stage, a deliver offset or event ids
 // past 32 bits, more than 2^24 packets over all ranks -- and the caller then runs the packing
 // path (relay_round_sharded_x24), which reruns the round from the uncommitted state.
 static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const shd_round* rd,
@@ -2926,15 +2991,27 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
                              ran ? R.bin_base.as<uint32_t>() + n_bins + 1 : nullptr, n_bins, ran ? 1u : 0u,
                              (int32_t)st, R.x_cap, n, (ok7 && abs_seq) ? 0u : kXsHost, (int32_t)SHD_ERR_NO_HOST,
                              (int32_t)SHD_ERR_INVALID, rows + (size_t)me * rw);
-    if (hipGetLastError() != hipSuccess && st == SHD_OK) st = SHD_ERR_HIP;   // (rides in no row: the collective must run)
+    if (hipGetLastError() != hipSuccess) {
+        // the row the peers size the exchange from must carry the failure: written from the host
+        if (st == SHD_OK) st = SHD_ERR_HIP;
+        std::vector<uint64_t> hrow(rw, 0);
+        hrow[0] = (uint64_t)(int64_t)st;
+        hrow[1] = hrow[2] = ~0ull;
+        (void)hipMemcpy(rows + (size_t)me * rw, hrow.data(), rw * 8, hipMemcpyHostToDevice);
+    }
     SHD_TRY(C.all_gather(rows + (size_t)me * rw, rows, rw * 8, s));   // agreed (LocalComm) / fatal (RCCL)
-    // 2. the sizing summary, one host sync
+    // 2. the sizing summary, one host sync.  From here on a local failure is carried into the
+    //    exchange (its status part) instead of returned: the peers are on their way to it.  A
+    //    failure of the summary's own read-back leaves this rank without the sizes, which is fatal
+    //    to the communicator, as an RCCL failure is.
+    shd_status st_post = SHD_OK;
     uint32_t* xb = R.xs_b.as<uint32_t>();
     xs_scan<<<world, 1024, 0, s>>>(rows, rw, n_bins, R.xs_sc.as<uint32_t>());
     xs_mat<<<1, 256, 0, s>>>(rows, rw, R.xs_sc.as<uint32_t>(), n_bins, world, me, xsh.bpr, R.xs_out.as<uint64_t>(), xb);
     const size_t out_words = 1 + (size_t)world * kXsHead + (size_t)world * world;
     SHD_TRY(readback_into(ctx, s, R.xs_out.p, out_words * 8, R.xs_pin.as<unsigned long long>()));
-    if (st != SHD_OK) return st;   // (a launch failure after the gather: local, no collective follows)
+    if (hipGetLastError() != hipSuccess) st_post = SHD_ERR_HIP;
+    if (ctx->knobs.get(K_TEST_FAIL, 0) == 1) st_post = SHD_ERR_HIP;   // (fault injection, tests)
     const uint64_t* pin = R.xs_pin.as<uint64_t>();
     auto hdr = [&](uint32_t q) { return pin + 1 + (size_t)q * kXsHead; };
     auto M = [&](uint32_t q, uint32_t r) { return pin[1 + (size_t)world * kXsHead + (size_t)q * world + r]; };
@@ -2973,53 +3050,67 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
         SHD_TRY(C.all_gather(agree + me, agree, 8, s));
         std::vector<uint64_t> a(world);
         SHD_HIP(hipMemcpyAsync(a.data(), agree, world * 8, hipMemcpyDeviceToHost, s));
-        SHD_HIP(hipStreamSynchronize(s));
+        SHD_HIP(hipStreamSynchronize(s));   // (a failed read-back of the agreement: fatal, as above)
         for (uint32_t q = 0; q < world; ++q)
             if ((shd_status)a[q] != SHD_OK) return (shd_status)a[q];
-        if (gs != SHD_OK) return gs;
     }
-    // 3. the exchange: the records of rank r's bins, as the stamp laid them out (own: none)
-    std::vector<const void*> sp(world);
-    std::vector<void*> rp(world);
-    std::vector<size_t> sb(world), rb(world);
+    // 3. the exchange: part 0 is the sender's status after the gather (every rank learns every
+    //    peer's, under RCCL too), part 1 the records of rank r's bins as the stamp laid them out
+    //    (own: none)
+    uint64_t* xst = R.xs_st.as<uint64_t>();
+    if (st_post != SHD_OK || R.xs_st_dirty) {
+        if (hipMemsetD32Async(xst, (uint32_t)st_post, 1, s) != hipSuccess && st_post == SHD_OK) st_post = SHD_ERR_HIP;
+        R.xs_st_dirty = st_post != SHD_OK;
+    }
+    std::vector<const void*> sp(2 * (size_t)world);
+    std::vector<void*> rp(2 * (size_t)world);
+    std::vector<size_t> sb(2 * (size_t)world), rb(2 * (size_t)world);
     uint64_t sent_before = 0, recv_before = 0;
     for (uint32_t r = 0; r < world; ++r) {
-        sp[r] = R.rec.as<uint4>() + sent_before;
-        sb[r] = r == me ? 0 : (size_t)M(me, r) * 16;
+        sp[2 * r] = xst;
+        sb[2 * r] = r == me ? 0 : 8;
+        rp[2 * r] = xst + 1 + r;
+        rb[2 * r] = r == me ? 0 : 8;
+        sp[2 * r + 1] = R.rec.as<uint4>() + sent_before;
+        sb[2 * r + 1] = r == me ? 0 : (size_t)M(me, r) * 16;
         sent_before += M(me, r);
-        rp[r] = R.x_rrec.as<uint4>() + recv_before;
-        rb[r] = r == me ? 0 : (size_t)M(r, me) * 16;
+        rp[2 * r + 1] = R.x_rrec.as<uint4>() + recv_before;
+        rb[2 * r + 1] = r == me ? 0 : (size_t)M(r, me) * 16;
         if (r != me) recv_before += M(r, me);
     }
-    SHD_TRY(C.exchange(1, sp.data(), sb.data(), rp.data(), rb.data(), s));   // agreed (LocalComm) / fatal (RCCL)
-    // 4. the bin sort of this rank's bins over every sender's records (no collective follows)
+    SHD_TRY(C.exchange(2, sp.data(), sb.data(), rp.data(), rb.data(), s, st_post));   // agreed (LocalComm, HostComm)
+    // 4. the bin sort of this rank's bins over every sender's records; it also combines the
+    //    statuses of part 0, which come back with the event count (no collective follows)
     uint32_t own_lo = 0, own_hi = 0;
     shard_range(H, (int)world, (int)me, &own_lo, &own_hi);
     const uint32_t n_own = own_hi - own_lo;
     const uint32_t fb_me = xsh.first_bin(me), nb = xsh.first_bin(me + 1) - fb_me;
+    uint32_t kq = 0;
+    while ((kq ? 2 * kq : 1u) < world) kq = kq ? 2 * kq : 1u;
+    XSrc xs{world, me, fb_me, n_bins + 1, kq, R.xs_sc.as<uint32_t>(), xb, xb + world, R.rec.as<uint4>(),
+            xst + 1, (uint32_t)st_post};
     if (nb) {
         V7Out vo{R.m_deliver.as<uint64_t>(), R.m_src.as<uint32_t>(), R.m_seq.as<uint64_t>(), R.m_pkt.as<uint32_t>(),
                  nullptr, rd->round_end};
-        uint32_t kq = 0;
-        while ((kq ? 2 * kq : 1u) < world) kq = kq ? 2 * kq : 1u;
-        XSrc xs{world, me, fb_me, n_bins + 1, kq, R.xs_sc.as<uint32_t>(), xb, xb + world, R.rec.as<uint4>()};
         bin_sort_v7<true><<<nb, kB7Threads, 0, s>>>(n_own, nb, nullptr, R.x_rrec.as<uint4>(),
                                                     R.bin_lb.as<unsigned long long>(), R.m_off.as<uint32_t>(), vo,
                                                     nullptr, 0u, xs);
     } else {
-        SHD_HIP(hipMemsetAsync(R.m_off.p, 0, 4, s));
+        xs_fin_empty<<<1, 64, 0, s>>>(xs, R.m_off.as<uint32_t>());
     }
     SHD_HIP(hipGetLastError());
+    // 5. the number of events this rank received (= its destinations' sent events) and the agreed
+    //    status: 16 aligned bytes holding m_off[n_own] and m_off[n_own + 1]
+    SHD_TRY(readback_into(ctx, s, R.m_off.as<uint32_t>() + (n_own & ~1u), 16, R.xs_pin.as<unsigned long long>()));
+    const uint32_t n_ev = R.xs_pin.as<uint32_t>()[n_own & 1u];
+    const shd_status agreed = (shd_status)R.xs_pin.as<uint32_t>()[(n_own & 1u) + 1];
+    if (agreed != SHD_OK) return agreed;   // every rank: nothing of the hosts' state is committed
     R.red_host[0] = hdr(me)[1];
     R.red_host[1] = hdr(me)[2];
     R.red_host[2] = hdr(me)[3];
     R.last_pipe = 8;   // pipeline 7's stamp, its bins exchanged and sorted by their destination ranks
     R.last_v2 = true;
     SHD_TRY(relay_commit(ctx, &lo));
-    // 5. the number of events this rank received (= its destinations' sent events)
-    // (8 aligned bytes holding m_off[n_own]; m_off has room past its n_own + 1 words)
-    SHD_TRY(readback_into(ctx, s, R.m_off.as<uint32_t>() + (n_own & ~1u), 8, R.xs_pin.as<unsigned long long>()));
-    const uint32_t n_ev = R.xs_pin.as<uint32_t>()[n_own & 1u];
     d_out->ev_off = R.m_off.as<uint32_t>();
     d_out->ev_deliver = R.m_deliver.as<uint64_t>();
     d_out->ev_src = R.m_src.as<uint32_t>();

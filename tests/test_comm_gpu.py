@@ -141,6 +141,49 @@ def test_local_two_ranks_failure_is_global(engine):
             e.close()
 
 
+def test_local_two_ranks_failure_after_gather_is_global(engine, knob):
+    """A failure on rank 1 after the sizing gather (injected: TEST_FAIL=1) rides the exchange's
+    status part: both ranks return it, neither commits host state, and the next round, with the
+    failure gone, is bit-exact against the restatement (advisor round 5)."""
+    from shadow_amd import dist as D
+    from shadow_amd import synth
+    from shadow_amd._native import ShdError
+    from shadow_amd.routing import Engine
+    H, NN = 1000, 20
+    _, lat, loss, host_node, rng0 = _case(H, NN, 5)
+    engines = [Engine(0), Engine(0)]
+    try:
+        D.comm_init_local(engines)
+        rels = [D.ShardedRelay(e, host_node, rng0, np.zeros(H, np.uint64), lat, loss) for e in engines]
+        b = synth.packet_batch(H, 50_000, 10**9, 10**9 + 10**6, seed=7)
+        parts = [_slice_batch(b, r.lo, r.hi) for r in rels]
+        rd = (10**9 + 10**6, 10**12, 0)
+
+        def go(r, p):
+            try:
+                r.round(*p[:4], rd)
+            except ShdError as e:
+                return e.code
+            return "OK"
+        knob("TEST_FAIL", 1, eng=engines[1])
+        codes = _run_ranks([lambda r=r, p=p: go(r, p) for r, p in zip(rels, parts)])
+        assert codes == ["HIP", "HIP"]
+        for r in rels:
+            st, nid = r.host_state()
+            assert np.array_equal(st, rng0) and not nid.any()
+        knob("TEST_FAIL", 0, eng=engines[1])
+        o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(),
+                             np.zeros(H, np.uint64), *rd)
+        outs = _run_ranks([lambda r=r, p=p: r.round(*p[:4], rd) for r, p in zip(rels, parts)])
+        assert [r.last_pipeline() for r in rels] == [8, 8]
+        bases = np.array([p[4] for p in parts], np.int64)
+        for r, out in zip(rels, outs):
+            _check_rank(out, o, r.lo, r.hi, lambda src: bases[(src >= 500).astype(np.int64)], b)
+    finally:
+        for e in engines:
+            e.close()
+
+
 @pytest.mark.parametrize("chunk_rows", [None, 7, 64, "replicate"])
 def test_local_two_ranks_routing_sharded(engine, chunk_rows):
     """Row shards + the table exchange: one all-gather, or row chunks exchanged while the next

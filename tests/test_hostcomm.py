@@ -142,9 +142,19 @@ def _gpu_worker(rank, world, port, q):
             rd = (start + ra, start + 10**12, start + ra // 2 if rnd == 0 else 0)
             rounds.append(rel.round(off, b.send_time[a:e], b.dst_host[a:e], b.payload[a:e], rd))
             start += ra
+        # a rank whose staging cannot be allocated (injected on rank 1) still takes part: the
+        # staging status round fails the next round on both ranks, and neither commits it
+        if rank == 1:
+            eng.set_knob("TEST_FAIL", 3)
+        try:
+            rel.round(off, b.send_time[a:e], b.dst_host[a:e], b.payload[a:e], rd)
+            fail_code = "OK"
+        except N.ShdError as ex:
+            fail_code = ex.code
+        eng.set_knob("TEST_FAIL", 0)
         st, nid = rel.host_state()
         q.put((rank, dict(table=table, rounds=rounds, lo=rel.lo, hi=rel.hi, rng=st[rel.lo:rel.hi].copy(),
-                          nid=nid[rel.lo:rel.hi].copy())))
+                          nid=nid[rel.lo:rel.hi].copy(), fail_code=fail_code)))
         del hc
         eng.close()
     finally:
@@ -160,6 +170,7 @@ def test_host_comm_two_processes_routing_and_relay():
     el = synth.complete_graph(n, 12)
     code, lat, loss, _ = corc.routing(n, el.src, el.dst, el.latency_ns, el.packet_loss, False,
                                       np.arange(n, dtype=np.uint32))
+    assert [res[r]["fail_code"] for r in (0, 1)] == ["NOMEM", "NOMEM"]
     for r in (0, 1):
         assert np.array_equal(res[r]["table"][0], lat)
         assert np.array_equal(res[r]["table"][1], loss.view(np.uint32))

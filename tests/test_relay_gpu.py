@@ -296,10 +296,11 @@ def test_bin_pipeline_failed_round_keeps_state(engine):
         assert np.array_equal(getattr(r, "ev_" + k), o["events"][k]), k
 
 
-def test_bin_pipeline_slot_counter_overflow_falls_back(engine):
+def test_bin_pipeline_large_workgroup_segment_stays_on_bins(engine):
     """64 hosts = one stamp workgroup, 5,000 sends into two bins: every bin fits pipeline 7's
-    LDS stage but the workgroup's 8-bit slot counters would overflow, so the round reruns on
-    the radix pipeline, bit-exact."""
+    LDS stage, and the workgroup's segment of each (~2,500 records) is far past the 8-bit slot
+    counters the stamp had before round 6, which made this round rerun on the radix pipeline.
+    The counters are 32-bit now: pipeline 7, bit-exact."""
     from shadow_amd.relay import Relay
     H, NN = 64, 8
     lat, loss, host_node, rng0, b = _c5_like(H, NN, 5_000, 23)
@@ -308,7 +309,7 @@ def test_bin_pipeline_slot_counter_overflow_falls_back(engine):
                          orng, onid, 10**9 + 10**6, 10**12, 0)
     rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
     r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, 10**9 + 10**6, 10**12, 0)
-    assert rl.last_pipeline() == 3
+    assert rl.last_pipeline() == 7
     assert np.array_equal(r.status, o["status"]) and np.array_equal(r.ev_off, o["events"]["off"])
     for k in ("deliver", "src", "seq", "pkt"):
         assert np.array_equal(getattr(r, "ev_" + k), o["events"][k]), k

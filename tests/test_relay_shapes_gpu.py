@@ -87,7 +87,7 @@ def _check_single(engine, lat, loss, host_node, rng0, nid0, b, rd):
                          nid0.copy(), *rd)
     rl = Relay(host_node, rng0, nid0, lat, loss, engine=engine)
     r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, *rd)
-    assert rl.last_pipeline() in (7, 3)   # 3: a workgroup's 8-bit bin slot counter would overflow
+    assert rl.last_pipeline() in (7, 3)   # 3: a bin over bin_sort_v7's LDS stage
     bad = np.flatnonzero(r.status != o["status"])
     assert len(bad) == 0, f"{len(bad)} status mismatches, first at sends {bad[:8].tolist()}"
     ev = o["events"]
