@@ -502,6 +502,156 @@ def relay_leg(eng, world, rank, steps, warmup, lat_table, loss_table, counters=F
                 pipeline=int(pipe.value), host_node=host_node, rng0=rng0, start=start, rd=rd)
 
 
+C5B_HOSTS, C5B_PACKETS, C5B_SLICE_HOSTS = 100_000, 10_000_000, 10_000
+
+
+def c5b_setup(eng, seed=6):
+    """C5b ("to stress random gathers"): the C5 round on the C4 table.  The 50k-node
+    BA graph's whole 50k x 50k table is built into the engine's resident table (no copy leaves
+    the GPU) and the relay runs on it: 100k hosts, host h on node h mod 50,000, 10M sends.  At
+    16 bits per host the host -> node map does not fit the stamp's LDS, so the round runs on
+    pipeline 3 (relay_stamp_v5: global gathers of the destinations' nodes and of the 20 GB packed
+    path table, radix sort by destination, per-destination sort)."""
+    from shadow_amd import _native as N
+    from shadow_amd import synth
+    el = synth.barabasi_albert(50_000, 4, 3)
+    n = prepare(eng, el)
+    log("c5b: graph prepared")
+    err = N.Error()
+    N.check(eng.lib.shd_routing_run(eng.ctx, N.ALGO_DELTA, 0, 0, None, None, C.byref(err)), "routing_run", err)
+    log("c5b: resident table built")
+    H, P = C5B_HOSTS, C5B_PACKETS
+    start, ra = synth.SIM_START + 10**9, 10**6
+    b = synth.packet_batch(H, P, start, start + ra, seed=seed)
+    host_node = (np.arange(H, dtype=np.uint64) % n).astype(np.uint32)
+    rng0 = synth.host_rng_states(H, 2)
+    nid0 = np.zeros(H, np.uint64)
+    log("c5b: batch made")
+    N.check(eng.lib.shd_relay_setup(eng.ctx, H, N.ptr(host_node), n, None, None, N.ptr(rng0), N.ptr(nid0)),
+            "relay_setup (resident C4 table)")
+    log("c5b: relay set up")
+    N.check(eng.lib.shd_relay_set_counters(eng.ctx, 0), "set_counters")
+    return dict(el=el, n=n, H=H, P=P, b=b, host_node=host_node, rng0=rng0, rd=(start + ra, start + 10**12, 0))
+
+
+def c5b_slice_check(eng, cs, status, ev_off, ev_deliver, ev_src, ev_seq, ev_pkt, threads=0, time_it=False):
+    """The first round from the setup state against the C restatement on its first 10k source hosts
+    (~1M sends): the oracle needs the table only at the pairs those sends use, which come from the
+    engine's resident table (shd_routing_lookup_batch) into a lazily allocated n x n array (only
+    the touched pages are committed).  Statuses of those sends, and every destination's events
+    from those sources (the round's events filtered to src < 10k: a sorted list filtered stays
+    sorted; packet indices agree, the slice being the batch's first sends)."""
+    from oracle import corc
+    from shadow_amd import _native as N
+    b, n, hn = cs["b"], cs["n"], cs["host_node"]
+    k = C5B_SLICE_HOSTS
+    e = int(b.src_off[k])
+    src_of = np.repeat(np.arange(k, dtype=np.uint32), np.diff(b.src_off[:k + 1]).astype(np.int64))
+    dst = np.minimum(b.dst_host[:e], cs["H"] - 1)
+    rows, cols = hn[src_of], hn[dst]
+    lat_v = np.zeros(e, np.uint64)
+    loss_v = np.zeros(e, np.float32)
+    N.check(eng.lib.shd_routing_lookup_batch(eng.ctx, e, N.ptr(np.ascontiguousarray(rows)),
+                                             N.ptr(np.ascontiguousarray(cols)), N.ptr(lat_v), N.ptr(loss_v)),
+            "lookup_batch")
+    lat = np.zeros((n, n), np.uint64)      # calloc: pages are committed only where written
+    loss = np.zeros((n, n), np.float32)
+    lat[rows, cols] = lat_v
+    loss[rows, cols] = loss_v
+    # every host stays in the batch (the oracle's per-host state and destination queues cover
+    # all of them); the hosts past the slice send nothing
+    off = np.concatenate([b.src_off[:k + 1], np.full(cs["H"] - k, b.src_off[k], b.src_off.dtype)])
+    reps, t0 = 0, time.perf_counter()
+    while True:   # (time_it: repeated for the CPU baseline, ~3 s of CPU work)
+        o = corc.relay_round(off, b.send_time[:e], b.dst_host[:e], b.payload[:e], hn, lat, loss,
+                             cs["rng0"].copy(), np.zeros(cs["H"], np.uint64), *cs["rd"], threads=threads)
+        reps += 1
+        if not time_it or time.perf_counter() - t0 > 3.0 or reps >= 50:
+            break
+    dt = (time.perf_counter() - t0) / reps
+    oe = o["events"]
+    keep = ev_src < k
+    ok = bool(np.array_equal(status[:e], o["status"]) and
+              np.array_equal(ev_deliver[keep], oe["deliver"]) and np.array_equal(ev_src[keep], oe["src"]) and
+              np.array_equal(ev_seq[keep], oe["seq"]) and np.array_equal(ev_pkt[keep], oe["pkt"]))
+    # per destination: the filtered counts are the oracle's offsets
+    cnt = np.bincount(np.repeat(np.arange(cs["H"]), np.diff(ev_off.astype(np.int64)))[keep], minlength=cs["H"])
+    ok = ok and bool(np.array_equal(np.concatenate([[0], np.cumsum(cnt)]).astype(np.uint32), oe["off"]))
+    del lat, loss
+    return (ok, e, dt) if time_it else ok
+
+
+def c5b_leg(eng, steps=5, warmup=1, cpu=True):
+    import torch
+    from shadow_amd import _native as N
+    cs = c5b_setup(eng)
+    H, P, b = cs["H"], cs["P"], cs["b"]
+    d_off, d_time = _dev(b.src_off, np.int32), _dev(b.send_time, np.int64)
+    d_dst, d_pay = _dev(b.dst_host, np.int32), _dev(b.payload, np.int32)
+    st = torch.empty(P, dtype=torch.uint8, device="cuda")
+    ev_off = torch.empty(H + 1, dtype=torch.int32, device="cuda")
+    ev_deliver = torch.empty(P, dtype=torch.int64, device="cuda")
+    ev_src = torch.empty(P, dtype=torch.int32, device="cuda")
+    ev_seq = torch.empty(P, dtype=torch.int64, device="cuda")
+    ev_pkt = torch.empty(P, dtype=torch.int32, device="cuda")
+    batch = N.Batch(P, N.ptr(d_off).value, N.ptr(d_time).value, N.ptr(d_dst).value, N.ptr(d_pay).value, None)
+    out = N.RelayOut(N.ptr(st).value, N.ptr(ev_off).value, N.ptr(ev_deliver).value,
+                     N.ptr(ev_src).value, N.ptr(ev_seq).value, N.ptr(ev_pkt).value, 0, 0, 0)
+    rnd = N.Round(*cs["rd"])
+
+    def step():
+        N.check(eng.lib.shd_relay_round_device(eng.ctx, C.byref(batch), C.byref(rnd), C.byref(out)),
+                "relay_round_device (C5b)")
+        return out.n_sent
+    step()   # the first round from the setup state: checked
+    torch.cuda.synchronize()
+    u32 = lambda t: t.cpu().numpy().view(np.uint32)   # noqa: E731
+    u64 = lambda t: t.cpu().numpy().view(np.uint64)   # noqa: E731
+    ns = out.n_sent
+    ok, e, cdt = c5b_slice_check(eng, cs, st.cpu().numpy(), u32(ev_off), u64(ev_deliver)[:ns], u32(ev_src)[:ns],
+                                 u64(ev_seq)[:ns], u32(ev_pkt)[:ns], threads=cpu_threads(), time_it=True)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ms = dt / steps * 1e3
+    pipe = C.c_int32(0)
+    N.check(eng.lib.shd_relay_last_pipeline(eng.ctx, C.byref(pipe)), "last_pipeline")
+    bytes_round = RELAY_BYTES_PER_PACKET * P + RELAY_BYTES_PER_HOST * H
+    ach = bytes_round / (ms * 1e-3) / 1e9
+    res = {"workload": "C5b: the C5 round on the C4 table -- 100k hosts, host h on node h mod 50,000 of the "
+                       "50k-node BA m=4 graph (table built by the engine, resident), 10M sends per round",
+           "hosts": H, "packets": P, "nodes": cs["n"], "steps": steps, "ms_per_round": ms,
+           "value": P / (ms * 1e-3), "unit": "packets/s", "pipeline": int(pipe.value),
+           "n_sent_last_round": int(out.n_sent),
+           "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ach / HBM_PEAK_GBS,
+                        "work": "84 B/packet + 80 B/host algorithmic (SURVEY 8(d)), whole round; the 8-byte path "
+                                "entries are random gathers from the 20 GB packed table"},
+           "bit_exact_vs_cpu_slice": ok,
+           "checked": f"first round, sends of source hosts 0-{C5B_SLICE_HOSTS - 1} ({e}): statuses and every "
+                      f"destination's events from them, against the C restatement"}
+    if cpu:
+        res["cpu_baseline"] = {"value": e / cdt, "unit": "packets/s", "cores": cpu_threads(), "kind": "port",
+                               "sample": f"the check's C restatement: {e} sends of the first {C5B_SLICE_HOSTS} "
+                                         f"source hosts on the C4 table (per-packet send_packet restatement, "
+                                         f"per-destination heap push, OpenMP over source hosts), {cdt * 1e3:.1f} ms "
+                                         f"per run, repeated for ~3 s",
+                               "bit_exact_vs_gpu": ok, **cpu_info()}
+    del d_off, d_time, d_dst, d_pay, st, ev_off, ev_deliver, ev_src, ev_seq, ev_pkt
+    torch.cuda.empty_cache()
+    return res
+
+
+def cpu_threads():
+    from oracle import corc
+    return corc.max_threads()
+
+
 def relay_check_sharded(eng, world, rank, rl, lat_table, loss_table):
     """N > 1: one sharded round from the setup state, every rank's statuses and destination events
     against the C restatement of the whole round (the RCCL exchange's own test at this size)."""
@@ -1004,6 +1154,7 @@ def main():
     ap.add_argument("--no-relay", action="store_true")
     ap.add_argument("--no-c3", action="store_true")
     ap.add_argument("--no-c4", action="store_true")
+    ap.add_argument("--no-c5b", action="store_true")
     ap.add_argument("--no-codel", action="store_true")
     ap.add_argument("--no-tbucket", action="store_true")
     ap.add_argument("--no-equeue", action="store_true")
@@ -1109,6 +1260,8 @@ def main():
         res["c4"] = c4_leg(eng, world, rank, args.c4_steps, gather=not args.c4_no_gather, cpu=cpu)
         if "check" in res["c4"]:
             checks["c4_last_rows_bit_exact"] = res["c4"].pop("check")
+    if world == 1 and not args.no_c5b:
+        res["c5b"] = c5b_leg(eng, cpu=cpu)
     if checks:
         res["parity_check"] = checks
     if world == 1 and not args.no_codel:

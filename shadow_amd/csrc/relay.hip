@@ -500,6 +500,10 @@ constexpr uint32_t kS5Per = 4;                  // sends per thread per chunk
 constexpr uint32_t kS5Cap = 256 * kS5Per;
 constexpr uint32_t kS5RowLds = 2048;            // staged path-table entries (16 KB)
 
+// (round 6: the chunk's loads issued together -- the sends' fields, then the destinations' nodes,
+// then the path entries, each a batch of independent loads -- instead of one guarded chain per
+// send; CH as relay_stamp_v6's)
+template <bool CH>
 __global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint32_t* __restrict__ draw) {
     __shared__ uint2 s_rows[kS5RowLds];
     __shared__ uint16_t s_scan[kS5Cap + 1];
@@ -556,45 +560,68 @@ __global__ __launch_bounds__(256) void relay_stamp_v5(RelayArgs3 a, const uint32
         const uint32_t cn = min(kS5Cap, T - c0);
         uint8_t st[kS5Per];
         uint32_t doff[kS5Per], dst[kS5Per], idx[kS5Per], hl[kS5Per], dn[kS5Per];
+        bool k0[kS5Per];
+        // (a) owners and packet indices (positions past the chunk clamped onto its last packet,
+        // so every load below is in bounds and unconditional)
+#pragma unroll
+        for (uint32_t i = 0; i < kS5Per; ++i) {
+            const uint32_t gp = c0 + min(tid + 256 * i, cn - 1);
+            uint32_t lo = 0, hi = nh;       // s_pre[lo] <= gp < s_pre[lo + 1]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_pre[mid] <= gp) lo = mid; else hi = mid;
+            }
+            hl[i] = lo;
+            const uint32_t k = gp - s_pre[lo];
+            k0[i] = k == 0;
+            idx[i] = s_beg[lo] + k;
+        }
+        // (b) the sends' fields, (c) their destinations' nodes, (d) the path entries
+        uint64_t now[kS5Per], prv[kS5Per];
+        std::conditional_t<CH, double, uint32_t> rv[kS5Per];
+        uint32_t pay[kS5Per];
+#pragma unroll
+        for (uint32_t i = 0; i < kS5Per; ++i) {
+            now[i] = a.send_time[idx[i]];
+            prv[i] = a.send_time[idx[i] - (k0[i] ? 0u : 1u)];
+            dst[i] = a.dst_host[idx[i]];
+            pay[i] = a.payload[idx[i]];
+            if constexpr (CH) rv[i] = a.chance[idx[i]];
+            else rv[i] = draw[idx[i]];
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kS5Per; ++i) dn[i] = a.host_node[min(dst[i], a.n_hosts - 1)];
+        uint2 pp[kS5Per];
+#pragma unroll
+        for (uint32_t i = 0; i < kS5Per; ++i)
+            pp[i] = staged ? s_rows[s_rowof[hl[i]] * a.n_nodes + dn[i]]
+                           : path_global(a.path, (size_t)s_node[hl[i]] * a.n_nodes + dn[i]);
 #pragma unroll
         for (uint32_t i = 0; i < kS5Per; ++i) {
             const uint32_t pos = tid + 256 * i;
             st[i] = kStSkipped;
-            doff[i] = dst[i] = idx[i] = hl[i] = dn[i] = 0;
+            doff[i] = 0;
             if (pos < cn) {
-                const uint32_t gp = c0 + pos;
-                uint32_t lo = 0, hi = nh;       // s_pre[lo] <= gp < s_pre[lo + 1]
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (s_pre[mid] <= gp) lo = mid; else hi = mid;
-                }
-                hl[i] = lo;
-                const uint32_t k = gp - s_pre[lo];
-                idx[i] = s_beg[lo] + k;
-                const uint64_t now = a.send_time[idx[i]];
-                dst[i] = a.dst_host[idx[i]];
-                const uint32_t pay = a.payload[idx[i]];
                 // a drawing send after a skipped one breaks K0's prefix rule
-                if (k > 0 && now < a.sim_end && !(a.send_time[idx[i] - 1] < a.sim_end)) disorder = true;
+                disorder |= !k0[i] & (now[i] < a.sim_end) & !(prv[i] < a.sim_end);
                 if (dst[i] >= a.n_hosts) {      // "No host ID for dest address" (worker.rs:350-355)
                     atomicMin(&a.red[3], (unsigned long long)idx[i]);
-                } else if (now < a.sim_end) {
-                    dn[i] = a.host_node[dst[i]];
-                    const uint2 pp = staged ? s_rows[s_rowof[lo] * a.n_nodes + dn[i]]
-                                            : path_global(a.path, (size_t)s_node[lo] * a.n_nodes + dn[i]);
-                    const double reliability = (double)one_minus(__uint_as_float(pp.y));
+                } else if (now[i] < a.sim_end) {
+                    const double reliability = (double)one_minus(__uint_as_float(pp[i].y));
                     bool tie = false;
-                    const bool ge = a.chance ? a.chance[idx[i]] >= reliability : draw_drops(draw[idx[i]], reliability, tie);
+                    bool ge;
+                    if constexpr (CH) ge = rv[i] >= reliability;
+                    else ge = draw_drops(rv[i], reliability, tie);
                     wide |= tie;   // a draw whose low bits would decide: redo the round on pipeline 1
-                    if (!(now < a.bootstrap_end) && ge && pay > 0) {
+                    if (!(now[i] < a.bootstrap_end) && ge && pay[i] > 0) {
                         st[i] = kStDropped;
                     } else {
-                        uint64_t tt = now + pp.x;
+                        uint64_t tt = now[i] + pp[i].x;
                         if (tt < a.round_end) tt = a.round_end;
                         const uint64_t dd = tt - a.round_end;
                         wide |= (dd >> 32) != 0;
                         min_d = tt < min_d ? tt : min_d;
-                        min_l = pp.x < min_l ? pp.x : min_l;
+                        min_l = pp[i].x < min_l ? pp[i].x : min_l;
                         doff[i] = (uint32_t)dd;
                         st[i] = kStSent;
                     }
@@ -2138,7 +2165,8 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
         k<<<std::min<uint32_t>(groups, (uint32_t)ctx->n_cu), kS6Threads, (size_t)R.hn_words * 4, s>>>(
             a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
     } else {
-        relay_stamp_v5<<<div_up(R.n_src, kS5Hosts), 256, 0, s>>>(a, R.draws.as<uint32_t>());
+        (a.chance ? relay_stamp_v5<true> : relay_stamp_v5<false>)<<<div_up(R.n_src, kS5Hosts), 256, 0, s>>>(
+            a, R.draws.as<uint32_t>());
     }
     SHD_HIP(hipGetLastError());
     // stable LSD radix sort of the records by destination (keys <= H), hand-written (scan.h)
@@ -2174,11 +2202,15 @@ static bool relay_v7_ok(shd_ctx* ctx, uint64_t n, uint32_t n_bins) {
     // two in-process ranks call the relay from two threads)
     static const size_t stat_lds = [] {
         hipFuncAttributes at{};
-        hipFuncAttributes at2{};   // (the two chance forms' static LDS: the larger)
-        return hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&relay_stamp_v6<true, false>)) == hipSuccess &&
-                       hipFuncGetAttributes(&at2, reinterpret_cast<const void*>(&relay_stamp_v6<true, true>)) == hipSuccess
-                   ? std::max((size_t)at.sharedSizeBytes, (size_t)at2.sharedSizeBytes)
-                   : (size_t)0;
+        // (both chance forms' static LDS: the larger)
+        const void* ks[] = {reinterpret_cast<const void*>(&relay_stamp_v6<true, false>),
+                            reinterpret_cast<const void*>(&relay_stamp_v6<true, true>)};
+        size_t m = 0;
+        for (const void* k : ks) {
+            if (hipFuncGetAttributes(&at, k) != hipSuccess) return (size_t)0;
+            m = std::max(m, (size_t)at.sharedSizeBytes);
+        }
+        return m;
     }();
     if (!stat_lds) return false;
     return stat_lds + (size_t)R.hn_words * 4 + (size_t)n_bins * 4 <= 160 * 1024;

@@ -5,7 +5,8 @@
           middle and the end of the used set, built by the global-label kernel, checked against
           the row-range oracle (orc_shortest_paths_rows);
   * C5 -- 100k hosts x 10M packets per round on the C2 table, two consecutive rounds (RNG
-          streams and event ids carried), every status and every event compared.
+          streams and event ids carried), every status and every event compared;
+  * C5b -- the C5 round on the resident C4 table (50k nodes), checked on a 1M-send slice.
 """
 import numpy as np
 import pytest
@@ -101,3 +102,20 @@ def test_c5_full_two_rounds_bit_exact(engine):
         st, nid = rl.host_state()
         assert np.array_equal(st, orng) and np.array_equal(nid, onid)
         start += ra
+
+
+def test_c5b_relay_on_resident_c4_table(engine):
+    """C5b: 100k hosts on the C4 graph's 50k nodes (host h on node h mod 50,000),
+    10M sends, the relay reading the engine's resident 30 GB C4 table (pipeline 3: the host map
+    does not fit the stamp's LDS).  The first round from the setup state against the C restatement
+    on the sends of source hosts 0-9,999 (~1M): their statuses and every destination's events from
+    them (bench.c5b_slice_check)."""
+    import bench
+    from shadow_amd.relay import Relay
+    cs = bench.c5b_setup(engine)
+    b, H = cs["b"], cs["H"]
+    # the Relay wrapper over the same resident table (lat = None), host buffers in and out
+    rl = Relay(cs["host_node"], cs["rng0"], np.zeros(H, np.uint64), engine=engine)
+    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, *cs["rd"])
+    assert rl.last_pipeline() in (3, 1)
+    assert bench.c5b_slice_check(engine, cs, r.status, r.ev_off, r.ev_deliver, r.ev_src, r.ev_seq, r.ev_pkt)
