@@ -112,10 +112,13 @@ def test_c5b_relay_on_resident_c4_table(engine):
     them (bench.c5b_slice_check)."""
     import bench
     from shadow_amd.relay import Relay
-    cs = bench.c5b_setup(engine)
-    b, H = cs["b"], cs["H"]
-    # the Relay wrapper over the same resident table (lat = None), host buffers in and out
-    rl = Relay(cs["host_node"], cs["rng0"], np.zeros(H, np.uint64), engine=engine)
-    r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, *cs["rd"])
-    assert rl.last_pipeline() in (3, 1)
-    assert bench.c5b_slice_check(engine, cs, r.status, r.ev_off, r.ev_deliver, r.ev_src, r.ev_seq, r.ev_pkt)
+    cs = bench.c5b_setup(engine)   # (turns the per-path counters off: 2 x 20 GB at 50k nodes)
+    try:
+        b, H = cs["b"], cs["H"]
+        # the Relay wrapper over the same resident table (lat = None), host buffers in and out
+        rl = Relay(cs["host_node"], cs["rng0"], np.zeros(H, np.uint64), engine=engine)
+        r = rl.round(b.src_off, b.send_time, b.dst_host, b.payload, *cs["rd"])
+        assert rl.last_pipeline() in (3, 1)
+        assert bench.c5b_slice_check(engine, cs, r.status, r.ev_off, r.ev_deliver, r.ev_src, r.ev_seq, r.ev_pkt)
+    finally:   # the session engine's default for the tests that follow
+        assert engine.lib.shd_relay_set_counters(engine.ctx, 1) == 0
