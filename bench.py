@@ -509,9 +509,9 @@ def c5b_setup(eng, seed=6):
     """C5b ("to stress random gathers"): the C5 round on the C4 table.  The 50k-node
     BA graph's whole 50k x 50k table is built into the engine's resident table (no copy leaves
     the GPU) and the relay runs on it: 100k hosts, host h on node h mod 50,000, 10M sends.  At
-    16 bits per host the host -> node map does not fit the stamp's LDS, so the round runs on
-    pipeline 3 (relay_stamp_v5: global gathers of the destinations' nodes and of the 20 GB packed
-    path table, radix sort by destination, per-destination sort)."""
+    16 bits per host the host -> node map does not fit the stamp's LDS, so the stamp gathers the
+    destinations' nodes from global memory and the path entries from the 20 GB packed table
+    (relay_stamp_v6<MAP = false>), and the records still go to their destination bins (pipeline 7)."""
     from shadow_amd import _native as N
     from shadow_amd import synth
     el = synth.barabasi_albert(50_000, 4, 3)

@@ -314,8 +314,9 @@ __global__ __launch_bounds__(256) void segment_sort_big(
 //   K1 relay_stamp_v5   workgroup per 64 source hosts (in source-node order), lane per send:
 //                       coalesced loads, path lookup (LDS-staged rows), drop rule, deliver
 //                       stamp, scan-based event ids, coalesced stores of status / key / record
-//   K2 rocPRIM onesweep radix sort of the records by destination -- stable: the batch is in
-//      (source host, event id) order, so every destination's run stays in that order
+//   K2 stable LSD radix sort of the records by destination (scan.h rs_hist / rs_scatter, 6-bit
+//      digits) -- stable: the batch is in (source host, event id) order, so every
+//      destination's run stays in that order
 //   K3 bucket_offsets   lower bound of every destination in the sorted keys
 //   K4 segment_sort_v4  wave per destination run: bitonic sort in registers of the unique key
 //                       (deliver offset << 32 | position in the run); ties on the deliver time
@@ -754,7 +755,12 @@ constexpr uint32_t kHistSplit = 2;   // histogram rows per stamp workgroup (rela
 // a run-time select: `a.chance ? chance64[i] : draw[i]` compiled to a branch whose join moved the
 // loaded value with an s_waitcnt vmcnt(0), so each of a thread's kS6Per load sets waited for the
 // one before it (four memory round trips per chunk instead of one).
-template <bool BIN, bool CH>
+// MAP = false (round 6, C5b): the host -> node map does not fit the LDS (50k nodes: 16 bits x
+// 100k hosts), so each chunk gathers its destinations' nodes from global memory (a 400 KB array,
+// L2-resident) and, the rows being too long to stage, its path entries from the packed table --
+// each a batch of unconditional loads -- and the records still go straight to their bins
+// (pipeline 7 instead of pipeline 3's radix sort: the bins need only the slot counters in LDS).
+template <bool BIN, bool CH, bool MAP = true>
 __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const uint32_t* __restrict__ draw,
                                                              const uint32_t* __restrict__ packed,
                                                              uint32_t n_words, uint32_t bits) {
@@ -783,7 +789,8 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
 #ifdef SHD_STAMP_PROF
     uint64_t sp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, sp_t = __builtin_amdgcn_s_memtime();
 #endif
-    for (uint32_t i = tid; i < n_words; i += kS6Threads) s_tbl[i] = packed[i];
+    if constexpr (MAP)
+        for (uint32_t i = tid; i < n_words; i += kS6Threads) s_tbl[i] = packed[i];
     if (BIN)
         for (uint32_t b = tid; b < a.n_bins; b += kS6Threads)
             s_slot[b] = a.bin_base[b] + a.seg_pre[(size_t)blockIdx.x * a.n_bins + b];
@@ -855,7 +862,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
         }
         __syncthreads();
         SP_MARK(1);
-        const bool staged = (uint64_t)s_nrows * a.n_nodes <= kS5RowLds;
+        const bool staged = MAP && (uint64_t)s_nrows * a.n_nodes <= kS5RowLds;
         if (staged) {
             const uint32_t tot = s_nrows * a.n_nodes;
             if (have_pf) {   // rows loaded during the previous group (same node list by construction)
@@ -919,14 +926,25 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                 else rv[i] = draw[idx[i]];
             }
             SP_MARK(9);
+            uint32_t dn[kS6Per];
+            uint2 pg[kS6Per];   // (!MAP: the path entries, gathered together)
+            if constexpr (!MAP) {
+#pragma unroll
+                for (uint32_t i = 0; i < kS6Per; ++i) dn[i] = a.host_node[min(dst[i], a.n_hosts - 1)];
+#pragma unroll
+                for (uint32_t i = 0; i < kS6Per; ++i)   // (unconditional: a select on `staged` made
+                                                         // each a branch, waited at its join)
+                    pg[i] = path_global(a.path, (size_t)s_node[hl[i] & kSlot] * a.n_nodes + dn[i]);
+            }
             // (c) decisions
             uint8_t st[kS6Per];
-            uint32_t doff[kS6Per], dn[kS6Per];
+            uint32_t doff[kS6Per];
 #pragma unroll
             for (uint32_t i = 0; i < kS6Per; ++i) {
                 const uint32_t pos = tid + kS6Threads * i;
                 st[i] = kStSkipped;
-                doff[i] = dn[i] = 0;
+                doff[i] = 0;
+                if constexpr (MAP) dn[i] = 0;
                 if (pos < cn) {
                     // a drawing send after a skipped one breaks K0's prefix rule
                     // (bitwise, not short-circuit: a `&&` chain let the compiler sink prv's load
@@ -935,9 +953,14 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
                     if (dst[i] >= a.n_hosts) {      // "No host ID for dest address" (worker.rs:350-355)
                         atomicMin(&a.red[3], (unsigned long long)idx[i]);
                     } else if (now[i] < a.sim_end) {
-                        dn[i] = packed_get(s_tbl, dst[i], bits);
-                        const uint2 pp = staged ? s_rows[s_rowof[hl[i] & kSlot] * a.n_nodes + dn[i]]
-                                                : path_global(a.path, (size_t)s_node[hl[i] & kSlot] * a.n_nodes + dn[i]);
+                        uint2 pp;
+                        if constexpr (MAP) {
+                            dn[i] = packed_get(s_tbl, dst[i], bits);
+                            pp = staged ? s_rows[s_rowof[hl[i] & kSlot] * a.n_nodes + dn[i]]
+                                        : path_global(a.path, (size_t)s_node[hl[i] & kSlot] * a.n_nodes + dn[i]);
+                        } else {
+                            pp = pg[i];   // (no row staging without the LDS map: see `staged`)
+                        }
                         const double reliability = (double)one_minus(__uint_as_float(pp.y));
                         bool tie = false;
                         const bool ge = CH ? __longlong_as_double((long long)rv[i]) >= reliability
@@ -973,7 +996,7 @@ __global__ __launch_bounds__(kS6Threads) void relay_stamp_v6(RelayArgs3 a, const
             SP_MARK(3);
             if (c0 == 0) {   // prefetch the next group's rows; they land while this group runs
                 const uint32_t pn = s_pfn;
-                if (pn && (uint64_t)pn * a.n_nodes <= kS5RowLds) {
+                if (MAP && pn && (uint64_t)pn * a.n_nodes <= kS5RowLds) {
 #pragma unroll
                     for (uint32_t j = 0; j < kPf; ++j) {
                         const uint32_t e = tid + j * kS6Threads;
@@ -2196,7 +2219,7 @@ static shd_status relay_device_v3(shd_ctx* ctx, const shd_batch* b, const shd_ro
 // key fields, and the stamp's LDS (map + slot counters) within the CU's 160 KB
 static bool relay_v7_ok(shd_ctx* ctx, uint64_t n, uint32_t n_bins) {
     RelayState& R = ctx->relay;
-    if (!R.hn_bits || R.force_v3 || R.n_hosts > kV7MaxHosts || n > kV7MaxPackets) return false;
+    if (R.force_v3 || R.n_hosts > kV7MaxHosts || n > kV7MaxPackets) return false;
     if (R.n_src == 0 || std::min<uint32_t>(div_up(R.n_src, kS5Hosts), (uint32_t)ctx->n_cu) > kColMaxG) return false;
     // the stamp's static LDS, asked once (a function-local static: initialised once even when
     // two in-process ranks call the relay from two threads)
@@ -2204,7 +2227,9 @@ static bool relay_v7_ok(shd_ctx* ctx, uint64_t n, uint32_t n_bins) {
         hipFuncAttributes at{};
         // (both chance forms' static LDS: the larger)
         const void* ks[] = {reinterpret_cast<const void*>(&relay_stamp_v6<true, false>),
-                            reinterpret_cast<const void*>(&relay_stamp_v6<true, true>)};
+                            reinterpret_cast<const void*>(&relay_stamp_v6<true, true>),
+                            reinterpret_cast<const void*>(&relay_stamp_v6<true, false, false>),
+                            reinterpret_cast<const void*>(&relay_stamp_v6<true, true, false>)};
         size_t m = 0;
         for (const void* k : ks) {
             if (hipFuncGetAttributes(&at, k) != hipSuccess) return (size_t)0;
@@ -2213,7 +2238,7 @@ static bool relay_v7_ok(shd_ctx* ctx, uint64_t n, uint32_t n_bins) {
         return m;
     }();
     if (!stat_lds) return false;
-    return stat_lds + (size_t)R.hn_words * 4 + (size_t)n_bins * 4 <= 160 * 1024;
+    return stat_lds + (R.hn_bits ? (size_t)R.hn_words * 4 : 0) + (size_t)n_bins * 4 <= 160 * 1024;
 }
 
 // Hosts per stamp group: about S sends per group (SHD_RELAY_GROUP_SENDS, 0 = fixed kS5Hosts),
@@ -2323,9 +2348,11 @@ static shd_status relay_device_v7(shd_ctx* ctx, const shd_batch* b, const shd_ro
                                                        SS.state.as<unsigned long long>(), SS.epoch);
     }
     if (k0 && !k0_inline) SHD_HIP(hipStreamWaitEvent(s, ctx->sev[1], 0));
-    auto* stamp = a.chance ? &relay_stamp_v6<true, true> : &relay_stamp_v6<true, false>;
-    stamp<<<G, kS6Threads, (size_t)R.hn_words * 4 + (size_t)n_bins * 4, s>>>(
-        a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_words, R.hn_bits);
+    // (no LDS host map -- e.g. C5b's 50k nodes -- : the stamp gathers the destinations' nodes)
+    auto* stamp = R.hn_bits ? (a.chance ? &relay_stamp_v6<true, true> : &relay_stamp_v6<true, false>)
+                            : (a.chance ? &relay_stamp_v6<true, true, false> : &relay_stamp_v6<true, false, false>);
+    stamp<<<G, kS6Threads, (R.hn_bits ? (size_t)R.hn_words * 4 : 0) + (size_t)n_bins * 4, s>>>(
+        a, R.draws.as<uint32_t>(), R.hn_packed.as<uint32_t>(), R.hn_bits ? R.hn_words : 0u, R.hn_bits);
     if (xsh) {
         SHD_HIP(hipGetLastError());
         return SHD_OK;
@@ -2746,70 +2773,77 @@ __global__ __launch_bounds__(256) void xs_row(const unsigned long long* __restri
     }
 }
 
-// block q: exclusive scan of sender q's bin counts -> sc[q * (n_bins + 1) + b]
-__global__ __launch_bounds__(1024) void xs_scan(const uint64_t* __restrict__ rows, size_t row_words, uint32_t n_bins,
-                                                uint32_t* __restrict__ sc) {
+// The sizing summary every rank derives alike from the gathered rows, one launch.  Block q:
+// exclusive scan of sender q's bin counts -> sc[q * (n_bins + 1) + b]; the last block to finish
+// (ctr, left at 0 for the next round) then writes out[0] = the largest bin over all senders (the
+// receiver's LDS stage bound), out[1 ..] the world headers, then the record counts M[q][r]
+// (sender q -> rank r); xb[q] = sender q's slice in this rank's received records (own records
+// are not received), xb[world + q] = the packets of the senders before q.
+__global__ __launch_bounds__(1024) void xs_sizing(const uint64_t* __restrict__ rows, size_t row_words, uint32_t n_bins,
+                                                  uint32_t world, uint32_t me, uint32_t bpr, uint32_t* sc,
+                                                  uint64_t* __restrict__ out, uint32_t* __restrict__ xb,
+                                                  uint32_t* ctr) {
     __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_last, s_max;
     const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t* t = reinterpret_cast<const uint32_t*>(rows + (size_t)q * row_words + kXsHead);
-    uint32_t* o = sc + (size_t)q * (n_bins + 1);
-    const uint32_t per = (n_bins + 1023) / 1024, b0 = min(n_bins, tid * per), b1 = min(n_bins, b0 + per);
-    uint32_t sum = 0;
-    for (uint32_t b = b0; b < b1; ++b) sum += t[b];
-    uint32_t incl = sum;
-    for (uint32_t k = 1; k < 64; k <<= 1) {
-        const uint32_t y = __shfl_up(incl, k);
-        if (lane >= k) incl += y;
+    {
+        const uint32_t* t = reinterpret_cast<const uint32_t*>(rows + (size_t)q * row_words + kXsHead);
+        uint32_t* o = sc + (size_t)q * (n_bins + 1);
+        const uint32_t per = (n_bins + 1023) / 1024, b0 = min(n_bins, tid * per), b1 = min(n_bins, b0 + per);
+        uint32_t sum = 0;
+        for (uint32_t b = b0; b < b1; ++b) sum += t[b];
+        uint32_t incl = sum;
+        for (uint32_t k = 1; k < 64; k <<= 1) {
+            const uint32_t y = __shfl_up(incl, k);
+            if (lane >= k) incl += y;
+        }
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        uint32_t run = incl - sum;
+        for (uint32_t u = 0; u < w; ++u) run += s_w[u];
+        for (uint32_t b = b0; b < b1; ++b) {
+            o[b] = run;
+            run += t[b];
+        }
+        if (tid == 1023) o[n_bins] = run;
     }
-    if (lane == 63) s_w[w] = incl;
+    __threadfence();   // this block's scan, visible device-wide before it counts itself done
     __syncthreads();
-    uint32_t run = incl - sum;
-    for (uint32_t u = 0; u < w; ++u) run += s_w[u];
-    for (uint32_t b = b0; b < b1; ++b) {
-        o[b] = run;
-        run += t[b];
+    if (tid == 0) {
+        s_last = atomicAdd(ctr, 1u) == world - 1;
+        s_max = 0;
     }
-    if (tid == 1023) o[n_bins] = run;
-}
-
-// the sizing summary every rank derives alike from the gathered rows: out[0] = the largest bin
-// over all senders (the receiver's LDS stage bound), out[1 ..] the world headers, then the record
-// counts M[q][r] (sender q -> rank r); xb[q] = sender q's slice in this rank's received records
-// (own records are not received), xb[world + q] = the packets of the senders before q
-__global__ __launch_bounds__(256) void xs_mat(const uint64_t* __restrict__ rows, size_t row_words, const uint32_t* __restrict__ sc,
-                                              uint32_t n_bins, uint32_t world, uint32_t me, uint32_t bpr,
-                                              uint64_t* __restrict__ out, uint32_t* __restrict__ xb) {
-    __shared__ uint32_t s_max;
-    const uint32_t t = threadIdx.x;
-    if (t == 0) s_max = 0;
     __syncthreads();
+    if (!s_last) return;
+    __threadfence();   // every block's scan
     uint32_t mx = 0;
-    for (uint32_t b = t; b < n_bins; b += 256) {
+    for (uint32_t b = tid; b < n_bins; b += 1024) {
         uint32_t tot = 0;
-        for (uint32_t q = 0; q < world; ++q) tot += reinterpret_cast<const uint32_t*>(rows + (size_t)q * row_words + kXsHead)[b];
+        for (uint32_t p = 0; p < world; ++p) tot += reinterpret_cast<const uint32_t*>(rows + (size_t)p * row_words + kXsHead)[b];
         mx = max(mx, tot);
     }
     atomicMax(&s_max, mx);
-    for (uint32_t i = t; i < world * kXsHead; i += 256) out[1 + i] = rows[(size_t)(i / kXsHead) * row_words + i % kXsHead];
+    for (uint32_t i = tid; i < world * kXsHead; i += 1024) out[1 + i] = rows[(size_t)(i / kXsHead) * row_words + i % kXsHead];
     uint64_t* M = out + 1 + (size_t)world * kXsHead;
-    for (uint32_t i = t; i < world * world; i += 256) {
-        const uint32_t q = i / world, r = i % world;
-        const uint32_t* sq = sc + (size_t)q * (n_bins + 1);
-        M[i] = sq[min(r * bpr + bpr, n_bins)] - sq[min(r * bpr, n_bins)];
+    for (uint32_t i = tid; i < world * world; i += 1024) {
+        const uint32_t p = i / world, r = i % world;
+        const uint32_t* sp = sc + (size_t)p * (n_bins + 1);
+        M[i] = sp[min(r * bpr + bpr, n_bins)] - sp[min(r * bpr, n_bins)];
     }
-    if (t == 0) {
+    if (tid == 0) {
         uint32_t rb = 0;
         uint64_t pb = 0;
-        for (uint32_t q = 0; q < world; ++q) {
-            const uint32_t* sq = sc + (size_t)q * (n_bins + 1);
-            xb[q] = rb;
-            if (q != me) rb += sq[min(me * bpr + bpr, n_bins)] - sq[min(me * bpr, n_bins)];
-            xb[world + q] = (uint32_t)pb;
-            pb += rows[(size_t)q * row_words + 6];
+        for (uint32_t p = 0; p < world; ++p) {
+            const uint32_t* sp = sc + (size_t)p * (n_bins + 1);
+            xb[p] = rb;
+            if (p != me) rb += sp[min(me * bpr + bpr, n_bins)] - sp[min(me * bpr, n_bins)];
+            xb[world + p] = (uint32_t)pb;
+            pb += rows[(size_t)p * row_words + 6];
         }
+        atomicExch(ctr, 0u);
     }
     __syncthreads();
-    if (t == 0) out[0] = s_max;
+    if (tid == 0) out[0] = s_max;
 }
 
 // sharded rounds' buffers that depend only on the host count and the ranks (shd_relay_setup)
@@ -2826,7 +2860,8 @@ static shd_status relay_shard_alloc(shd_ctx* ctx) {
     const size_t out_bytes = (1 + (size_t)world * kXsHead + (size_t)world * world) * 8 + 64;
     SHD_TRY(R.xs_out.ensure(out_bytes));
     SHD_TRY(R.xs_pin.ensure(out_bytes));
-    SHD_TRY(R.xs_b.ensure((size_t)world * 8 + 64));
+    SHD_TRY(R.xs_b.ensure((size_t)world * 8 + 64));   // xb[2 * world] + xs_sizing's done counter
+    SHD_HIP(hipMemsetAsync(R.xs_b.p, 0, (size_t)world * 8 + 64, ctx->stream));
     SHD_TRY(R.x_off.ensure(((size_t)H + world) * 4));
     SHD_TRY(R.x_roff.ensure((size_t)world * (n_own + 1) * 4 + (size_t)(world + 1) * 4));
     SHD_TRY(R.m_off.ensure((n_own + 4) * 4));   // + the received statuses' word (bin_sort_v7<true>)
@@ -3038,8 +3073,8 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
     //    to the communicator, as an RCCL failure is.
     shd_status st_post = SHD_OK;
     uint32_t* xb = R.xs_b.as<uint32_t>();
-    xs_scan<<<world, 1024, 0, s>>>(rows, rw, n_bins, R.xs_sc.as<uint32_t>());
-    xs_mat<<<1, 256, 0, s>>>(rows, rw, R.xs_sc.as<uint32_t>(), n_bins, world, me, xsh.bpr, R.xs_out.as<uint64_t>(), xb);
+    xs_sizing<<<world, 1024, 0, s>>>(rows, rw, n_bins, world, me, xsh.bpr, R.xs_sc.as<uint32_t>(),
+                                     R.xs_out.as<uint64_t>(), xb, xb + 2 * world);
     const size_t out_words = 1 + (size_t)world * kXsHead + (size_t)world * world;
     SHD_TRY(readback_into(ctx, s, R.xs_out.p, out_words * 8, R.xs_pin.as<unsigned long long>()));
     if (hipGetLastError() != hipSuccess) st_post = SHD_ERR_HIP;
@@ -3131,7 +3166,8 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
         xs_fin_empty<<<1, 64, 0, s>>>(xs, R.m_off.as<uint32_t>());
     }
     SHD_HIP(hipGetLastError());
-    // 5. the number of events this rank received (= its destinations' sent events) and the agreed
+    // 5. the number of events this rank received (= its destinations' SENT events: the bins also
+    //    hold the dropped packets' records, so the record matrix does not give it) and the agreed
     //    status: 16 aligned bytes holding m_off[n_own] and m_off[n_own + 1]
     SHD_TRY(readback_into(ctx, s, R.m_off.as<uint32_t>() + (n_own & ~1u), 16, R.xs_pin.as<unsigned long long>()));
     const uint32_t n_ev = R.xs_pin.as<uint32_t>()[n_own & 1u];
