@@ -4,7 +4,11 @@ on their halves of the same batch, against one context running the whole batch t
 entry point at world size 1.  Both ranks share the device, so their local work adds up to about
 the single context's; what the two-rank round costs beyond it is the exchange between ranks: the sizing
 all-to-all and its host sync, the 24-byte event packing, the exchange and the per-destination
-merge of the two senders' runs.  Prints ms per round for both (median of the timed rounds).
+merge of the two senders' runs.  Prints ms per round for both (median of the timed rounds), and
+first the plain device round (shd_relay_round_device) on the same batch, the baseline of the
+sharded entry point's fixed cost.  Every timed round ends with a device synchronize.  Under
+`rocprofv3 --kernel-trace --memory-copy-trace`, tools/r06_shard_trace.py splits the trace into
+the three legs' rounds and prints one round's phases.
 
     python tools/sharded_round_probe.py [rounds]
 """
@@ -38,6 +42,26 @@ def main():
     b = synth.packet_batch(H, P, start, start + 10**6, seed=4)
     dev = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).view(dt)).cuda()  # noqa: E731
 
+    # ---- the plain device round (shd_relay_round_device), same box, same batch: the baseline the
+    #      sharded entry point's fixed cost is measured against
+    from shadow_amd.relay import Relay
+    e0 = Engine(0)
+    N.check(e0.lib.shd_relay_set_counters(e0.ctx, int(os.environ.get("PROBE_COUNTERS", "0"))), "set_counters")
+    r0 = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=e0)
+    d0 = [dev(b.src_off, np.int32), dev(b.send_time, np.int64), dev(b.dst_host, np.int32), dev(b.payload, np.int32)]
+    bufs = r0.device_buffers(P)
+    t_plain = []
+    for k in range(rounds + 2):
+        d0[1].add_(10**6)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r0.round_device(*d0, start + (k + 2) * 10**6, start + 10**12, 0, bufs)
+        torch.cuda.synchronize()
+        if k >= 2:
+            t_plain.append((time.perf_counter() - t0) * 1e3)
+    e0.close()
+    del d0, bufs
+
     # ---- one context, the whole batch (the sharded entry point at world size 1)
     e1 = Engine(0)
     D.comm_init_local([e1])
@@ -52,6 +76,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         one.round_device(*d1, (start + (k + 2) * 10**6, start + 10**12, 0), st1)
+        torch.cuda.synchronize()
         if k >= 2:
             t_one.append((time.perf_counter() - t0) * 1e3)
     p1 = one.last_pipeline()
@@ -82,12 +107,14 @@ def main():
             t.start()
         for t in ths:
             t.join()
+        torch.cuda.synchronize()
         if k >= 2:
             t_two.append((time.perf_counter() - t0) * 1e3)
     p2 = [r.last_pipeline() for r in rels]
     for e in engines:
         e.close()
-    m1, m2 = statistics.median(t_one), statistics.median(t_two)
+    m0, m1, m2 = statistics.median(t_plain), statistics.median(t_one), statistics.median(t_two)
+    print(f"plain device round (shd_relay_round_device): {m0:.3f} ms; world-1 fixed cost {m1 - m0:.3f} ms", flush=True)
     print(f"one context (world 1), whole C5 round: {m1:.3f} ms; two in-process ranks on the same GPU (halves + "
           f"exchange + merge): {m2:.3f} ms; sharded-path overhead {m2 - m1:.3f} ms per round; pipelines "
           f"{p1} / {p2} (SHD_RELAY_SHARD_X24={os.environ.get('SHD_RELAY_SHARD_X24', '')})", flush=True)
