@@ -38,12 +38,14 @@ static void drop_resident_table(shd_ctx* ctx) {
 }
 
 namespace shd {
-// Wait for the stream by polling a pinned host word that a marker copy, enqueued behind the
-// work, sets to 1: the copy lands when every earlier operation on the stream has completed
+// Wait for the stream by polling a pinned host word that a marker kernel (or copy), enqueued
+// behind the work, sets to 1: the marker lands when every earlier operation on the stream has completed
 // (streams run in order), and the host sees it within a few hundred ns, while
 // hipStreamSynchronize's wake-up costs several us on every synchronous call (the C2 build
 // is ~0.1 ms).  A wait longer than 20 ms (long kernels, or a fault that stops the queue) falls
 // back to hipStreamSynchronize, which also reports a failed kernel.
+shd_status readback_launch(hipStream_t s, const void* d_src, uint32_t n_words, unsigned long long* h_dst,
+                           unsigned long long* h_marker);
 shd_status wait_stream(shd_ctx* ctx, hipStream_t s) {
     if (!ctx->spin_wait) {
         SHD_HIP(hipStreamSynchronize(s));
@@ -51,6 +53,12 @@ shd_status wait_stream(shd_ctx* ctx, hipStream_t s) {
     }
     volatile unsigned long long* done = ctx->h_pin + kPinMarker;
     *done = 0;
+    // the marker from a one-wave kernel (readback_mark, no words): a D2H copy of it goes through
+    // the runtime's blit kernel and left ~30 us of idle device before it (round-6 trace)
+    if (ctx->knobs.get(K_SYNC_KERNEL, 1) != 0) {
+        SHD_TRY(readback_launch(s, nullptr, 0, nullptr, const_cast<unsigned long long*>(done)));
+        return wait_marker(ctx, s);
+    }
     SHD_HIP(hipMemcpyAsync(const_cast<unsigned long long*>(done), ctx->g_one.p, 8, hipMemcpyDeviceToHost, s));
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 1; *done != 1; ++i) {
@@ -60,8 +68,6 @@ shd_status wait_stream(shd_ctx* ctx, hipStream_t s) {
     if (*done != 1) SHD_HIP(hipStreamSynchronize(s));
     return SHD_OK;
 }
-shd_status readback_launch(hipStream_t s, const void* d_src, uint32_t n_words, unsigned long long* h_dst,
-                           unsigned long long* h_marker);
 
 // n_bytes (a multiple of 8) from device memory into the pinned words h_pin[at ...], and wait for
 // everything before it on stream s: one kernel writes the words and then the marker the host polls

@@ -78,6 +78,14 @@ struct LocalGroup {
     std::vector<const void*> ptr;     // published per rank (exchange: n * n * parts pointers)
     std::vector<size_t> bytes;
     std::vector<int> pre, post;       // per rank: status on entry (with its pointers), on exit
+    // per rank, on its device: its inputs are complete (recorded on entry) / its pulls are done
+    // (recorded on exit); peers order their streams on them instead of the host syncing streams
+    std::vector<hipEvent_t> ev_in, ev_out;
+    ~LocalGroup() {
+        for (auto* v : {&ev_in, &ev_out})
+            for (hipEvent_t e : *v)
+                if (e) (void)hipEventDestroy(e);
+    }
     void barrier() {
         std::unique_lock<std::mutex> lk(mu);
         const uint64_t g = gen;
@@ -94,43 +102,53 @@ struct LocalGroup {
 struct LocalComm final : Comm {
     std::shared_ptr<LocalGroup> g;
     int device = 0;
-    shd_ctx* cx = nullptr;   // its context: waits poll the context's pinned marker (wait_stream)
-    // every collective: the rank's inputs are complete (stream sync), pointers and the entry
-    // status are published (barrier), each rank pulls what it receives onto its own stream --
-    // nothing from a rank that entered failed -- syncs, and the exit statuses are agreed (the
-    // lowest failing rank's wins, on every rank); the last barrier keeps the senders' buffers
-    // alive until every pull has finished and the statuses have been read
+    // every collective: the rank's inputs are marked by an event on its stream and its pointers
+    // and entry status are published (barrier); each rank's stream waits for a sender's event,
+    // then pulls what it receives -- nothing from a rank that entered failed; the exit statuses
+    // are agreed (the lowest failing rank's wins, on every rank), and each rank's stream waits
+    // for every peer's pulls to finish before anything after the collective can overwrite what
+    // the peers read.  No host sync of a stream (round 6: each collective cost two polled stream
+    // syncs, ~30 us of idle device apiece -- four of the six host gaps of a world-1 sharded
+    // relay round; one rank alone needs no ordering at all).
     shd_status copy(void* dst, const void* src, int src_dev, size_t n, hipStream_t s) {
         if (!n) return SHD_OK;
         const hipError_t e = src_dev == device ? hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, s)
                                                : hipMemcpyPeerAsync(dst, device, src, src_dev, n, s);
         return e == hipSuccess ? SHD_OK : SHD_ERR_HIP;
     }
-    // (a polled wait: hipStreamSynchronize's wake-up cost ~25 us per collective on a C5 round)
-    shd_status sync(hipStream_t s) { return wait_stream(cx, s); }
     shd_status enter(hipStream_t s) {
-        const shd_status st = sync(s);
+        shd_status st = SHD_OK;
+        if (size > 1 && hipEventRecord(g->ev_in[rank], s) != hipSuccess) st = SHD_ERR_HIP;
         g->pre[rank] = (int)st;
         return st;
     }
+    // before the first pull from rank q: q's inputs are complete
+    shd_status from(int q, hipStream_t s) {
+        return q == rank || hipStreamWaitEvent(s, g->ev_in[q], 0) == hipSuccess ? SHD_OK : SHD_ERR_HIP;
+    }
     shd_status leave(shd_status st, hipStream_t s) {
-        if (sync(s) != SHD_OK && st == SHD_OK) st = SHD_ERR_HIP;
+        if (size == 1) return st;
+        if (hipEventRecord(g->ev_out[rank], s) != hipSuccess && st == SHD_OK) st = SHD_ERR_HIP;
+        g->barrier();   // every rank's pulls are enqueued and marked
+        for (int q = 0; q < size; ++q)
+            if (q != rank && hipStreamWaitEvent(s, g->ev_out[q], 0) != hipSuccess && st == SHD_OK) st = SHD_ERR_HIP;
         g->post[rank] = (int)st;
         g->barrier();
         shd_status all = SHD_OK;
         for (int q = 0; q < size && all == SHD_OK; ++q) all = (shd_status)g->post[q];
-        g->barrier();
+        g->barrier();   // every rank has read the statuses and enqueued its waits before the next collective
         return all;
     }
     shd_status all_to_all_u64(const uint64_t* send, uint64_t* recv, size_t count, hipStream_t s) override {
         shd_status st = enter(s);
         g->ptr[rank] = send;
         g->barrier();
-        for (int q = 0; q < size && st == SHD_OK; ++q)
-            st = g->pre[q] != SHD_OK ? (shd_status)g->pre[q]
-                                     : copy(recv + (size_t)q * count,
-                                            static_cast<const uint64_t*>(g->ptr[q]) + (size_t)rank * count,
-                                            g->device[q], count * 8, s);
+        for (int q = 0; q < size && st == SHD_OK; ++q) {
+            st = g->pre[q] != SHD_OK ? (shd_status)g->pre[q] : from(q, s);
+            if (st == SHD_OK)
+                st = copy(recv + (size_t)q * count, static_cast<const uint64_t*>(g->ptr[q]) + (size_t)rank * count,
+                          g->device[q], count * 8, s);
+        }
         return leave(st, s);
     }
     shd_status exchange(int n_parts, const void* const* send, const size_t* send_bytes, void* const* recv,
@@ -152,6 +170,7 @@ struct LocalComm final : Comm {
                 st = (shd_status)g->pre[q];
                 break;
             }
+            st = from(q, s);
             for (int k = 0; k < n_parts && st == SHD_OK; ++k) {
                 const size_t from = (size_t)q * per_rank + (size_t)rank * n_parts + k;   // q's part k to me
                 const size_t to = (size_t)q * n_parts + k;
@@ -168,7 +187,7 @@ struct LocalComm final : Comm {
         for (int q = 0; q < size && st == SHD_OK; ++q) {
             char* dst = static_cast<char*>(recv) + (size_t)q * bytes;
             if (g->pre[q] != SHD_OK) st = (shd_status)g->pre[q];
-            else if (dst != g->ptr[q]) st = copy(dst, g->ptr[q], g->device[q], bytes, s);
+            else if (dst != g->ptr[q] && (st = from(q, s)) == SHD_OK) st = copy(dst, g->ptr[q], g->device[q], bytes, s);
         }
         return leave(st, s);
     }
@@ -390,13 +409,19 @@ shd_status shd_comm_init_local(shd_ctx** ctxs, int32_t n_ranks) {
     g->bytes.assign(slots, 0);
     g->pre.assign(n_ranks, 0);
     g->post.assign(n_ranks, 0);
-    for (int r = 0; r < n_ranks; ++r) g->device[r] = ctxs[r]->device;
+    g->ev_in.assign(n_ranks, nullptr);
+    g->ev_out.assign(n_ranks, nullptr);
+    for (int r = 0; r < n_ranks; ++r) {
+        g->device[r] = ctxs[r]->device;
+        SHD_HIP(hipSetDevice(ctxs[r]->device));
+        SHD_HIP(hipEventCreateWithFlags(&g->ev_in[r], hipEventDisableTiming));
+        SHD_HIP(hipEventCreateWithFlags(&g->ev_out[r], hipEventDisableTiming));
+    }
     for (int r = 0; r < n_ranks; ++r) {
         auto c = std::unique_ptr<LocalComm>(new (std::nothrow) LocalComm());
         if (!c) return SHD_ERR_NOMEM;
         c->g = g;
         c->device = ctxs[r]->device;
-        c->cx = ctxs[r];
         c->rank = r;
         c->size = n_ranks;
         ctxs[r]->comm = std::move(c);

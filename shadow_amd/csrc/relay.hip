@@ -1967,7 +1967,7 @@ __global__ __launch_bounds__(kB7Threads) void bin_sort_v7(uint32_t n_hosts, uint
     __shared__ uint4 x[kB7Cap];
     __shared__ uint16_t ls[kB7Cap], pm[kB7Cap];
     __shared__ uint32_t s_cnt[kBinDst], s_off[kBinDst + 1], s_cur[kBinDst], s_bin, s_excl;
-    __shared__ uint32_t s_qpre[X ? 65 : 1], s_qat[X ? 64 : 1], s_pb[X ? 64 : 1];
+    __shared__ uint32_t s_pb[X ? 64 : 1];
     // (X: the own sender's records are read from xs.own, every other sender's from rec)
     if (!X && red[6]) return;   // overflow: the host reruns the round on v3
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1976,54 +1976,63 @@ __global__ __launch_bounds__(kB7Threads) void bin_sort_v7(uint32_t n_hosts, uint
     __syncthreads();
     const uint32_t bin = s_bin;
     uint32_t B = 0, N = 0;
-    if constexpr (X) {   // wave 0: every sender's segment of the bin
-        if (tid < 64) {
-            uint32_t c = 0, at = 0, pb = 0;
-            if (lane < xs.world) {
-                const uint32_t* sq = xs.sc + (size_t)lane * xs.stride + xs.fb;
-                const uint32_t a0 = sq[0], a1 = sq[bin], a2 = sq[bin + 1];
-                at = lane == xs.me ? a1 : xs.rbase[lane] + (a1 - a0);
-                c = a2 - a1;
-                pb = xs.pbase[lane];
-            }
-            uint32_t incl = c;
-            for (uint32_t q = 1; q < 64; q <<= 1) {
-                const uint32_t y = __shfl_up(incl, q);
-                if (lane >= q) incl += y;
-            }
-            s_qpre[lane + 1] = incl;
-            if (lane == 0) s_qpre[0] = 0;
-            s_qat[lane] = at;
-            s_pb[lane] = pb;
+    // X: every wave reads the senders' segments of the bin itself (lane q: sender q) and keeps
+    // them in registers, so no wave waits at a barrier for another's loads before its record
+    // loads (measured the same as a wave-0 table in LDS behind a barrier: the X form's extra
+    // ~25 us over bin_sort_v7<false> at world size 1 is its look-back phase, +13 us, and the
+    // loads, +6 us; tools/r06_b7x_phases.sh)
+    uint32_t x_at = 0, x_pre = 0, x_pb = 0;
+    if constexpr (X) {
+        uint32_t c = 0;
+        if (lane < xs.world) {
+            const uint32_t* sq = xs.sc + (size_t)lane * xs.stride + xs.fb;
+            const uint32_t a0 = sq[0], a1 = sq[bin], a2 = sq[bin + 1];
+            x_at = lane == xs.me ? a1 : xs.rbase[lane] + (a1 - a0);
+            c = a2 - a1;
+            x_pb = xs.pbase[lane];
         }
-        __syncthreads();
-        N = s_qpre[xs.world];   // <= kB7Cap: the host checked every bin's total before the exchange
+        uint32_t incl = c;
+        for (uint32_t q = 1; q < 64; q <<= 1) {
+            const uint32_t y = __shfl_up(incl, q);
+            if (lane >= q) incl += y;
+        }
+        x_pre = incl - c;
+        if (w == 0) s_pb[lane] = x_pb;   // (read by the emit, behind later barriers)
+        N = __shfl(incl, xs.world - 1);   // <= kB7Cap: the host checked every bin's total before the exchange
     } else {
         B = bin_base[bin];
         N = bin_base[bin + 1] - B;
     }
     {   // every load of the bin in flight at once (N <= kB7Cap)
         uint4 r[kB7Per];
+        uint32_t qs[kB7Per], pbq[kB7Per];   // X: each record's sender and its packet base
 #pragma unroll
         for (uint32_t u = 0; u < kB7Per; ++u) {
             const uint32_t i = tid + u * kB7Threads;
-            if (i < N) {
-                if constexpr (X) {
-                    uint32_t q = 0;   // the sender of staged index i: the last q with s_qpre[q] <= i
-                    for (uint32_t k = xs.kq; k > 0; k >>= 1)   // (kq: the largest power of two < world)
-                        if (q + k < xs.world && s_qpre[q + k] <= i) q += k;
-                    r[u] = (q == xs.me ? xs.own : rec)[s_qat[q] + (i - s_qpre[q])];
-                    r[u].w += s_pb[q];   // global packet order
-                    r[u].y |= q << 26;   // the sender, for the packet index of the output
-                } else {
-                    r[u] = rec[B + i];
+            if constexpr (X) {
+                // (the shuffles run on every lane, outside the i < N guard: a bpermute must not
+                // read a lane that skipped the computation)
+                uint32_t q = 0;   // the sender of staged index i: the last q with pre[q] <= i
+                for (uint32_t k = xs.kq; k > 0; k >>= 1) {   // (kq: the largest power of two < world)
+                    const uint32_t pk = (uint32_t)__shfl((int)x_pre, (int)min(q + k, xs.world - 1));
+                    if (q + k < xs.world && pk <= i) q += k;
                 }
+                const uint32_t at = (uint32_t)__shfl((int)x_at, (int)q), pre = (uint32_t)__shfl((int)x_pre, (int)q);
+                qs[u] = q;
+                pbq[u] = (uint32_t)__shfl((int)x_pb, (int)q);
+                if (i < N) r[u] = (q == xs.me ? xs.own : rec)[at + (i - pre)];
+            } else {
+                if (i < N) r[u] = rec[B + i];
             }
         }
 #pragma unroll
         for (uint32_t u = 0; u < kB7Per; ++u) {
             const uint32_t i = tid + u * kB7Threads;
             if (i < N) {
+                if constexpr (X) {
+                    r[u].w += pbq[u];          // global packet order
+                    r[u].y |= qs[u] << 26;     // the sender, for the packet index of the output
+                }
                 x[i] = r[u];
                 if (((r[u].y >> 24) & 3u) == kStSent) atomicAdd(&s_cnt[(r[u].y >> 18) & (kBinDst - 1)], 1u);
             }
@@ -2744,10 +2753,10 @@ __global__ __launch_bounds__(256) void xs_row(const unsigned long long* __restri
                                               uint32_t n_bins, uint32_t ran, int32_t st_local, uint64_t cap,
                                               uint64_t n_pkt, uint32_t host_flags, int32_t st_nohost,
                                               int32_t st_invalid, uint64_t* __restrict__ row) {
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, b = blockIdx.x * 256 + t;
     uint32_t* rt = reinterpret_cast<uint32_t*>(row + kXsHead);
-    for (uint32_t b = t; b < n_bins; b += 256) rt[b] = ran ? tot[b] : 0u;
-    if (t == 0) {
+    if (b < n_bins) rt[b] = ran ? tot[b] : 0u;   // a bin per thread (one block: 13 dependent trips, 7 us)
+    if (blockIdx.x == 0 && t == 0) {
         uint64_t st = (uint64_t)(int64_t)st_local, md = ~0ull, ml = ~0ull, ns = 0;
         uint32_t fl = host_flags;
         if (ran) {
@@ -2773,25 +2782,41 @@ __global__ __launch_bounds__(256) void xs_row(const unsigned long long* __restri
     }
 }
 
-// The sizing summary every rank derives alike from the gathered rows, one launch.  Block q:
-// exclusive scan of sender q's bin counts -> sc[q * (n_bins + 1) + b]; the last block to finish
-// (ctr, left at 0 for the next round) then writes out[0] = the largest bin over all senders (the
-// receiver's LDS stage bound), out[1 ..] the world headers, then the record counts M[q][r]
-// (sender q -> rank r); xb[q] = sender q's slice in this rank's received records (own records
-// are not received), xb[world + q] = the packets of the senders before q.
+// bins per thread of xs_sizing's 1024: n_bins <= 2^18 / 32 hosts + 64 ranks (relay_round_sharded_v7)
+constexpr uint32_t kXsPer = 9;
+static_assert(kXsPer * 1024 >= (kV7MaxHosts >> kBinShift) + 64, "xs_sizing: bins per thread");
+
+// The sizing summary every rank derives alike from the gathered rows, one workgroup: sender by
+// sender, the exclusive scan of its bin counts -> sc[q * (n_bins + 1) + b] (a thread's counts in
+// registers); then out[0] = the largest bin over all senders (the receiver's LDS stage bound),
+// out[1 ..] the world headers, then the record counts M[q][r] (sender q -> rank r); xb[q] =
+// sender q's slice in this rank's received records (own records are not received), xb[world +
+// q] = the packets of the senders before q.  (A block per sender with the last one to finish
+// writing the summary took 15 us at world size 1: its device-scope fences write the XCD's L2
+// back after the stamp's stores.  One workgroup needs no fence beyond its own.)
 __global__ __launch_bounds__(1024) void xs_sizing(const uint64_t* __restrict__ rows, size_t row_words, uint32_t n_bins,
                                                   uint32_t world, uint32_t me, uint32_t bpr, uint32_t* sc,
-                                                  uint64_t* __restrict__ out, uint32_t* __restrict__ xb,
-                                                  uint32_t* ctr) {
+                                                  uint64_t* __restrict__ out, uint32_t* __restrict__ xb) {
     __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_last, s_max;
-    const uint32_t q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    {
+    __shared__ uint32_t s_max;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t per = (n_bins + 1023) / 1024, b0 = min(n_bins, tid * per), b1 = min(n_bins, b0 + per);
+    if (tid == 0) s_max = 0;
+    uint32_t tot[kXsPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kXsPer; ++j) tot[j] = 0;
+    for (uint32_t q = 0; q < world; ++q) {
         const uint32_t* t = reinterpret_cast<const uint32_t*>(rows + (size_t)q * row_words + kXsHead);
         uint32_t* o = sc + (size_t)q * (n_bins + 1);
-        const uint32_t per = (n_bins + 1023) / 1024, b0 = min(n_bins, tid * per), b1 = min(n_bins, b0 + per);
+        uint32_t v[kXsPer];   // (per <= kXsPer: every load of the thread in flight at once)
+#pragma unroll
+        for (uint32_t j = 0; j < kXsPer; ++j) v[j] = b0 + j < b1 ? t[b0 + j] : 0u;
         uint32_t sum = 0;
-        for (uint32_t b = b0; b < b1; ++b) sum += t[b];
+#pragma unroll
+        for (uint32_t j = 0; j < kXsPer; ++j) {
+            sum += v[j];
+            tot[j] += v[j];
+        }
         uint32_t incl = sum;
         for (uint32_t k = 1; k < 64; k <<= 1) {
             const uint32_t y = __shfl_up(incl, k);
@@ -2801,29 +2826,22 @@ __global__ __launch_bounds__(1024) void xs_sizing(const uint64_t* __restrict__ r
         __syncthreads();
         uint32_t run = incl - sum;
         for (uint32_t u = 0; u < w; ++u) run += s_w[u];
-        for (uint32_t b = b0; b < b1; ++b) {
-            o[b] = run;
-            run += t[b];
+#pragma unroll
+        for (uint32_t j = 0; j < kXsPer; ++j) {
+            if (b0 + j < b1) o[b0 + j] = run;
+            run += v[j];
         }
         if (tid == 1023) o[n_bins] = run;
+        __syncthreads();   // (s_w is rewritten by the next sender)
     }
-    __threadfence();   // this block's scan, visible device-wide before it counts itself done
-    __syncthreads();
-    if (tid == 0) {
-        s_last = atomicAdd(ctr, 1u) == world - 1;
-        s_max = 0;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();   // every block's scan
     uint32_t mx = 0;
-    for (uint32_t b = tid; b < n_bins; b += 1024) {
-        uint32_t tot = 0;
-        for (uint32_t p = 0; p < world; ++p) tot += reinterpret_cast<const uint32_t*>(rows + (size_t)p * row_words + kXsHead)[b];
-        mx = max(mx, tot);
-    }
+#pragma unroll
+    for (uint32_t j = 0; j < kXsPer; ++j) mx = max(mx, tot[j]);
     atomicMax(&s_max, mx);
     for (uint32_t i = tid; i < world * kXsHead; i += 1024) out[1 + i] = rows[(size_t)(i / kXsHead) * row_words + i % kXsHead];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // the scans' stores, before the reads below
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     uint64_t* M = out + 1 + (size_t)world * kXsHead;
     for (uint32_t i = tid; i < world * world; i += 1024) {
         const uint32_t p = i / world, r = i % world;
@@ -2840,10 +2858,8 @@ __global__ __launch_bounds__(1024) void xs_sizing(const uint64_t* __restrict__ r
             xb[world + p] = (uint32_t)pb;
             pb += rows[(size_t)p * row_words + 6];
         }
-        atomicExch(ctr, 0u);
+        out[0] = s_max;
     }
-    __syncthreads();
-    if (tid == 0) out[0] = s_max;
 }
 
 // sharded rounds' buffers that depend only on the host count and the ranks (shd_relay_setup)
@@ -2860,8 +2876,7 @@ static shd_status relay_shard_alloc(shd_ctx* ctx) {
     const size_t out_bytes = (1 + (size_t)world * kXsHead + (size_t)world * world) * 8 + 64;
     SHD_TRY(R.xs_out.ensure(out_bytes));
     SHD_TRY(R.xs_pin.ensure(out_bytes));
-    SHD_TRY(R.xs_b.ensure((size_t)world * 8 + 64));   // xb[2 * world] + xs_sizing's done counter
-    SHD_HIP(hipMemsetAsync(R.xs_b.p, 0, (size_t)world * 8 + 64, ctx->stream));
+    SHD_TRY(R.xs_b.ensure((size_t)world * 8 + 64));
     SHD_TRY(R.x_off.ensure(((size_t)H + world) * 4));
     SHD_TRY(R.x_roff.ensure((size_t)world * (n_own + 1) * 4 + (size_t)(world + 1) * 4));
     SHD_TRY(R.m_off.ensure((n_own + 4) * 4));   // + the received statuses' word (bin_sort_v7<true>)
@@ -3054,7 +3069,7 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
     }
     uint64_t* rows = R.x_words.as<uint64_t>();
     uint64_t* agree = rows + (size_t)world * rw;
-    xs_row<<<1, 256, 0, s>>>(ran ? R.red.as<unsigned long long>() : nullptr,
+    xs_row<<<std::max<uint32_t>(1, div_up(n_bins, 256)), 256, 0, s>>>(ran ? R.red.as<unsigned long long>() : nullptr,
                              ran ? R.bin_base.as<uint32_t>() + n_bins + 1 : nullptr, n_bins, ran ? 1u : 0u,
                              (int32_t)st, R.x_cap, n, (ok7 && abs_seq) ? 0u : kXsHost, (int32_t)SHD_ERR_NO_HOST,
                              (int32_t)SHD_ERR_INVALID, rows + (size_t)me * rw);
@@ -3073,8 +3088,8 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
     //    to the communicator, as an RCCL failure is.
     shd_status st_post = SHD_OK;
     uint32_t* xb = R.xs_b.as<uint32_t>();
-    xs_sizing<<<world, 1024, 0, s>>>(rows, rw, n_bins, world, me, xsh.bpr, R.xs_sc.as<uint32_t>(),
-                                     R.xs_out.as<uint64_t>(), xb, xb + 2 * world);
+    xs_sizing<<<1, 1024, 0, s>>>(rows, rw, n_bins, world, me, xsh.bpr, R.xs_sc.as<uint32_t>(),
+                                 R.xs_out.as<uint64_t>(), xb);
     const size_t out_words = 1 + (size_t)world * kXsHead + (size_t)world * world;
     SHD_TRY(readback_into(ctx, s, R.xs_out.p, out_words * 8, R.xs_pin.as<unsigned long long>()));
     if (hipGetLastError() != hipSuccess) st_post = SHD_ERR_HIP;
@@ -3161,7 +3176,7 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
                  nullptr, rd->round_end};
         bin_sort_v7<true><<<nb, kB7Threads, 0, s>>>(n_own, nb, nullptr, R.x_rrec.as<uint4>(),
                                                     R.bin_lb.as<unsigned long long>(), R.m_off.as<uint32_t>(), vo,
-                                                    nullptr, 0u, xs);
+                                                    nullptr, ctx->knobs.get(K_B7_STOP, 0), xs);   // (stop: tuning only)
     } else {
         xs_fin_empty<<<1, 64, 0, s>>>(xs, R.m_off.as<uint32_t>());
     }
@@ -3172,7 +3187,9 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
     SHD_TRY(readback_into(ctx, s, R.m_off.as<uint32_t>() + (n_own & ~1u), 16, R.xs_pin.as<unsigned long long>()));
     const uint32_t n_ev = R.xs_pin.as<uint32_t>()[n_own & 1u];
     const shd_status agreed = (shd_status)R.xs_pin.as<uint32_t>()[(n_own & 1u) + 1];
-    if (agreed != SHD_OK) return agreed;   // every rank: nothing of the hosts' state is committed
+    // every rank: nothing of the hosts' state is committed (B7_STOP, tuning only: the bin sort
+    // stopped before writing the count and the status)
+    if (agreed != SHD_OK && ctx->knobs.get(K_B7_STOP, 0) == 0) return agreed;
     R.red_host[0] = hdr(me)[1];
     R.red_host[1] = hdr(me)[2];
     R.red_host[2] = hdr(me)[3];
@@ -3195,7 +3212,10 @@ static shd_status relay_round_sharded_v7(shd_ctx* ctx, const shd_batch* b, const
 }
 
 static shd_status relay_round_sharded(shd_ctx* ctx, const shd_batch* b, const shd_round* rd, shd_relay_out* d_out) {
-    if (ctx->knobs.on(K_RELAY_SHARD_X24)) return relay_round_sharded_x24(ctx, b, rd, d_out);
+    // (more hosts than the records' source bits: every rank has the same host count, so every
+    // rank takes the packing path without asking; xs_sizing's registers also assume it)
+    if (ctx->knobs.on(K_RELAY_SHARD_X24) || ctx->relay.n_hosts > kV7MaxHosts)
+        return relay_round_sharded_x24(ctx, b, rd, d_out);
     bool fallback = false;
     SHD_TRY(relay_round_sharded_v7(ctx, b, rd, d_out, &fallback));
     return fallback ? relay_round_sharded_x24(ctx, b, rd, d_out) : SHD_OK;

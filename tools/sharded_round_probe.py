@@ -6,7 +6,8 @@ the single context's; what the two-rank round costs beyond it is the exchange be
 all-to-all and its host sync, the 24-byte event packing, the exchange and the per-destination
 merge of the two senders' runs.  Prints ms per round for both (median of the timed rounds), and
 first the plain device round (shd_relay_round_device) on the same batch, the baseline of the
-sharded entry point's fixed cost.  Every timed round ends with a device synchronize.  Under
+sharded entry point's fixed cost (PROBE_RCCL=1: the world-1 leg over RCCL instead of the
+in-process communicator).  Every timed round ends with a device synchronize.  Under
 `rocprofv3 --kernel-trace --memory-copy-trace`, tools/r06_shard_trace.py splits the trace into
 the three legs' rounds and prints one round's phases.
 
@@ -64,7 +65,10 @@ def main():
 
     # ---- one context, the whole batch (the sharded entry point at world size 1)
     e1 = Engine(0)
-    D.comm_init_local([e1])
+    if os.environ.get("PROBE_RCCL"):   # the world-1 leg over RCCL (the transport of the driver's N > 1 runs)
+        D.comm_init_rccl(e1)
+    else:
+        D.comm_init_local([e1])
     one = D.ShardedRelay(e1, host_node, rng0, np.zeros(H, np.uint64), lat, loss)
     counters = int(os.environ.get("PROBE_COUNTERS", "0"))   # the bench's relay leg runs without them
     N.check(e1.lib.shd_relay_set_counters(e1.ctx, counters), "set_counters")
