@@ -375,7 +375,8 @@ void shd_host_free(void* p);
  *                        shd_comm_unique_id and the caller hands it to every rank (MPI, a file,
  *                        torch.distributed ...); collective over the ranks
  *   shd_comm_init_local  every rank in this process (one host thread per rank must then drive
- *                        each sharded call concurrently): device copies between the contexts
+ *                        each sharded call concurrently): device copies between the contexts,
+ *                        ordered by HIP events between their streams (no host stream syncs)
  *   shd_comm_init_host   ranks are processes the caller connects itself (MPI, gloo, sockets):
  *                        one all-to-all-v callback moves host bytes; the device bytes are staged
  *                        through pinned host memory around it (slower than RCCL: PCIe both ways)
