@@ -80,6 +80,28 @@ def test_flush_rounds_vs_c_oracle(engine, knob, n_threads, pinned, event_bytes, 
     assert np.array_equal(nid, onid)          # event ids advanced by the sent packets
 
 
+def test_flush_many_hosts_runs(engine):
+    """600k hosts with about one send each (a host has one run: the staging contract), so the scans
+    of the run counts and of the per-host counts span more than 64 tiles of 8192 -- the look-back's
+    second window (scan.h) -- and the round takes the radix pipeline (more hosts than pipeline 7's
+    2^18)."""
+    from shadow_amd import synth
+    from shadow_amd.relay import Relay
+    H, NN, P = 600_000, 200, 650_000
+    lat, loss, host_node, rng0 = _case(H, NN, 23)
+    rl = Relay(host_node, rng0, np.zeros(H, np.uint64), lat, loss, engine=engine)
+    start, ra = 10**9, 10**6
+    b = synth.packet_batch(H, P, start, start + ra, seed=71)
+    st = synth.stage_round(b, 4, start, seed=5)
+    assert sum(len(h) for h in st.run_host) > 64 * 8192
+    chance = (st.draw64 >> np.uint64(11)).astype(np.float64) * 2.0**-53
+    onid = np.zeros(H, np.uint64)
+    o = corc.relay_round(b.src_off, b.send_time, b.dst_host, b.payload, host_node, lat, loss, rng0.copy(),
+                         onid, start + ra, start + 100 * ra, 0, chance=chance)
+    fr = rl.flush(st.run_host, st.run_count, st.sends, start, start + ra, start + 100 * ra, 0)
+    _check(fr, o, st, np.zeros(H, np.uint64), start + ra)
+
+
 def test_flush_then_device_draws_round(engine):
     """A flush round (CPU draws) followed by a device-drawn round: ids carry over, the device
     streams start where they were."""
