@@ -2455,16 +2455,17 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
     if (P.narrow_arcs && (lds > ctx->max_lds || ctx->knobs.get(K_SSSP_GLOBAL, 0) == 1)) {
         // labels exceed the LDS: global-label kernel (C4)
         bool ovf = false;
-        // bucket width: 0.4 x mean_arc_lat, never below the smallest arc.  (mean_arc_lat is the
+        // bucket width: 0.52 x mean_arc_lat, never below the smallest arc.  (mean_arc_lat is the
         // edge latencies' sum over the arc count: half the mean edge latency of an undirected
-        // graph -- C4: 12.5 ms of 25 -- so this is 5 ms.)  Re-swept at the end of round 2 with
+        // graph -- C4: 12.5 ms of 25 -- so this is 6.5 ms.)  Re-swept at the end of round 2 with
         // the LDS labels and locality order: rows 0-4095 (tools/c4_delta_sweep.sh) 3 ms 20.2 ms,
         // 4 ms 19.4, 5 ms 19.1, 6 ms 19.0, 8 ms 19.3, 10 ms 20.0, 15 ms 22.2; full builds
         // alternated on one box (tools/c4_full_ab.sh) 4 ms 232.3, 5 ms 229.0 / 229.2, 6 ms 228.4 -
-        // 228.8, 7 ms 231.0, 10 ms 241.2 / 242.0
+        // 228.8, 7 ms 231.0, 10 ms 241.2 / 242.0.  Round 6 (tools/c4_full_ab.sh, alternated): 5 ms
+        // 194.2-194.4, 6.5 ms 193.0-193.2, 8 ms 194.8 -> 0.52 x mean_arc_lat
         uint32_t delta = kLat32Inf;
         if (algo == SHD_ALGO_DELTA)
-            delta = ctx->knobs.get(K_SSSP_DELTA, std::max(P.min_arc_lat, (uint32_t)(P.mean_arc_lat * 2ull / 5)));
+            delta = ctx->knobs.get(K_SSSP_DELTA, std::max(P.min_arc_lat, (uint32_t)(P.mean_arc_lat * 13ull / 25)));
         ArcView A{ctx->g_off.as<uint32_t>(), ctx->g_off.as<uint32_t>() + 1, ctx->g_arc16.as<uint4>(),
                   P.arcs};
         SHD_TRY(run_sssp_global(ctx, A, rb, re, d_lat, d_loss, delta, &ovf));
