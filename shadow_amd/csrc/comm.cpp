@@ -172,10 +172,10 @@ struct LocalComm final : Comm {
             }
             st = from(q, s);
             for (int k = 0; k < n_parts && st == SHD_OK; ++k) {
-                const size_t from = (size_t)q * per_rank + (size_t)rank * n_parts + k;   // q's part k to me
+                const size_t at = (size_t)q * per_rank + (size_t)rank * n_parts + k;   // q's part k to me
                 const size_t to = (size_t)q * n_parts + k;
-                if (g->bytes[from] != recv_bytes[to]) st = SHD_ERR_INVALID;
-                else st = copy(recv[to], g->ptr[from], g->device[q], recv_bytes[to], s);
+                if (g->bytes[at] != recv_bytes[to]) st = SHD_ERR_INVALID;
+                else st = copy(recv[to], g->ptr[at], g->device[q], recv_bytes[to], s);
             }
         }
         return leave(st, s);
