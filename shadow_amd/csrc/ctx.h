@@ -200,6 +200,7 @@ struct PreparedGraph {
     uint64_t arcs = 0, max_arc_lat = 0, pruned_arcs = 0, tight_arcs = 0;
     uint32_t mean_arc_lat = 1, min_arc_lat = 1;
     bool reordered = false;   // g_offr / g_usedr / g_arc8r / g_aqr hold the locality order
+    bool spread = false;      // g_offs / g_useds / g_arc16s hold the wave-spread order (LDS kernel)
     bool used_ident = false;  // used[j] == j for every node (the LDS kernels then skip that gather)
     uint32_t lds_labels = 0;  // how many of the first (highest-degree) nodes keep LDS labels
     std::vector<uint32_t> used, node_ids, es, ed;
@@ -274,7 +275,8 @@ struct shd_ctx {
     // routing scratch
     shd::DevBuf g_off, g_dst, g_lat, g_q, g_lat64, g_used, g_diag_lat, g_diag_loss, g_flags,
         g_dense, g_prune_dst, g_prune_cnt, g_labels, g_aux, g_arc16, g_arc8, g_aq, g_fw, g_glab, g_pred,
-        g_offr, g_usedr, g_arc8r, g_aqr;   // locality-ordered copies (global-label kernel)
+        g_offr, g_usedr, g_arc8r, g_aqr,   // locality-ordered copies (global-label kernel)
+        g_offs, g_useds, g_arc16s;         // wave-spread copies (1024-thread LDS kernel)
     uint32_t* nh_out = nullptr;   // next-hop rows of the running build (shd_routing_run_next_hops)
     // global-label slots left unlaunched while a sharded build's previous chunk is still being
     // exchanged on the side stream: the persistent kernel fills every CU's LDS, so RCCL's

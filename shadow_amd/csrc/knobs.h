@@ -15,7 +15,7 @@ namespace shd {
 #define SHD_KNOB_LIST(X)                                                                         \
     X(SSSP_NO_PAD) X(SSSP_LFLAT) X(SSSP_NO_OFFL) X(SSSP_G) X(SSSP_BLOCK) X(SSSP_NO_REORDER)      \
     X(SSSP_DYN) X(SSSP_FLAT) X(SSSP_NO_BKT) X(SSSP_WMIN) X(SSSP_SLOTS) X(SSSP_NO_LDS_LABELS)     \
-    X(SSSP_RESERVE) X(FW_TILE) X(PRUNE_K) X(SSSP_REORDER) X(REORDER_MODE) X(SSSP_GLOBAL)        \
+    X(SSSP_RESERVE) X(FW_TILE) X(PRUNE_K) X(SSSP_REORDER) X(REORDER_MODE) X(SSSP_NO_SPREAD) X(SSSP_GLOBAL)        \
     X(SSSP_NO_DELTA) X(SSSP_DELTA) X(SSSP_STATS) X(SPIN_WAIT)                                   \
     X(PRUNE_DENSE_BUILD) X(SSSP_HUB) X(SYNC_KERNEL)                                               \
     X(EQ_COUNT_BLOCKS) X(EQ_WAVE_MERGE) X(EQ_SEARCH_ONLY) X(EQ_MAX_RUNS) X(RELAY_GROUP_SENDS) X(HIST_SCALAR) X(B7_STOP) X(RELAY_FORCE_V1)         \

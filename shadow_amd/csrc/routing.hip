@@ -1596,6 +1596,7 @@ struct HostGraph {
 // (offsets, compact arcs, the used list); results are indexed by used position, so the table is
 // unchanged.  Next hops (lowest-index tie-break in GML order) run on the original numbering.
 static shd_status prepare_reordered(shd_ctx* ctx, const HostGraph& H, const uint32_t* used, uint32_t n_used);
+static shd_status prepare_spread(shd_ctx* ctx, const HostGraph& H, const uint32_t* used, uint32_t n_used);
 
 static uint32_t gml_id(const shd_graph* g, uint32_t idx) {
     return g->node_ids ? g->node_ids[idx] : idx;
@@ -1833,6 +1834,7 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
     hipStream_t s = ctx->stream;
     P.mode = mode;
     P.reordered = false;
+    P.spread = false;
     P.V = g->n_nodes;
     P.n_used = n_used;
     P.directed = g->directed != 0;
@@ -1883,6 +1885,7 @@ shd_status routing_prepare_impl(shd_ctx* ctx, const shd_graph* g, const uint32_t
             P.pruned_arcs = 0;
             P.tight_arcs = 0;
             SHD_TRY(prepare_reordered(ctx, H, used, n_used));
+            SHD_TRY(prepare_spread(ctx, H, used, n_used));
         }
     }
     SHD_HIP(hipStreamSynchronize(s));
@@ -1937,6 +1940,7 @@ struct ArcView {
     const uint4* arcs;
     uint64_t n_arcs;
     bool padded = false;   // lists padded to kArcPad slots with no-op arcs (prune_rows)
+    const uint32_t* used = nullptr;   // a relabelled copy (prepare_spread): the used nodes' new ids
 };
 
 template <int BLOCK, int G, bool CACHE>
@@ -1956,7 +1960,7 @@ static void launch_group(shd_ctx* ctx, const ArcView& A, uint32_t rb, uint32_t r
     auto* unreach = reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 16);
     auto* stats = ctx->stats_on ? reinterpret_cast<unsigned long long*>(ctx->g_flags.as<char>() + 32) : nullptr;
     hipEvent_t e0 = ctx->time_now ? ctx->ev[2] : nullptr, e1 = ctx->time_now ? ctx->ev[3] : nullptr;
-    const uint32_t* usedp = P.used_ident ? nullptr : (const uint32_t*)ctx->g_used.as<uint32_t>();
+    const uint32_t* usedp = A.used ? A.used : P.used_ident ? nullptr : (const uint32_t*)ctx->g_used.as<uint32_t>();
     if constexpr (kArcPad % (G * 8) == 0) {
         if (lat_guard) {
             hipExtLaunchKernelGGL(sssp_lds_group<BLOCK, G, R, CACHE, 8>, dim3(re - rb), dim3(BLOCK), (uint32_t)lds,
@@ -2346,6 +2350,79 @@ static shd_status prepare_reordered(shd_ctx* ctx, const HostGraph& H, const uint
     return SHD_OK;
 }
 
+// Wave-spread relabelling for the 1024-thread LDS kernel (sparse graphs whose labels fill the
+// LDS, C3).  Its bitmap word k belongs to wave k mod 16 for the whole build, so on a
+// preferential-attachment graph -- hubs are the first nodes -- the first waves own every hub and
+// the other waves wait for them at each sweep's barrier (24 % of the kernel).  The nodes are
+// dealt in descending degree order to the 16 waves' words (rank r -> wave r mod 16), and the
+// kernel runs on that copy of the CSR; the table is the same (labels are minima over paths, and
+// the used columns keep their order: used[j] -> its new id).  C3 DELTA 6.79 -> 6.59 ms, tables
+// identical (tools/c2_probe.py, SSSP_NO_SPREAD=1 alternated; a random relabelling: 7.05).  Not with next hops (the
+// kernel would write relabelled ids) nor a seed (indexed by the original ids).
+static shd_status prepare_spread(shd_ctx* ctx, const HostGraph& H, const uint32_t* used, uint32_t n_used) {
+    PreparedGraph& P = ctx->prep;
+    P.spread = false;
+    const uint32_t V = P.V;
+    constexpr uint32_t NW = 1024 / 64;
+    const bool dense = V <= kPruneMaxV && P.arcs * 8 >= (uint64_t)V * V;   // the prune path instead
+    if (V == 0 || dense || ctx->knobs.get(K_SSSP_NO_SPREAD, 0) == 1 ||
+        sssp_lds_bytes(V, 1024, false) > ctx->max_lds ||          // global labels (C4)
+        sssp_lds_bytes(V, 256, true) <= ctx->max_lds / 2)         // not the 1024-thread kernel
+        return SHD_OK;
+    hipStream_t s = ctx->stream;
+    std::vector<uint32_t> deg(V), r2n(V);
+    for (uint32_t v = 0; v < V; ++v) {
+        deg[v] = H.off[v + 1] - H.off[v];
+        r2n[v] = v;
+    }
+    std::stable_sort(r2n.begin(), r2n.end(), [&](uint32_t a, uint32_t b) { return deg[a] > deg[b]; });
+    // rank r -> position ((q / 32) * NW + r mod NW) * 32 + q mod 32 (q = r / NW: the rank's place
+    // among its wave's nodes), compacted to 0 .. V-1 in position order
+    std::vector<uint64_t> pos(V);
+    std::vector<uint32_t> byp(V);
+    for (uint32_t r = 0; r < V; ++r) {
+        const uint64_t q = r / NW;
+        pos[r] = ((q / 32) * NW + r % NW) * 32 + q % 32;
+        byp[r] = r;
+    }
+    std::stable_sort(byp.begin(), byp.end(), [&](uint32_t a, uint32_t b) { return pos[a] < pos[b]; });
+    std::vector<uint32_t> pi(V), ord(V);   // node -> new id, new id -> node
+    for (uint32_t i = 0; i < V; ++i) {
+        ord[i] = r2n[byp[i]];
+        pi[ord[i]] = i;
+    }
+    const size_t A = H.dst.size();
+    std::vector<uint32_t> offs(V + 1, 0), dsts(A), lats(A), useds(n_used);
+    std::vector<float> losss(A);
+    for (uint32_t i = 0; i < V; ++i) {
+        const uint32_t u = ord[i];
+        uint32_t at = offs[i];
+        for (uint32_t k = H.off[u]; k < H.off[u + 1]; ++k, ++at) {
+            dsts[at] = pi[H.dst[k]];
+            lats[at] = (uint32_t)H.lat[k];
+            losss[at] = H.loss[k];
+        }
+        offs[i + 1] = at;
+    }
+    for (uint32_t j = 0; j < n_used; ++j) useds[j] = pi[used[j]];
+    SHD_TRY(upload(ctx->g_offs, offs, s));
+    SHD_TRY(upload(ctx->g_useds, useds, s));
+    DevBuf d_dst, d_lat, d_loss, d_a8, d_q;
+    SHD_TRY(upload(d_dst, dsts, s));
+    SHD_TRY(upload(d_lat, lats, s));
+    SHD_TRY(upload(d_loss, losss, s));
+    SHD_TRY(ctx->g_arc16s.ensure(std::max<size_t>(A, 1) * 16));
+    SHD_TRY(d_a8.ensure(std::max<size_t>(A, 1) * 8));
+    SHD_TRY(d_q.ensure(std::max<size_t>(A, 1) * 4));
+    if (A)
+        arcs_pack<<<div_up(A, 256), 256, 0, s>>>(d_dst.as<uint32_t>(), d_lat.as<uint32_t>(), d_loss.as<float>(),
+                                                  ctx->g_arc16s.as<uint4>(), d_a8.as<uint2>(), d_q.as<float>(), A);
+    SHD_HIP(hipGetLastError());
+    SHD_HIP(hipStreamSynchronize(s));   // the temporaries are freed on return
+    P.spread = true;
+    return SHD_OK;
+}
+
 // the dominant kernel's device time, when this build was timed (shd_routing_set_timing)
 static float main_ms(shd_ctx* ctx) {
     // the read-back kernel (readback) can return before the runtime has seen the stop event
@@ -2414,6 +2491,10 @@ shd_status routing_run_impl(shd_ctx* ctx, uint32_t algo, uint32_t rb, uint32_t r
     if (lds_path) {
         ArcView A{ctx->g_off.as<uint32_t>(), ctx->g_off.as<uint32_t>() + 1, ctx->g_arc16.as<uint4>(),
                   P.arcs};
+        if (!prune && P.spread && !ctx->nh_out && ctx->knobs.get(K_SSSP_NO_SPREAD, 0) != 1) {   // prepare_spread
+            A = ArcView{ctx->g_offs.as<uint32_t>(), ctx->g_offs.as<uint32_t>() + 1, ctx->g_arc16s.as<uint4>(), P.arcs};
+            A.used = ctx->g_useds.as<uint32_t>();
+        }
         if (prune) {
             SHD_TRY(run_prune(ctx, &A));
             // the kept-arc count steers the lane-group width: counted once per prepared graph,

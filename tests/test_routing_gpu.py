@@ -158,6 +158,25 @@ def test_c3_rows_bit_exact(engine):
     del rows
 
 
+@pytest.mark.parametrize("spread", [1, 0])
+def test_c3_spread_order_used_subset(engine, knob, spread):
+    """The 1024-thread LDS kernel on its wave-spread relabelled CSR (prepare_spread, default for
+    C3-like graphs) against the C restatement, with a used set that is neither every node nor in
+    index order, so the relabelled ids of the used columns carry the table's column order."""
+    from shadow_amd import synth
+    el = synth.barabasi_albert(10_000, 3, 2)
+    used = np.random.default_rng(3).permutation(10_000)[:7_000].astype(np.uint32)
+    knob("SSSP_NO_SPREAD", 1 - spread)
+    g = engine_graph_from_edges(el)
+    for lo, hi in ((0, 64), (6_900, 7_000)):
+        code, lat, loss, _ = corc.routing(10_000, el.src, el.dst, el.latency_ns, el.packet_loss, False, used,
+                                          rows=(lo, hi))
+        assert code == "OK"
+        for algo in (0, 1):
+            t = g.compute_shortest_paths(used, engine, algo=algo, rows=(lo, hi))
+            _assert_table(t, lat, loss.view(np.uint32))
+
+
 def test_direct_paths_c2(engine):
     from shadow_amd import synth
     el = synth.complete_graph(300, 9)
